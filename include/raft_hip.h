@@ -1,0 +1,200 @@
+/*
+ * raft_hip.h — C-ABI of the MI355X-native RAFT inference path (libraft_hip.so).
+ *
+ * Plain pointers, sizes and a hipStream_t (passed as void*).  No allocation
+ * happens inside any entry point (callers own every buffer, including the
+ * workspaces whose sizes the *_workspace_floats queries return), nothing
+ * synchronises the host, so every call is legal inside hipStreamBeginCapture
+ * (hipGraph capture).  Every entry point returns 0 on success, a positive
+ * hipError_t from the launch, or a negative RAFT_E_* argument error; the
+ * message of the last failure on the calling thread is raft_hip_last_error().
+ *
+ * All device buffers are fp32.  "NHWC rows" means pixel-major rows of `ld`
+ * floats: element (pixel m, channel c) lives at ptr[m * ld + c], with pixel
+ * m = (b * H + y) * W + x.
+ *
+ * Reference interfaces replaced (paths relative to the reference root):
+ *   raft_alt_corr_forward   <- alt_cuda_corr.forward   (alt_cuda_corr/correlation.cpp:23-33,
+ *                                                      correlation_kernel.cu:260-286)
+ *   raft_alt_corr_backward  <- alt_cuda_corr.backward  (alt_cuda_corr/correlation.cpp:36-48,
+ *                                                      correlation_kernel.cu:288-324)
+ *   raft_corr_build         <- CorrBlock.__init__ + CorrBlock.corr (core/corr.py:25-54, 96-127)
+ *   raft_corr_lookup        <- CorrBlock.__call__ + bilinear_sampler (core/corr.py:56-94,
+ *                                                      core/utils/utils.py:57-71)
+ *   raft_conv2d             <- nn.Conv2d + fused activations / GRU gates of
+ *                              core/update.py:6-325 and core/extractor.py:6-267
+ *   raft_instnorm_*         <- nn.InstanceNorm2d in core/extractor.py (norm_fn='instance')
+ *   raft_convex_upsample    <- RAFT.upsample_flow (core/raft.py:112-142)
+ *   raft_upflow8            <- upflow8 (core/utils/utils.py:80-82)
+ *   raft_prep_images        <- RAFT.forward normalisation 2*(x/255)-1 (core/raft.py:164-169)
+ *   raft_avgpool2_nhwc      <- F.avg_pool2d(x, 2, stride=2) in AlternateCorrBlock (core/corr.py:157-161)
+ */
+#ifndef RAFT_HIP_H_
+#define RAFT_HIP_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RAFT_HIP_ABI_VERSION 1
+
+/* Negative return codes (argument errors, raised before any launch). */
+#define RAFT_E_INVALID (-1)   /* bad size / null pointer / unsupported shape */
+#define RAFT_E_ALIGN (-2)     /* pointer or leading dimension not aligned as required */
+
+typedef void* raft_stream_t;  /* hipStream_t; NULL = the legacy default stream */
+
+int raft_hip_abi_version(void);
+const char* raft_hip_arch(void);        /* offload arch the library was built for ("gfx950") */
+const char* raft_hip_last_error(void);  /* message of the last failure on this thread ("" if none) */
+
+/* ---------------------------------------------------------------------------
+ * All-pairs correlation pyramid (CorrBlock)
+ *
+ * fmap1, fmap2: NHWC rows [B*H*W][ld] (channels 0..C-1 used).
+ * pyramid: num_levels levels stored back to back; level l is
+ *   [B][H*W][H_l][W_l] with H_0 = H, H_{l+1} = floor(H_l / 2) (same for W),
+ *   i.e. for query pixel p of batch b the level-l map starts at
+ *   pyramid + off_l + (b*H*W + p) * H_l*W_l,  off_l = B*H*W * sum_{j<l} H_j*W_j.
+ * Level 0 = <fmap1[p], fmap2[q]> / sqrt_c (a division, as core/corr.py:127);
+ * level l+1 = 2x2 average pool (floor) of level l.
+ * --------------------------------------------------------------------------- */
+size_t raft_corr_pyramid_floats(int B, int H, int W, int num_levels);
+int raft_corr_build(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C,
+                    int num_levels, float sqrt_c, float* pyramid, raft_stream_t stream);
+
+/* Radius-r bilinear window lookup of every level (CorrBlock.__call__).
+ * coords: (x, y) per query pixel; coords_layout 0 = NHWC [B*H*W][2],
+ *         1 = NCHW [B][2][H][W] (the reference's tensor as it stands).
+ * out: out_layout 0 = NHWC rows [B*H*W][out_ld], channel lvl*(2r+1)^2 + ix*(2r+1) + iy;
+ *      out_layout 1 = NCHW [B][L*(2r+1)^2][H][W] (out_ld ignored).
+ * flow_out (optional, may be NULL): NHWC rows [B*H*W][flow_ld] receive
+ *      coords - coords_grid (the RAFT loop's `flow`, core/raft.py:222). */
+int raft_corr_lookup(const float* pyramid, int B, int H, int W, int num_levels, int radius,
+                     const float* coords, int coords_layout, float* out, int out_ld, int out_layout,
+                     float* flow_out, int flow_ld, raft_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * On-the-fly ("alternate") correlation — the alt_cuda_corr plugin.
+ *
+ * fmap1 [B][H1][W1][C], fmap2 [B][H2][W2][C] (NHWC, contiguous),
+ * coords [B][N][H1][W1][2] (x, y in fmap2 pixels).
+ * corr [B][N][(2r+1)^2][H1][W1], channel iy + (2r+1)*ix, every element
+ * written (no pre-zeroing needed), divided by `scale_div` (1.0f = the
+ * reference's unscaled output; sqrtf(C) = AlternateCorrBlock's / sqrt(dim),
+ * core/corr.py:198).
+ * --------------------------------------------------------------------------- */
+int raft_alt_corr_forward(const float* fmap1, const float* fmap2, const float* coords, float* corr,
+                          int B, int H1, int W1, int H2, int W2, int C, int N, int radius, float scale_div,
+                          raft_stream_t stream);
+
+/* Same computation, NHWC output: out rows [B*H1*W1][out_ld] at channel
+ * offset already applied by the caller; coords_layout as raft_corr_lookup
+ * (coordinates are divided by coord_div before use: 2**level in RAFT). */
+int raft_alt_corr_lookup_nhwc(const float* fmap1, const float* fmap2, const float* coords, int coords_layout,
+                              float coord_div, float* out, int out_ld, int B, int H1, int W1, int H2, int W2,
+                              int C, int radius, float scale_div, float* flow_out, int flow_ld,
+                              raft_stream_t stream);
+
+/* Gradients of raft_alt_corr_forward (unscaled), like correlation_kernel.cu:122-256:
+ * fmap1_grad is a deterministic gather; fmap2_grad is accumulated with float
+ * atomics (order-dependent in the last bits, as the reference); coords_grad is
+ * written with zeros, like the reference (correlation_kernel.cu:307 never fills it). */
+int raft_alt_corr_backward(const float* fmap1, const float* fmap2, const float* coords, const float* corr_grad,
+                           float* fmap1_grad, float* fmap2_grad, float* coords_grad,
+                           int B, int H1, int W1, int H2, int W2, int C, int N, int radius,
+                           float* workspace, size_t workspace_floats, raft_stream_t stream);
+size_t raft_alt_corr_backward_workspace_floats(int B, int H1, int W1, int H2, int W2, int C, int N, int radius);
+
+/* 2x2 / stride-2 average pool (floor), NHWC contiguous [B][H][W][C] -> [B][H/2][W/2][C]. */
+int raft_avgpool2_nhwc(const float* in, float* out, int B, int H, int W, int C, raft_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Convolution as implicit GEMM on fp32 MFMA (v_mfma_f32_32x32x2_f32), NHWC.
+ * M = batch*out_h*out_w pixels, N = out channels, K = taps x input channels.
+ * The input is a virtual concat of up to two NHWC row sources (seg 0, then
+ * seg 1), which is how torch.cat([...], dim=1) of the reference is elided.
+ *
+ * Packed weights (see raft_conv2d_packed_shape):
+ *   mode RAFT_CONV_VEC    (every segment's channel count % 4 == 0, seg0 % 32 == 0
+ *                          when seg 1 is used): w[n_pad][KH*KW][c_pad],
+ *                          c_pad = roundup(c0 + c1, 32), zero padded;
+ *   mode RAFT_CONV_GATHER (small inputs, e.g. 2- or 3-channel):
+ *                          w[n_pad][k_pad], k = (ky*KW + kx)*(c0+c1) + c,
+ *                          k_pad = roundup(KH*KW*(c0+c1), 32), zero padded;
+ *   n_pad = roundup(N, 64).
+ * --------------------------------------------------------------------------- */
+#define RAFT_CONV_VEC 0
+#define RAFT_CONV_GATHER 1
+
+/* epilogues: v = acc + bias[n] */
+#define RAFT_EPI_LINEAR 0         /* out = alpha * v                                          */
+#define RAFT_EPI_RELU 1           /* out = relu(v)                                            */
+#define RAFT_EPI_RESID_RELU 2     /* out = relu(aux0[m,n] + relu(v))    (ResidualBlock tail) */
+#define RAFT_EPI_GRU_ZR 3         /* n <  split: out[m,n] = sigmoid(v)               (z)      */
+                                  /* n >= split: out1[m,n-split] = sigmoid(v)*aux0[m,n-split] (r*h) */
+#define RAFT_EPI_GRU_Q 4          /* q = tanh(v); out[m,n] = (1-aux1[m,n])*aux0[m,n] + aux1[m,n]*q */
+#define RAFT_EPI_TANH_RELU 5      /* n < split: out[m,n] = tanh(v); else out1[m,n-split] = relu(v) */
+#define RAFT_EPI_ADD_TO_OUT 6     /* out[m,n] = out[m,n] + v   (coords1 += delta_flow)         */
+
+typedef struct raft_conv2d_params {
+  const float* in0; int in0_ld; int in0_c;  /* seg 0: NHWC rows, first channel at in0 */
+  const float* in1; int in1_ld; int in1_c;  /* seg 1 (in1_c = 0: unused) */
+  int batch, in_h, in_w;
+  int out_h, out_w;
+  int kh, kw, stride_h, stride_w, pad_h, pad_w;
+  int mode;                                 /* RAFT_CONV_VEC / RAFT_CONV_GATHER */
+  const float* weight;                      /* packed, see above */
+  const float* bias;                        /* [N] or NULL */
+  int n;                                    /* output channels N */
+  float* out; int out_ld;
+  int epilogue; float alpha; int split;
+  const float* aux0; int aux0_ld;
+  const float* aux1; int aux1_ld;
+  float* out1; int out1_ld;
+} raft_conv2d_params;
+
+/* Packed weight geometry for a conv (n_pad, k_pad in floats per row). */
+int raft_conv2d_packed_shape(int mode, int n, int kh, int kw, int cin, int* n_pad, int* k_pad);
+int raft_conv2d(const raft_conv2d_params* p, raft_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * InstanceNorm2d (affine=False, eps): statistics per (image, channel) over
+ * the image's hw pixels; stats[(b*C + c)*2 + {0,1}] = {mean, 1/sqrt(var+eps)}.
+ * --------------------------------------------------------------------------- */
+size_t raft_instnorm_workspace_floats(int B, int HW, int C);
+int raft_instnorm_stats(const float* x, int ld, int B, int HW, int C, float eps, float* stats,
+                        float* workspace, raft_stream_t stream);
+/* out = act( norm(x) + resid ) where resid = 0 (resid NULL), raw resid rows, or
+ * norm(resid) with its own stats (resid_stats != NULL); relu_mode: 0 none, 1 relu(norm(x)),
+ * 2 relu(resid + relu(norm(x)))  (ResidualBlock tail). */
+int raft_instnorm_apply(const float* x, int ld, const float* stats, const float* resid, int resid_ld,
+                        const float* resid_stats, int relu_mode, float* out, int out_ld,
+                        int B, int HW, int C, raft_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Small elementwise / layout kernels of RAFT.forward
+ * --------------------------------------------------------------------------- */
+/* images NCHW [B][3][H][W] in 0..255 -> NHWC rows [2B*H*W][3]: img1 batch then img2, 2*(x/255)-1 */
+int raft_prep_images(const float* img1, const float* img2, float* out, int B, int H, int W,
+                     raft_stream_t stream);
+/* coords NHWC [B*H*W][2] = coords_grid (+ flow_init NCHW [B][2][H][W] if not NULL) */
+int raft_init_coords(float* coords, const float* flow_init, int B, int H, int W, raft_stream_t stream);
+/* flow_low NCHW [B][2][H][W] = coords - coords_grid */
+int raft_flow_from_coords(const float* coords, float* flow, int B, int H, int W, raft_stream_t stream);
+/* convex upsample of flow = coords - grid with mask rows [B*H*W][mask_ld] (576 used)
+ * -> NCHW [B][2][8H][8W] */
+int raft_convex_upsample(const float* coords, const float* mask, int mask_ld, float* flow_up,
+                         int B, int H, int W, raft_stream_t stream);
+/* 8 * bilinear(align_corners=True) x8 upsample of flow = coords - grid -> NCHW [B][2][8H][8W] */
+int raft_upflow8(const float* coords, float* flow_up, int B, int H, int W, raft_stream_t stream);
+/* NCHW [B][C][H][W] <-> NHWC rows [B*H*W][ld] */
+int raft_nchw_to_nhwc(const float* in, float* out, int out_ld, int B, int C, int H, int W, raft_stream_t stream);
+int raft_nhwc_to_nchw(const float* in, int in_ld, float* out, int B, int C, int H, int W, raft_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RAFT_HIP_H_ */

@@ -1,0 +1,128 @@
+"""ctypes binding of libraft_hip.so (the C-ABI declared in include/raft_hip.h).
+
+The library is built in-tree by `python __graft_entry__.py build` (or
+`make -C raft_optical_flow_amd/csrc`).  There is no fallback: if the library
+is missing or fails to load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("RAFT_HIP_LIB", os.path.join(_HERE, "libraft_hip.so"))
+
+c_int = ctypes.c_int
+c_float = ctypes.c_float
+c_size_t = ctypes.c_size_t
+c_void_p = ctypes.c_void_p
+c_char_p = ctypes.c_char_p
+P = c_void_p  # device pointers are passed as integers / void*
+
+RAFT_CONV_VEC = 0
+RAFT_CONV_GATHER = 1
+
+EPI_LINEAR = 0
+EPI_RELU = 1
+EPI_RESID_RELU = 2
+EPI_GRU_ZR = 3
+EPI_GRU_Q = 4
+EPI_TANH_RELU = 5
+EPI_ADD_TO_OUT = 6
+
+
+class ConvParams(ctypes.Structure):
+    """Mirror of `raft_conv2d_params` (include/raft_hip.h)."""
+
+    _fields_ = [
+        ("in0", P), ("in0_ld", c_int), ("in0_c", c_int),
+        ("in1", P), ("in1_ld", c_int), ("in1_c", c_int),
+        ("batch", c_int), ("in_h", c_int), ("in_w", c_int),
+        ("out_h", c_int), ("out_w", c_int),
+        ("kh", c_int), ("kw", c_int), ("stride_h", c_int), ("stride_w", c_int), ("pad_h", c_int), ("pad_w", c_int),
+        ("mode", c_int),
+        ("weight", P), ("bias", P),
+        ("n", c_int),
+        ("out", P), ("out_ld", c_int),
+        ("epilogue", c_int), ("alpha", c_float), ("split", c_int),
+        ("aux0", P), ("aux0_ld", c_int),
+        ("aux1", P), ("aux1_ld", c_int),
+        ("out1", P), ("out1_ld", c_int),
+    ]
+
+
+# name -> (restype, argtypes)
+_PROTOS = {
+    "raft_hip_abi_version": (c_int, []),
+    "raft_hip_arch": (c_char_p, []),
+    "raft_hip_last_error": (c_char_p, []),
+    "raft_corr_pyramid_floats": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "raft_corr_build": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, P, P]),
+    "raft_corr_lookup": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, c_int, c_int, P, c_int, P]),
+    "raft_alt_corr_forward": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, P]),
+    "raft_alt_corr_lookup_nhwc": (c_int, [P, P, P, c_int, c_float, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                          c_int, c_float, P, c_int, P]),
+    "raft_alt_corr_backward": (c_int, [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                       P, c_size_t, P]),
+    "raft_alt_corr_backward_workspace_floats": (c_size_t, [c_int] * 8),
+    "raft_avgpool2_nhwc": (c_int, [P, P, c_int, c_int, c_int, c_int, P]),
+    "raft_conv2d_packed_shape": (c_int, [c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int),
+                                         ctypes.POINTER(c_int)]),
+    "raft_conv2d": (c_int, [ctypes.POINTER(ConvParams), P]),
+    "raft_instnorm_workspace_floats": (c_size_t, [c_int, c_int, c_int]),
+    "raft_instnorm_stats": (c_int, [P, c_int, c_int, c_int, c_int, c_float, P, P, P]),
+    "raft_instnorm_apply": (c_int, [P, c_int, P, P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, P]),
+    "raft_prep_images": (c_int, [P, P, P, c_int, c_int, c_int, P]),
+    "raft_init_coords": (c_int, [P, P, c_int, c_int, c_int, P]),
+    "raft_flow_from_coords": (c_int, [P, P, c_int, c_int, c_int, P]),
+    "raft_convex_upsample": (c_int, [P, P, c_int, P, c_int, c_int, c_int, P]),
+    "raft_upflow8": (c_int, [P, P, c_int, c_int, c_int, P]),
+    "raft_nchw_to_nhwc": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),
+    "raft_nhwc_to_nchw": (c_int, [P, c_int, P, c_int, c_int, c_int, c_int, P]),
+}
+
+EXPORTED = tuple(_PROTOS)
+
+_lib = None
+_lock = threading.Lock()
+
+
+class RaftHipError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libraft_hip.so (once).  Raises RaftHipError if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RaftHipError(
+                f"libraft_hip.so not found at {LIB_PATH}: build it with `python __graft_entry__.py build` "
+                "(there is no CPU fallback)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _PROTOS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.raft_hip_abi_version() != 1:
+            raise RaftHipError("libraft_hip.so ABI version mismatch")
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = _lib.raft_hip_last_error().decode(errors="replace") if _lib is not None else ""
+        raise RaftHipError(f"{what} failed (rc={rc}): {msg}")
+
+
+def call(name: str, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    check(rc, name)
+    return rc

@@ -1,0 +1,347 @@
+// Elementwise / reduction kernels of the RAFT inference path (gfx950):
+// image normalisation, InstanceNorm, coordinate state, convex upsampling.
+#include "common.hpp"
+
+namespace raft {
+
+char* last_error_buf() {
+  static thread_local char buf[512] = {0};
+  return buf;
+}
+
+namespace {
+
+int grid_for(long n, int block = 256) {
+  long g = (n + block - 1) / block;
+  if (g > 65536) g = 65536;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+#define GRID_STRIDE(i, total) \
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < (total); i += (long)gridDim.x * blockDim.x)
+
+// core/raft.py:164-169: 2 * (image / 255.0) - 1.0, NCHW -> NHWC, img1 batch then img2
+__global__ void prep_images_kernel(const float* img1, const float* img2, float* out, int B, int H, int W) {
+  const long HW = (long)H * W;
+  const long total = 2L * B * HW * 3;
+  GRID_STRIDE(i, total) {
+    const int c = i % 3;
+    const long pix = i / 3;  // (bb*H + y)*W + x
+    const int bb = (int)(pix / HW);
+    const long yx = pix - (long)bb * HW;
+    const float* src = bb < B ? img1 + ((long)bb * 3 + c) * HW : img2 + ((long)(bb - B) * 3 + c) * HW;
+    out[i] = 2.0f * (src[yx] / 255.0f) - 1.0f;
+  }
+}
+
+// core/raft.py:89-110 + :208-209: coords1 = coords_grid (+ flow_init)
+__global__ void init_coords_kernel(float* coords, const float* flow_init, int B, int H, int W) {
+  const long P = (long)H * W;
+  const long total = (long)B * P * 2;
+  GRID_STRIDE(i, total) {
+    const int c = i & 1;
+    const long pix = i >> 1;
+    const int b = (int)(pix / P);
+    const long p = pix - (long)b * P;
+    float v = c == 0 ? (float)(p % W) : (float)(p / W);
+    if (flow_init) v = v + flow_init[((long)b * 2 + c) * P + p];
+    coords[i] = v;
+  }
+}
+
+// flow = coords1 - coords0, NCHW
+__global__ void flow_from_coords_kernel(const float* coords, float* flow, int B, int H, int W) {
+  const long P = (long)H * W;
+  const long total = (long)B * 2 * P;
+  GRID_STRIDE(i, total) {
+    const long p = i % P;
+    const long t = i / P;
+    const int c = (int)(t % 2);
+    const int b = (int)(t / 2);
+    const float g = c == 0 ? (float)(p % W) : (float)(p / W);
+    flow[i] = coords[((long)b * P + p) * 2 + c] - g;
+  }
+}
+
+// RAFT.upsample_flow (core/raft.py:112-142).  One thread per output pixel
+// (8h+a, 8w+b): softmax over the 9 mask logits k*64 + a*8 + b, weighted sum of
+// 8*flow over the zero-padded 3x3 neighbourhood (k = ky*3 + kx).
+__global__ void convex_upsample_kernel(const float* coords, const float* mask, int mask_ld, float* out, int B, int H,
+                                       int W) {
+  const int H8 = 8 * H, W8 = 8 * W;
+  const long P8 = (long)H8 * W8;
+  const long total = (long)B * P8;
+  GRID_STRIDE(i, total) {
+    const int X = i % W8;
+    const long t = i / W8;
+    const int Y = t % H8;
+    const int b = (int)(t / H8);
+    const int h = Y >> 3, a = Y & 7, w = X >> 3, bb = X & 7;
+    const float* m = mask + ((long)b * H * W + (long)h * W + w) * mask_ld + a * 8 + bb;
+    float lg[9];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      lg[k] = m[k * 64];
+      mx = fmaxf(mx, lg[k]);
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      lg[k] = expf(lg[k] - mx);
+      sum += lg[k];
+    }
+    float fx = 0.f, fy = 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int yy = h + k / 3 - 1, xx = w + k % 3 - 1;
+      float vx = 0.f, vy = 0.f;
+      if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+        const float* c = coords + ((long)b * H * W + (long)yy * W + xx) * 2;
+        vx = 8.0f * (c[0] - (float)xx);
+        vy = 8.0f * (c[1] - (float)yy);
+      }
+      const float wk = lg[k] / sum;
+      fx += wk * vx;
+      fy += wk * vy;
+    }
+    out[((long)b * 2) * P8 + (long)Y * W8 + X] = fx;
+    out[((long)b * 2 + 1) * P8 + (long)Y * W8 + X] = fy;
+  }
+}
+
+// upflow8 (core/utils/utils.py:80-82): 8 * bilinear(align_corners=True)
+__global__ void upflow8_kernel(const float* coords, float* out, int B, int H, int W) {
+  const int H8 = 8 * H, W8 = 8 * W;
+  const long P8 = (long)H8 * W8;
+  const float sy = H8 > 1 ? (float)(H - 1) / (float)(H8 - 1) : 0.f;
+  const float sx = W8 > 1 ? (float)(W - 1) / (float)(W8 - 1) : 0.f;
+  const long total = (long)B * 2 * P8;
+  GRID_STRIDE(i, total) {
+    const int X = i % W8;
+    long t = i / W8;
+    const int Y = t % H8;
+    t /= H8;
+    const int c = (int)(t % 2);
+    const int b = (int)(t / 2);
+    const float ry = sy * Y, rx = sx * X;
+    const int y0 = min((int)ry, H - 1), x0 = min((int)rx, W - 1);
+    const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
+    const float ly = ry - y0, lx = rx - x0;
+    auto f = [&](int yy, int xx) {
+      return coords[((long)b * H * W + (long)yy * W + xx) * 2 + c] - (c == 0 ? (float)xx : (float)yy);
+    };
+    const float v = (1.f - ly) * ((1.f - lx) * f(y0, x0) + lx * f(y0, x1)) + ly * ((1.f - lx) * f(y1, x0) + lx * f(y1, x1));
+    out[i] = 8.0f * v;
+  }
+}
+
+__global__ void nchw_to_nhwc_kernel(const float* in, float* out, int ld, int B, int C, int H, int W) {
+  const long P = (long)H * W;
+  const long total = (long)B * P * C;
+  GRID_STRIDE(i, total) {
+    const int c = i % C;
+    const long pix = i / C;
+    const int b = (int)(pix / P);
+    const long p = pix - (long)b * P;
+    out[pix * ld + c] = in[((long)b * C + c) * P + p];
+  }
+}
+
+__global__ void nhwc_to_nchw_kernel(const float* in, int ld, float* out, int B, int C, int H, int W) {
+  const long P = (long)H * W;
+  const long total = (long)B * C * P;
+  GRID_STRIDE(i, total) {
+    const long p = i % P;
+    const long t = i / P;
+    const int c = (int)(t % C);
+    const int b = (int)(t / C);
+    out[i] = in[((long)b * P + p) * ld + c];
+  }
+}
+
+// InstanceNorm statistics, stage 1: per (image, pixel chunk) partial sums of
+// (x - shift[c]) and (x - shift[c])^2 with shift = the image's first pixel
+// (shifted data keeps E[x^2] - E[x]^2 well conditioned).
+constexpr int IN_CHUNK = 2048;
+
+__global__ __launch_bounds__(256) void instnorm_partial_kernel(const float* x, int ld, int HW, int C, float* part) {
+  __shared__ float red[2][256];
+  const int b = blockIdx.y, chunk = blockIdx.x;
+  const int nchunk = gridDim.x;
+  const int p0 = chunk * IN_CHUNK, p1 = min(HW, p0 + IN_CHUNK);
+  const float* xb = x + (long)b * HW * ld;
+  for (int cg = 0; cg < C; cg += 256) {
+    const int ce = min(256, C - cg);
+    const int R = 256 / ce;
+    const int c = cg + threadIdx.x % ce, r = threadIdx.x / ce;
+    float s = 0.f, ss = 0.f;
+    if (r < R) {
+      const float shift = xb[c];
+      for (int p = p0 + r; p < p1; p += R) {
+        const float d = xb[(long)p * ld + c] - shift;
+        s += d;
+        ss += d * d;
+      }
+    }
+    red[0][threadIdx.x] = s;
+    red[1][threadIdx.x] = ss;
+    __syncthreads();
+    if (threadIdx.x < ce) {
+      float S = 0.f, SS = 0.f;
+      for (int k = 0; k < R; ++k) {
+        S += red[0][k * ce + threadIdx.x];
+        SS += red[1][k * ce + threadIdx.x];
+      }
+      float* o = part + (((long)b * nchunk + chunk) * C + cg + threadIdx.x) * 2;
+      o[0] = S;
+      o[1] = SS;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void instnorm_finalize_kernel(const float* x, int ld, int HW, int C, int nchunk, const float* part,
+                                         float eps, float* stats, int B) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * C) return;
+  const int b = i / C, c = i - b * C;
+  double S = 0.0, SS = 0.0;
+  for (int k = 0; k < nchunk; ++k) {
+    const float* o = part + (((long)b * nchunk + k) * C + c) * 2;
+    S += o[0];
+    SS += o[1];
+  }
+  const double n = (double)HW;
+  const double md = S / n;
+  double var = SS / n - md * md;
+  if (var < 0) var = 0;
+  const double shift = x[(long)b * HW * ld + c];
+  stats[2 * i] = (float)(shift + md);
+  stats[2 * i + 1] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+__global__ void instnorm_apply_kernel(const float* x, int ld, const float* stats, const float* resid, int rld,
+                                      const float* rstats, int mode, float* out, int old, int B, int HW, int C) {
+  const long total = (long)B * HW * C;
+  GRID_STRIDE(i, total) {
+    const int c = i % C;
+    const long pix = i / C;
+    const int b = (int)(pix / HW);
+    const float* st = stats + 2 * ((long)b * C + c);
+    float v = (x[pix * ld + c] - st[0]) * st[1];
+    if (mode >= 1) v = fmaxf(v, 0.f);
+    if (resid) {
+      float r = resid[pix * rld + c];
+      if (rstats) {
+        const float* rs = rstats + 2 * ((long)b * C + c);
+        r = (r - rs[0]) * rs[1];
+      }
+      v = r + v;
+      if (mode == 2) v = fmaxf(v, 0.f);
+    }
+    out[pix * old + c] = v;
+  }
+}
+
+}  // namespace
+}  // namespace raft
+
+using namespace raft;
+
+extern "C" int raft_hip_abi_version(void) { return RAFT_HIP_ABI_VERSION; }
+extern "C" const char* raft_hip_arch(void) { return "gfx950"; }
+extern "C" const char* raft_hip_last_error(void) { return last_error_buf(); }
+
+extern "C" int raft_prep_images(const float* img1, const float* img2, float* out, int B, int H, int W,
+                                raft_stream_t stream) {
+  RAFT_REQUIRE(img1 && img2 && out && B > 0 && H > 0 && W > 0, "raft_prep_images: bad arguments");
+  const long n = 2L * B * H * W * 3;
+  hipLaunchKernelGGL(prep_images_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), img1, img2, out, B, H,
+                     W);
+  return check_launch("raft_prep_images");
+}
+
+extern "C" int raft_init_coords(float* coords, const float* flow_init, int B, int H, int W, raft_stream_t stream) {
+  RAFT_REQUIRE(coords && B > 0 && H > 0 && W > 0, "raft_init_coords: bad arguments");
+  const long n = (long)B * H * W * 2;
+  hipLaunchKernelGGL(init_coords_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), coords, flow_init, B, H,
+                     W);
+  return check_launch("raft_init_coords");
+}
+
+extern "C" int raft_flow_from_coords(const float* coords, float* flow, int B, int H, int W, raft_stream_t stream) {
+  RAFT_REQUIRE(coords && flow && B > 0 && H > 0 && W > 0, "raft_flow_from_coords: bad arguments");
+  const long n = (long)B * H * W * 2;
+  hipLaunchKernelGGL(flow_from_coords_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), coords, flow, B, H,
+                     W);
+  return check_launch("raft_flow_from_coords");
+}
+
+extern "C" int raft_convex_upsample(const float* coords, const float* mask, int mask_ld, float* flow_up, int B, int H,
+                                    int W, raft_stream_t stream) {
+  RAFT_REQUIRE(coords && mask && flow_up && B > 0 && H > 0 && W > 0, "raft_convex_upsample: bad arguments");
+  RAFT_REQUIRE(mask_ld >= 576, "raft_convex_upsample: mask_ld must be >= 576");
+  const long n = (long)B * 64 * H * W;
+  hipLaunchKernelGGL(convex_upsample_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), coords, mask,
+                     mask_ld, flow_up, B, H, W);
+  return check_launch("raft_convex_upsample");
+}
+
+extern "C" int raft_upflow8(const float* coords, float* flow_up, int B, int H, int W, raft_stream_t stream) {
+  RAFT_REQUIRE(coords && flow_up && B > 0 && H > 0 && W > 0, "raft_upflow8: bad arguments");
+  const long n = (long)B * 2 * 64 * H * W;
+  hipLaunchKernelGGL(upflow8_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), coords, flow_up, B, H, W);
+  return check_launch("raft_upflow8");
+}
+
+extern "C" int raft_nchw_to_nhwc(const float* in, float* out, int out_ld, int B, int C, int H, int W,
+                                 raft_stream_t stream) {
+  RAFT_REQUIRE(in && out && B > 0 && C > 0 && H > 0 && W > 0 && out_ld >= C, "raft_nchw_to_nhwc: bad arguments");
+  const long n = (long)B * C * H * W;
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), in, out, out_ld, B, C,
+                     H, W);
+  return check_launch("raft_nchw_to_nhwc");
+}
+
+extern "C" int raft_nhwc_to_nchw(const float* in, int in_ld, float* out, int B, int C, int H, int W,
+                                 raft_stream_t stream) {
+  RAFT_REQUIRE(in && out && B > 0 && C > 0 && H > 0 && W > 0 && in_ld >= C, "raft_nhwc_to_nchw: bad arguments");
+  const long n = (long)B * C * H * W;
+  hipLaunchKernelGGL(nhwc_to_nchw_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), in, in_ld, out, B, C,
+                     H, W);
+  return check_launch("raft_nhwc_to_nchw");
+}
+
+extern "C" size_t raft_instnorm_workspace_floats(int B, int HW, int C) {
+  if (B <= 0 || HW <= 0 || C <= 0) return 0;
+  const long nchunk = cdiv_l(HW, IN_CHUNK);
+  return (size_t)B * nchunk * C * 2;
+}
+
+extern "C" int raft_instnorm_stats(const float* x, int ld, int B, int HW, int C, float eps, float* stats,
+                                   float* workspace, raft_stream_t stream) {
+  RAFT_REQUIRE(x && stats && workspace && B > 0 && HW > 0 && C > 0 && ld >= C, "raft_instnorm_stats: bad arguments");
+  const int nchunk = (int)cdiv_l(HW, IN_CHUNK);
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(instnorm_partial_kernel, dim3(nchunk, B), dim3(256), 0, s, x, ld, HW, C, workspace);
+  int rc = check_launch("raft_instnorm_stats(partial)");
+  if (rc) return rc;
+  hipLaunchKernelGGL(instnorm_finalize_kernel, dim3(cdiv(B * C, 256)), dim3(256), 0, s, x, ld, HW, C, nchunk,
+                     workspace, eps, stats, B);
+  return check_launch("raft_instnorm_stats(finalize)");
+}
+
+extern "C" int raft_instnorm_apply(const float* x, int ld, const float* stats, const float* resid, int resid_ld,
+                                   const float* resid_stats, int relu_mode, float* out, int out_ld, int B, int HW,
+                                   int C, raft_stream_t stream) {
+  RAFT_REQUIRE(x && stats && out && B > 0 && HW > 0 && C > 0 && ld >= C && out_ld >= C,
+               "raft_instnorm_apply: bad arguments");
+  RAFT_REQUIRE(relu_mode >= 0 && relu_mode <= 2, "raft_instnorm_apply: bad relu_mode");
+  RAFT_REQUIRE(!resid || resid_ld >= C, "raft_instnorm_apply: bad resid_ld");
+  const long n = (long)B * HW * C;
+  hipLaunchKernelGGL(instnorm_apply_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, ld, stats, resid,
+                     resid_ld, resid_stats, relu_mode, out, out_ld, B, HW, C);
+  return check_launch("raft_instnorm_apply");
+}

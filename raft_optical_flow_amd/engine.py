@@ -1,0 +1,474 @@
+"""Execution plans for the RAFT inference path on MI355X.
+
+A plan is built once per (model weights, batch, image size, iters, mode): it
+allocates every device buffer up front (NHWC row buffers, correlation
+pyramid, recurrent state) and records the exact sequence of C-ABI kernel
+launches with their fixed pointers.  `RaftPlan.run()` replays the launch list
+on the current stream; `RaftPlan.capture()` records it into a hipGraph
+(torch.cuda.CUDAGraph on ROCm) so the 32-iteration refinement loop replays
+with no host work per kernel.
+
+Buffer layout of the recurrent state (P = B * H/8 * W/8 rows), RAFT-full:
+  HX   [P, 384]  = h (128) | inp (128) | motion conv (126) | flow (2)
+                 -> hx = cat[h, x] of core/update.py:106 without a copy,
+                    x = cat[inp, motion, flow] of core/update.py:318
+  CORR [P, 324]  lookup output, channel lvl*81 + ix*9 + iy
+  COR1 [P, 256], CF [P, 256] = cor (192) | flo (64), FLO1 [P, 128]
+  Z, RH [P, 128] GRU gate z and r*h
+  FH   [P, 512]  flow-head conv1 (256) | mask conv1 (256), one fused GEMM
+  MASK [P, 576], coords1 [P, 2]
+RAFT-small uses the same scheme with hdim 96 / cdim 64 (HX ld 244, two zero
+pad channels keep every row 16-byte aligned).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from . import kernels as K
+from .kernels import Launch, PackedConv, Rows, conv_launch, conv_params, pack_conv, fold_bn
+
+# ----------------------------------------------------------------------------
+# Weight packing
+# ----------------------------------------------------------------------------
+
+
+def _conv_bn(conv, bn, device, **kw):
+    if bn is None:
+        return pack_conv(conv.weight, conv.bias, conv.stride, conv.padding, device=device, **kw)
+    w, b = fold_bn(conv.weight, conv.bias, bn)
+    return pack_conv(w, b, conv.stride, conv.padding, device=device, **kw)
+
+
+class PackedEncoder:
+    """BasicEncoder (core/extractor.py:118-192) / SmallEncoder (:195-267) weights, packed."""
+
+    def __init__(self, enc, device):
+        self.norm = enc.norm_fn
+        if self.norm not in ("instance", "batch", "none"):
+            raise NotImplementedError(f"norm_fn={self.norm!r} is not on the RAFT inference path")
+        self.small = enc.__class__.__name__ == "SmallEncoder"
+        bn = (lambda m: m) if self.norm == "batch" else (lambda m: None)
+        self.stem = _conv_bn(enc.conv1, bn(enc.norm1), device, mode=_lib.RAFT_CONV_GATHER)
+        self.blocks = []
+        for layer in (enc.layer1, enc.layer2, enc.layer3):
+            for blk in layer:
+                d = {"stride": blk.conv1.stride[0] if not self.small else blk.conv2.stride[0]}
+                d["conv1"] = _conv_bn(blk.conv1, bn(blk.norm1), device)
+                d["conv2"] = _conv_bn(blk.conv2, bn(blk.norm2), device)
+                if self.small:
+                    d["conv3"] = _conv_bn(blk.conv3, bn(blk.norm3), device)
+                    dsn = getattr(blk, "norm4", None)
+                else:
+                    dsn = getattr(blk, "norm3", None)
+                d["ds"] = None if blk.downsample is None else _conv_bn(blk.downsample[0], bn(dsn), device)
+                d["planes"] = d["conv3" if self.small else "conv2"].n
+                self.blocks.append(d)
+        self.head = pack_conv(enc.conv2.weight, enc.conv2.bias, 1, 0, device=device)
+
+
+class PackedUpdate:
+    """BasicUpdateBlock (core/update.py:265-325) / SmallUpdateBlock (:218-263) weights, packed,
+    with the z/r gates of each GRU step fused into one GEMM and, for the basic
+    block, the flow-head and mask-head first convs fused into one GEMM."""
+
+    def __init__(self, ub, small, device):
+        e, g, fh = ub.encoder, ub.gru, ub.flow_head
+        self.small = small
+        if small:
+            hd, cd = 96, 64
+            self.hdim, self.cdim, self.ld = hd, cd, 244
+            x_real, x_decl = 146, 148
+            self.convc1 = pack_conv(e.convc1.weight, e.convc1.bias, 1, 0, device=device)
+            self.convc2 = None
+            self.convf1 = pack_conv(e.convf1.weight, e.convf1.bias, 1, 3, device=device, mode=_lib.RAFT_CONV_GATHER)
+            self.convf2 = pack_conv(e.convf2.weight, e.convf2.bias, 1, 1, device=device)
+            self.conv = pack_conv(e.conv.weight, e.conv.bias, 1, 1, device=device)
+            steps = [(g.convz, g.convr, g.convq, 1)]
+        else:
+            hd, cd = 128, 128
+            self.hdim, self.cdim, self.ld = hd, cd, 384
+            x_real, x_decl = 256, 256
+            self.convc1 = pack_conv(e.convc1.weight, e.convc1.bias, 1, 0, device=device)
+            self.convc2 = pack_conv(e.convc2.weight, e.convc2.bias, 1, 1, device=device)
+            self.convf1 = pack_conv(e.convf1.weight, e.convf1.bias, 1, 3, device=device, mode=_lib.RAFT_CONV_GATHER)
+            self.convf2 = pack_conv(e.convf2.weight, e.convf2.bias, 1, 1, device=device)
+            self.conv = pack_conv(e.conv.weight, e.conv.bias, 1, 1, device=device)
+            steps = [(g.convz1, g.convr1, g.convq1, 1), (g.convz2, g.convr2, g.convq2, 1)]
+        self.gru = []
+        for cz, cr, cq, _ in steps:
+            wzr = torch.cat([cz.weight, cr.weight], 0)
+            bzr = torch.cat([cz.bias, cr.bias], 0)
+            zr = pack_conv(wzr, bzr, 1, cz.padding, seg_real=[hd + x_real], seg_decl=[hd + x_decl], device=device)
+            q = pack_conv(cq.weight, cq.bias, 1, cq.padding, seg_real=[hd, x_real], seg_decl=[hd, x_decl],
+                          device=device)
+            self.gru.append((zr, q))
+        self.fh1 = pack_conv(fh.conv1.weight, fh.conv1.bias, 1, 1, device=device)
+        self.fh2 = pack_conv(fh.conv2.weight, fh.conv2.bias, 1, 1, device=device)
+        if not small:
+            m0, m2 = ub.mask[0], ub.mask[2]
+            self.fh1_mask = pack_conv(torch.cat([fh.conv1.weight, m0.weight], 0), torch.cat([fh.conv1.bias, m0.bias], 0),
+                                      1, 1, device=device)
+            self.mask2 = pack_conv(m2.weight, m2.bias, 1, 0, device=device)
+        else:
+            self.fh1_mask = None
+            self.mask2 = None
+        self.cor_planes = e.convc1.weight.shape[1]
+
+
+class PackedRaft:
+    def __init__(self, model, device):
+        self.small = bool(model.args.small)
+        self.hdim, self.cdim = model.hidden_dim, model.context_dim
+        self.radius = model.args.corr_radius
+        self.levels = model.args.corr_levels
+        self.fnet = PackedEncoder(model.fnet, device)
+        self.cnet = PackedEncoder(model.cnet, device)
+        self.update = PackedUpdate(model.update_block, self.small, device)
+        self.fdim = self.fnet.head.n
+
+
+# ----------------------------------------------------------------------------
+# Plan building blocks
+# ----------------------------------------------------------------------------
+
+
+class Arena:
+    def __init__(self, device):
+        self.device = device
+        self.bufs = []
+
+    def rows(self, npix, ld, zero=False) -> torch.Tensor:
+        t = (torch.zeros if zero else torch.empty)(npix, ld, device=self.device, dtype=torch.float32)
+        self.bufs.append(t)
+        return t
+
+    def flat(self, n, zero=False) -> torch.Tensor:
+        t = (torch.zeros if zero else torch.empty)(max(int(n), 1), device=self.device, dtype=torch.float32)
+        self.bufs.append(t)
+        return t
+
+
+def _in_stats(L, A: Arena, x: Rows, n_img, hw):
+    c = x.c
+    st = A.flat(2 * n_img * c)
+    ws = A.flat(_lib.load().raft_instnorm_workspace_floats(n_img, hw, c))
+    L.append(Launch("raft_instnorm_stats", x.ptr, x.ld, n_img, hw, c, 1e-5, st.data_ptr(), ws.data_ptr()))
+    return st
+
+
+def _in_apply(L, A: Arena, x: Rows, st, n_img, hw, mode, resid: Rows | None = None, rst=None) -> Rows:
+    out = Rows(A.rows(n_img * hw, x.c))
+    L.append(Launch("raft_instnorm_apply", x.ptr, x.ld, st.data_ptr(), resid.ptr if resid else None,
+                    resid.ld if resid else 0, rst.data_ptr() if rst is not None else None, mode,
+                    out.ptr, out.ld, n_img, hw, x.c))
+    return out
+
+
+def _conv(L, pc: PackedConv, src: Rows, n_img, h, w, out: Rows, **kw):
+    L.append(conv_launch(conv_params(pc, src, n_img, h, w, out, **kw)))
+
+
+def plan_encoder_trunk(L, A: Arena, pe: PackedEncoder, x: Rows, n_img, h, w):
+    """Everything of the encoder but its final 1x1 conv.  Returns (rows, h, w)."""
+    ho, wo = K.conv_out_hw(pe.stem, h, w)
+    if pe.norm == "instance":
+        t = Rows(A.rows(n_img * ho * wo, pe.stem.n))
+        _conv(L, pe.stem, x, n_img, h, w, t)
+        st = _in_stats(L, A, t, n_img, ho * wo)
+        x = _in_apply(L, A, t, st, n_img, ho * wo, 1)
+    else:
+        t = Rows(A.rows(n_img * ho * wo, pe.stem.n))
+        _conv(L, pe.stem, x, n_img, h, w, t, epilogue=_lib.EPI_RELU)
+        x = t
+    h, w = ho, wo
+    for d in pe.blocks:
+        if pe.small:
+            x, h, w = _plan_bottleneck(L, A, pe, d, x, n_img, h, w)
+        else:
+            x, h, w = _plan_residual(L, A, pe, d, x, n_img, h, w)
+    return x, h, w
+
+
+def _plan_residual(L, A, pe, d, x: Rows, n, h, w):
+    """ResidualBlock (core/extractor.py:6-56)."""
+    c1, c2, ds = d["conv1"], d["conv2"], d["ds"]
+    ho, wo = K.conv_out_hw(c1, h, w)
+    npx = n * ho * wo
+    if pe.norm == "instance":
+        t1 = Rows(A.rows(npx, c1.n))
+        _conv(L, c1, x, n, h, w, t1)
+        y1 = _in_apply(L, A, t1, _in_stats(L, A, t1, n, ho * wo), n, ho * wo, 1)
+        t2 = Rows(A.rows(npx, c2.n))
+        _conv(L, c2, y1, n, ho, wo, t2)
+        st2 = _in_stats(L, A, t2, n, ho * wo)
+        if ds is not None:
+            t3 = Rows(A.rows(npx, ds.n))
+            _conv(L, ds, x, n, h, w, t3)
+            out = _in_apply(L, A, t2, st2, n, ho * wo, 2, resid=t3, rst=_in_stats(L, A, t3, n, ho * wo))
+        else:
+            out = _in_apply(L, A, t2, st2, n, ho * wo, 2, resid=x)
+        return out, ho, wo
+    y1 = Rows(A.rows(npx, c1.n))
+    _conv(L, c1, x, n, h, w, y1, epilogue=_lib.EPI_RELU)
+    if ds is not None:
+        xs = Rows(A.rows(npx, ds.n))
+        _conv(L, ds, x, n, h, w, xs)
+    else:
+        xs = x
+    out = Rows(A.rows(npx, c2.n))
+    _conv(L, c2, y1, n, ho, wo, out, epilogue=_lib.EPI_RESID_RELU, aux0=xs)
+    return out, ho, wo
+
+
+def _plan_bottleneck(L, A, pe, d, x: Rows, n, h, w):
+    """BottleneckBlock (core/extractor.py:60-116)."""
+    c1, c2, c3, ds = d["conv1"], d["conv2"], d["conv3"], d["ds"]
+    ho, wo = K.conv_out_hw(c2, h, w)
+    if pe.norm == "instance":
+        t1 = Rows(A.rows(n * h * w, c1.n))
+        _conv(L, c1, x, n, h, w, t1)
+        y1 = _in_apply(L, A, t1, _in_stats(L, A, t1, n, h * w), n, h * w, 1)
+        t2 = Rows(A.rows(n * ho * wo, c2.n))
+        _conv(L, c2, y1, n, h, w, t2)
+        y2 = _in_apply(L, A, t2, _in_stats(L, A, t2, n, ho * wo), n, ho * wo, 1)
+        t3 = Rows(A.rows(n * ho * wo, c3.n))
+        _conv(L, c3, y2, n, ho, wo, t3)
+        st3 = _in_stats(L, A, t3, n, ho * wo)
+        if ds is not None:
+            t4 = Rows(A.rows(n * ho * wo, ds.n))
+            _conv(L, ds, x, n, h, w, t4)
+            out = _in_apply(L, A, t3, st3, n, ho * wo, 2, resid=t4, rst=_in_stats(L, A, t4, n, ho * wo))
+        else:
+            out = _in_apply(L, A, t3, st3, n, ho * wo, 2, resid=x)
+        return out, ho, wo
+    y1 = Rows(A.rows(n * h * w, c1.n))
+    _conv(L, c1, x, n, h, w, y1, epilogue=_lib.EPI_RELU)
+    y2 = Rows(A.rows(n * ho * wo, c2.n))
+    _conv(L, c2, y1, n, h, w, y2, epilogue=_lib.EPI_RELU)
+    if ds is not None:
+        xs = Rows(A.rows(n * ho * wo, ds.n))
+        _conv(L, ds, x, n, h, w, xs)
+    else:
+        xs = x
+    out = Rows(A.rows(n * ho * wo, c3.n))
+    _conv(L, c3, y2, n, ho, wo, out, epilogue=_lib.EPI_RESID_RELU, aux0=xs)
+    return out, ho, wo
+
+
+class UpdateBuffers:
+    """Recurrent-state buffers of the update block for P rows (module docstring)."""
+
+    def __init__(self, A: Arena, pu: PackedUpdate, P, corr_ld):
+        self.P = P
+        self.hx = A.rows(P, pu.ld, zero=True)
+        self.corr = A.rows(P, corr_ld)
+        hd = pu.hdim
+        if pu.small:
+            self.cor1 = None
+            self.cf = A.rows(P, 128)       # cor (96) | flo (32)
+            self.flo1 = A.rows(P, 64)
+            self.fh = A.rows(P, 128)
+            self.mask = None
+        else:
+            self.cor1 = A.rows(P, 256)
+            self.cf = A.rows(P, 256)       # cor (192) | flo (64)
+            self.flo1 = A.rows(P, 128)
+            self.fh = A.rows(P, 512)
+            self.mask = A.rows(P, 576)
+        self.z = A.rows(P, hd)
+        self.rh = A.rows(P, hd)
+        self.coords = A.rows(P, 2)
+
+    # channel slots of HX
+    def h(self, pu):
+        return Rows(self.hx, 0, pu.hdim)
+
+    def inp(self, pu):
+        return Rows(self.hx, pu.hdim, pu.cdim)
+
+    def motion(self, pu):
+        return Rows(self.hx, pu.hdim + pu.cdim, self.motion_c(pu))
+
+    @staticmethod
+    def motion_c(pu):
+        return 80 if pu.small else 126
+
+    def flow_off(self, pu):
+        return pu.hdim + pu.cdim + self.motion_c(pu)
+
+    def x(self, pu):
+        """x = cat[inp, motion, flow] (+ zero pad for the small model)."""
+        return Rows(self.hx, pu.hdim, pu.ld - pu.hdim)
+
+
+def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool):
+    """One BasicUpdateBlock / SmallUpdateBlock step (core/update.py:297-325 / :250-263)
+    followed by coords1 += delta_flow (core/raft.py:232).  Assumes ub.corr and the
+    flow slot of HX were filled by the lookup."""
+    P = B * h * w
+    hx = Rows(ub.hx)
+    flow = Rows(ub.hx, ub.flow_off(pu), 2)
+    if pu.small:
+        cf = Rows(ub.cf)
+        _conv(L, pu.convc1, Rows(ub.corr), B, h, w, cf.sub(0, 96), epilogue=_lib.EPI_RELU)
+        _conv(L, pu.convf1, flow, B, h, w, Rows(ub.flo1), epilogue=_lib.EPI_RELU)
+        _conv(L, pu.convf2, Rows(ub.flo1), B, h, w, cf.sub(96, 32), epilogue=_lib.EPI_RELU)
+        _conv(L, pu.conv, cf, B, h, w, ub.motion(pu), epilogue=_lib.EPI_RELU)
+    else:
+        cf = Rows(ub.cf)
+        _conv(L, pu.convc1, Rows(ub.corr), B, h, w, Rows(ub.cor1), epilogue=_lib.EPI_RELU)
+        _conv(L, pu.convc2, Rows(ub.cor1), B, h, w, cf.sub(0, 192), epilogue=_lib.EPI_RELU)
+        _conv(L, pu.convf1, flow, B, h, w, Rows(ub.flo1), epilogue=_lib.EPI_RELU)
+        _conv(L, pu.convf2, Rows(ub.flo1), B, h, w, cf.sub(192, 64), epilogue=_lib.EPI_RELU)
+        _conv(L, pu.conv, cf, B, h, w, ub.motion(pu), epilogue=_lib.EPI_RELU)
+    hd = pu.hdim
+    hrows = ub.h(pu)
+    for zr, q in pu.gru:
+        _conv(L, zr, hx, B, h, w, Rows(ub.z), epilogue=_lib.EPI_GRU_ZR, split=hd, aux0=hrows, out1=Rows(ub.rh))
+        _conv(L, q, Rows(ub.rh), B, h, w, hrows, src1=ub.x(pu), epilogue=_lib.EPI_GRU_Q, aux0=hrows,
+              aux1=Rows(ub.z))
+    coords = Rows(ub.coords)
+    if pu.small:
+        _conv(L, pu.fh1, hrows, B, h, w, Rows(ub.fh), epilogue=_lib.EPI_RELU)
+        _conv(L, pu.fh2, Rows(ub.fh), B, h, w, coords, epilogue=_lib.EPI_ADD_TO_OUT)
+    else:
+        fh = Rows(ub.fh)
+        if with_mask:
+            _conv(L, pu.fh1_mask, hrows, B, h, w, fh, epilogue=_lib.EPI_RELU)
+        else:
+            _conv(L, pu.fh1, hrows, B, h, w, fh.sub(0, 256), epilogue=_lib.EPI_RELU)
+        _conv(L, pu.fh2, fh.sub(0, 256), B, h, w, coords, epilogue=_lib.EPI_ADD_TO_OUT)
+        if with_mask:
+            _conv(L, pu.mask2, fh.sub(256, 256), B, h, w, Rows(ub.mask), epilogue=_lib.EPI_LINEAR, alpha=0.25)
+
+
+# ----------------------------------------------------------------------------
+# The whole forward
+# ----------------------------------------------------------------------------
+
+
+class RaftPlan:
+    """RAFT.forward (core/raft.py:145-251, eval mode) as a fixed launch list."""
+
+    def __init__(self, pk: PackedRaft, B, H, W, iters, test_mode=True, alternate=False, flow_init=False,
+                 device=None):
+        if H % 8 or W % 8:
+            raise ValueError(f"image size {H}x{W} must be a multiple of 8 (pad with InputPadder)")
+        self.pk, self.B, self.H, self.W, self.iters = pk, B, H, W, iters
+        self.test_mode, self.alternate = test_mode, alternate
+        self.device = device
+        A = self.arena = Arena(device)
+        L = self.launches = []
+        h, w = H // 8, W // 8
+        self.h, self.w = h, w
+        P = B * h * w
+        self.img1 = torch.empty(B, 3, H, W, device=device)
+        self.img2 = torch.empty(B, 3, H, W, device=device)
+        self.flow_init = torch.zeros(B, 2, h, w, device=device) if flow_init else None
+        prep = Rows(A.rows(2 * B * H * W, 3))
+        L.append(Launch("raft_prep_images", self.img1.data_ptr(), self.img2.data_ptr(), prep.ptr, B, H, W))
+        # feature network on [img1; img2] (core/raft.py:177-182)
+        x, fh_, fw_ = plan_encoder_trunk(L, A, pk.fnet, prep, 2 * B, H, W)
+        assert (fh_, fw_) == (h, w), ((fh_, fw_), (h, w))
+        fm = Rows(A.rows(2 * B * h * w, pk.fdim))
+        _conv(L, pk.fnet.head, x, 2 * B, h, w, fm)
+        self.fmap = fm.t
+        r, lv = pk.radius, pk.levels
+        corr_ld = lv * (2 * r + 1) ** 2
+        pu = pk.update
+        ub = self.ub = UpdateBuffers(A, pu, P, corr_ld)
+        fmap1 = fm.t[: B * h * w]
+        fmap2 = fm.t[B * h * w:]
+        C = pk.fdim
+        div = K.sqrt_c(C)
+        if not alternate:
+            self.pyramid = A.flat(K.pyramid_floats(B, h, w, lv))
+            L.append(Launch("raft_corr_build", fmap1.data_ptr(), fmap2.data_ptr(), C, B, h, w, C, lv, div,
+                            self.pyramid.data_ptr()))
+        else:
+            # AlternateCorrBlock pools num_levels times (core/corr.py:157-161); the
+            # last level is never used, but its existence is the reference's size check.
+            hh, ww = h, w
+            for _ in range(lv):
+                hh, ww = hh // 2, ww // 2
+                if hh < 1 or ww < 1:
+                    raise RuntimeError(f"AlternateCorrBlock: feature map {h}x{w} too small for {lv} pooling levels")
+            self.f2levels = [(fmap2, h, w)]
+            hh, ww = h, w
+            for _ in range(lv - 1):
+                nh, nw = hh // 2, ww // 2
+                dst = A.rows(B * nh * nw, C)
+                L.append(Launch("raft_avgpool2_nhwc", self.f2levels[-1][0].data_ptr(), dst.data_ptr(), B, hh, ww, C))
+                self.f2levels.append((dst, nh, nw))
+                hh, ww = nh, nw
+        # context network (core/raft.py:193-200): tanh/relu split fused into its last conv
+        xc, _, _ = plan_encoder_trunk(L, A, pk.cnet, Rows(prep.t[: B * H * W]), B, H, W)
+        _conv(L, pk.cnet.head, xc, B, h, w, ub.h(pu), epilogue=_lib.EPI_TANH_RELU, split=pk.hdim, out1=ub.inp(pu))
+        L.append(Launch("raft_init_coords", ub.coords.data_ptr(),
+                        self.flow_init.data_ptr() if self.flow_init is not None else None, B, h, w))
+        self.loop_start = len(L)
+        self.flow_up = [torch.empty(B, 2, H, W, device=device) for _ in range(1 if test_mode else iters)]
+        flow_slot = ub.flow_off(pu)
+        for it in range(iters):
+            last = it == iters - 1
+            if not alternate:
+                L.append(Launch("raft_corr_lookup", self.pyramid.data_ptr(), B, h, w, lv, r, ub.coords.data_ptr(), 0,
+                                ub.corr.data_ptr(), corr_ld, 0, ub.hx.data_ptr() + 4 * flow_slot, pu.ld))
+            else:
+                for i, (f2, hh, ww) in enumerate(self.f2levels):
+                    fl = ub.hx.data_ptr() + 4 * flow_slot if i == 0 else None
+                    L.append(Launch("raft_alt_corr_lookup_nhwc", fmap1.data_ptr(), f2.data_ptr(), ub.coords.data_ptr(),
+                                    0, float(2 ** i), ub.corr.data_ptr() + 4 * i * (2 * r + 1) ** 2, corr_ld,
+                                    B, h, w, hh, ww, C, r, div, fl, pu.ld))
+            want_up = last or not test_mode
+            plan_update(L, pu, ub, B, h, w, with_mask=want_up and not pu.small)
+            if want_up:
+                dst = self.flow_up[-1 if test_mode else it]
+                if pu.small:
+                    L.append(Launch("raft_upflow8", ub.coords.data_ptr(), dst.data_ptr(), B, h, w))
+                else:
+                    L.append(Launch("raft_convex_upsample", ub.coords.data_ptr(), ub.mask.data_ptr(), 576,
+                                    dst.data_ptr(), B, h, w))
+        self.loop_end = len(L)
+        self.flow_low = torch.empty(B, 2, h, w, device=device)
+        L.append(Launch("raft_flow_from_coords", ub.coords.data_ptr(), self.flow_low.data_ptr(), B, h, w))
+        self.graph = None
+
+    # -- execution --------------------------------------------------------
+    def run(self):
+        s = K.stream_handle()
+        for l in self.launches:
+            l(s)
+
+    def capture(self):
+        """Record the whole launch list into a hipGraph (static buffers, no allocation)."""
+        torch.cuda.synchronize()
+        self.run()  # warm-up outside capture (first-launch code object loads)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.run()
+        torch.cuda.synchronize()
+        self.graph = g
+        return g
+
+    def replay(self):
+        if self.graph is None:
+            self.capture()
+        self.graph.replay()
+
+    def set_inputs(self, image1, image2, flow_init=None):
+        self.img1.copy_(image1)
+        self.img2.copy_(image2)
+        if self.flow_init is not None:
+            self.flow_init.copy_(flow_init)
+
+    def outputs(self, clone=True):
+        f = (lambda t: t.clone()) if clone else (lambda t: t)
+        if self.test_mode:
+            return f(self.flow_low), f(self.flow_up[0])
+        return [f(t) for t in self.flow_up]
+
+    def kernel_names(self):
+        return [l.name for l in self.launches]

@@ -1,0 +1,126 @@
+"""RAFT — drop-in for core/raft.py (inference on MI355X).
+
+`RAFT(args)` builds the same module tree as the reference (`core/raft.py:37-78`:
+fnet / cnet / update_block with identical parameter names, so reference
+checkpoints — including DataParallel `module.` ones via the caller's wrapper —
+load unchanged) and `forward(image1, image2, iters=12, flow_init=None,
+upsample=True, test_mode=False)` keeps the reference's contract
+(`core/raft.py:145-251`): NCHW float images in [0, 255] with H, W multiples of
+8 on the model's device; returns `(flow_low, flow_up)` in test_mode, else the
+list of `iters` upsampled flows.
+
+Execution is an engine.RaftPlan: every kernel is hand-written HIP (encoders,
+correlation build + pyramid, window lookup, update block, upsampling), the
+launch list is fixed per input shape, and with `model.hip_graph = True` the
+whole forward (including the 32-iteration loop) replays as one hipGraph.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import kernels as K
+from .engine import PackedRaft, RaftPlan
+from .extractor import BasicEncoder, SmallEncoder
+from .update import BasicUpdateBlock, SmallUpdateBlock
+from .utils.utils import coords_grid
+
+
+class RAFT(nn.Module):
+    def __init__(self, args):
+        super().__init__()
+        self.args = args
+        if args.small:
+            self.hidden_dim = hdim = 96
+            self.context_dim = cdim = 64
+            args.corr_levels = 4
+            args.corr_radius = 3
+        else:
+            self.hidden_dim = hdim = 128
+            self.context_dim = cdim = 128
+            args.corr_levels = 4
+            args.corr_radius = 4
+        if "dropout" not in self.args:
+            self.args.dropout = 0
+        if "alternate_corr" not in self.args:
+            self.args.alternate_corr = False
+        if "mixed_precision" not in self.args:
+            self.args.mixed_precision = False
+        if args.small:
+            self.fnet = SmallEncoder(output_dim=128, norm_fn="instance", dropout=args.dropout)
+            self.cnet = SmallEncoder(output_dim=hdim + cdim, norm_fn="none", dropout=args.dropout)
+            self.update_block = SmallUpdateBlock(self.args, hidden_dim=hdim)
+        else:
+            self.fnet = BasicEncoder(output_dim=256, norm_fn="instance", dropout=args.dropout)
+            self.cnet = BasicEncoder(output_dim=hdim + cdim, norm_fn="batch", dropout=args.dropout)
+            self.update_block = BasicUpdateBlock(self.args, hidden_dim=hdim)
+        # execution state (not part of state_dict)
+        self.hip_graph = bool(getattr(args, "hip_graph", False))
+        self._packed = None
+        self._packed_key = None
+        self._plans = {}
+
+    def freeze_bn(self):
+        for m in self.modules():
+            if isinstance(m, nn.BatchNorm2d):
+                m.eval()
+
+    def initialize_flow(self, img):
+        n, c, h, w = img.shape
+        coords0 = coords_grid(n, h // 8, w // 8, device=img.device)
+        coords1 = coords_grid(n, h // 8, w // 8, device=img.device)
+        return coords0, coords1
+
+    def upsample_flow(self, flow, mask):
+        """Convex upsampling (core/raft.py:112-142) on the HIP kernel; flow [N,2,H,W], mask [N,576,H,W]."""
+        from . import _lib
+        K.require_device(flow, mask)
+        n, _, h, w = flow.shape
+        coords = coords_grid(n, h, w, device=flow.device) + flow
+        crow = K.nchw_to_rows(coords.contiguous())
+        mrow = K.nchw_to_rows(mask.contiguous())
+        out = torch.empty(n, 2, 8 * h, 8 * w, device=flow.device)
+        _lib.call("raft_convex_upsample", crow.data_ptr(), mrow.data_ptr(), 576, out.data_ptr(), n, h, w,
+                  K.stream_handle())
+        return out
+
+    # -- weights / plans ---------------------------------------------------
+    def _weights_key(self):
+        return tuple((p.data_ptr(), p._version) for p in self.parameters()) + tuple(
+            (b.data_ptr(), b._version) for b in self.buffers())
+
+    def packed(self, device):
+        key = (self._weights_key(), str(device))
+        if self._packed is None or self._packed_key != key:
+            with torch.no_grad():
+                self._packed = PackedRaft(self, device)
+            self._packed_key = key
+            self._plans = {}
+        return self._packed
+
+    def plan(self, batch, height, width, iters, test_mode=True, flow_init=False, device=None):
+        device = device or next(self.parameters()).device
+        pk = self.packed(device)
+        key = (batch, height, width, iters, bool(test_mode), bool(self.args.alternate_corr), bool(flow_init))
+        pl = self._plans.get(key)
+        if pl is None:
+            pl = RaftPlan(pk, batch, height, width, iters, test_mode=test_mode,
+                          alternate=bool(self.args.alternate_corr), flow_init=flow_init, device=device)
+            self._plans[key] = pl
+        return pl
+
+    def forward(self, image1, image2, iters=12, flow_init=None, upsample=True, test_mode=False):
+        if self.training:
+            raise NotImplementedError("raft_optical_flow_amd.RAFT is an inference path: call model.eval() "
+                                      "(training / BatchNorm batch statistics are out of scope)")
+        K.require_device(image1, image2, flow_init)
+        if image1.shape != image2.shape or image1.dim() != 4 or image1.shape[1] != 3:
+            raise ValueError(f"images must both be [N, 3, H, W], got {tuple(image1.shape)} / {tuple(image2.shape)}")
+        b, _, H, W = image1.shape
+        pl = self.plan(b, H, W, iters, test_mode, flow_init is not None, image1.device)
+        pl.set_inputs(image1, image2, flow_init)
+        if self.hip_graph:
+            pl.replay()
+        else:
+            pl.run()
+        return pl.outputs(clone=True)

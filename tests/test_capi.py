@@ -1,0 +1,57 @@
+"""The C-ABI library loads and exports every entry point include/raft_hip.h declares
+(no compute calls: runs without a GPU)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import REPO
+from raft_optical_flow_amd import _lib
+
+HEADER = os.path.join(REPO, "include", "raft_hip.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(raft_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for must in ("raft_alt_corr_forward", "raft_alt_corr_backward", "raft_corr_build", "raft_corr_lookup",
+                 "raft_conv2d", "raft_convex_upsample", "raft_hip_abi_version"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.fail(f"{_lib.LIB_PATH} not built (run python __graft_entry__.py build)")
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    # the ctypes prototype table covers the same set
+    assert sorted(_lib.EXPORTED) == declared_functions()
+
+
+def test_abi_queries_without_gpu():
+    lib = _lib.load()
+    assert lib.raft_hip_abi_version() == 1
+    assert lib.raft_hip_arch() == b"gfx950"
+    # size queries are pure host arithmetic
+    assert lib.raft_corr_pyramid_floats(1, 55, 128, 4) == 7040 * (55 * 128 + 27 * 64 + 13 * 32 + 6 * 16)
+    n, k = ctypes.c_int(), ctypes.c_int()
+    assert lib.raft_conv2d_packed_shape(0, 126, 3, 3, 256, ctypes.byref(n), ctypes.byref(k)) == 0
+    assert (n.value, k.value) == (128, 9 * 256)
+    assert lib.raft_conv2d_packed_shape(1, 128, 7, 7, 2, ctypes.byref(n), ctypes.byref(k)) == 0
+    assert (n.value, k.value) == (128, 128)
+
+
+def test_argument_errors_are_reported_without_launch():
+    lib = _lib.load()
+    rc = lib.raft_corr_lookup(None, 1, 8, 8, 4, 4, None, 0, None, 0, 0, None, 0, None)
+    assert rc == -1
+    assert b"null" in lib.raft_hip_last_error()
+    rc = lib.raft_corr_build(1, 1, 256, 1, 8, 8, 100, 4, 10.0, 1, None)  # C % 32 != 0
+    assert rc == -1 and b"multiple of 32" in lib.raft_hip_last_error()

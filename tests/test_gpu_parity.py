@@ -1,0 +1,339 @@
+"""GPU parity: the HIP path (through the C-ABI) against the golden vectors of the
+reference and against the numpy oracle.  Tolerances (max-abs, fp32):
+  lookup / pyramid   1e-5   (values O(1..10))
+  conv GEMM          1e-4 x max|ref| scale
+  update block       1e-4
+  end-to-end flow    1e-3   (north_star bound on the final flow field)
+"""
+import argparse
+import io
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import load_golden
+from oracle import raft_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def maxabs(a, b):
+    a = a.detach().cpu().numpy() if torch.is_tensor(a) else np.asarray(a)
+    b = b.detach().cpu().numpy() if torch.is_tensor(b) else np.asarray(b)
+    return float(np.max(np.abs(a.astype(np.float64) - b.astype(np.float64))))
+
+
+def t(x):
+    return torch.from_numpy(np.ascontiguousarray(x)).float().to(DEV)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from raft_optical_flow_amd import _lib
+    _lib.load()
+
+
+def make_model(small, seed=0, alternate=False):
+    from raft_optical_flow_amd import RAFT
+    from raft_optical_flow_amd.init import seeded_state_dict
+    m = RAFT(argparse.Namespace(small=small, mixed_precision=False, alternate_corr=alternate))
+    sd = seeded_state_dict(m, seed)
+    m.load_state_dict(sd)
+    return m.to(DEV).eval(), {k: v.numpy() for k, v in sd.items()}
+
+
+# ----------------------------------------------------------------------------- correlation
+
+
+def test_pyramid_golden():
+    from raft_optical_flow_amd import CorrBlock
+    g = load_golden("pyramid_b1c32_8x12.npz")
+    cb = CorrBlock(t(g["fmap1"]), t(g["fmap2"]), num_levels=4, radius=4)
+    for i in range(4):
+        assert maxabs(cb.corr_pyramid[i], g[f"level{i}"]) < 1e-5
+
+
+def test_pyramid_vs_oracle_ragged():
+    """C=256, odd sizes (floor pooling, partial GEMM tiles), B=2."""
+    from raft_optical_flow_amd import CorrBlock
+    rng = np.random.default_rng(0)
+    f1 = rng.standard_normal((2, 256, 23, 37)).astype(np.float32)
+    f2 = rng.standard_normal((2, 256, 23, 37)).astype(np.float32)
+    cb = CorrBlock(t(f1), t(f2), num_levels=4, radius=4)
+    ref = O.corr_pyramid(f1, f2, 4)
+    for i in range(4):
+        scale = np.abs(ref[i]).max()
+        assert maxabs(cb.corr_pyramid[i], ref[i]) < 1e-5 * max(1.0, scale)
+
+
+@pytest.mark.parametrize("r", [4, 3])
+def test_lookup_golden(r):
+    from raft_optical_flow_amd import CorrBlock
+    g = load_golden("lookup_b2c64_16x20.npz")
+    cb = CorrBlock(t(g["fmap1"]), t(g["fmap2"]), num_levels=4, radius=r)
+    out = cb(t(g["coords"]))
+    assert maxabs(out, g[f"corr_r{r}"]) < 1e-5
+
+
+def test_lookup_degenerate_level_nan():
+    from raft_optical_flow_amd import CorrBlock
+    g = load_golden("lookup_degenerate_6x8.npz")
+    cb = CorrBlock(t(g["fmap1"]), t(g["fmap2"]), num_levels=3, radius=2)
+    out = cb(t(g["coords"])).cpu().numpy()
+    ref = g["corr"]
+    np.testing.assert_array_equal(np.isnan(out), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    assert maxabs(out[ok], ref[ok]) < 1e-5
+
+
+def test_lookup_far_out_of_bounds_and_large_coords():
+    from raft_optical_flow_amd import CorrBlock
+    rng = np.random.default_rng(1)
+    f1 = rng.standard_normal((1, 64, 20, 30)).astype(np.float32)
+    f2 = rng.standard_normal((1, 64, 20, 30)).astype(np.float32)
+    coords = (rng.uniform(-60, 90, (1, 2, 20, 30))).astype(np.float32)
+    coords[0, :, 0, :5] = np.round(coords[0, :, 0, :5])  # exact integers
+    cb = CorrBlock(t(f1), t(f2), num_levels=4, radius=4)
+    ref = O.corr_lookup(O.corr_pyramid(f1, f2, 4), coords, 4)
+    assert maxabs(cb(t(coords)), ref) < 2e-5
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_alt_cuda_corr_forward_vs_oracle(n):
+    from raft_optical_flow_amd import alt_cuda_corr
+    rng = np.random.default_rng(2)
+    B, H1, W1, H2, W2, C, r = 2, 9, 13, 5, 7, 96, 4
+    f1 = rng.standard_normal((B, H1, W1, C)).astype(np.float32)
+    f2 = rng.standard_normal((B, H2, W2, C)).astype(np.float32)
+    coords = rng.uniform(-4, 12, (B, n, H1, W1, 2)).astype(np.float32)
+    corr, = alt_cuda_corr.forward(t(f1), t(f2), t(coords), r)
+    ref = O.alt_corr_forward(f1, f2, coords, r)
+    assert corr.shape == ref.shape
+    assert maxabs(corr, ref) < 1e-4
+
+
+@pytest.mark.parametrize("r", [4, 3])
+def test_alternate_corr_block_golden(r):
+    from raft_optical_flow_amd import AlternateCorrBlock
+    g = load_golden("lookup_b2c64_16x20.npz")
+    ab = AlternateCorrBlock(t(g["fmap1"]), t(g["fmap2"]), num_levels=4, radius=r)
+    out = ab(t(g["coords"]))
+    assert maxabs(out, g[f"iter_r{r}"]) < 5e-5
+    assert maxabs(out, g[f"corr_r{r}"]) < 5e-5
+
+
+def test_alt_cuda_corr_backward_vs_autograd():
+    """Gradients of the alt plugin vs autograd through the oracle-equivalent torch expression."""
+    from raft_optical_flow_amd import alt_cuda_corr
+    rng = np.random.default_rng(3)
+    B, H1, W1, H2, W2, C, r = 1, 6, 7, 6, 7, 32, 2
+    f1 = rng.standard_normal((B, H1, W1, C)).astype(np.float32)
+    f2 = rng.standard_normal((B, H2, W2, C)).astype(np.float32)
+    coords = rng.uniform(-1, 8, (B, 1, H1, W1, 2)).astype(np.float32)
+    gout = rng.standard_normal((B, 1, (2 * r + 1) ** 2, H1, W1)).astype(np.float32)
+    f1g, f2g, cg = alt_cuda_corr.backward(t(f1), t(f2), t(coords), t(gout), r)
+    # finite-dimensional linear map: grad via the oracle's linearity in f1, f2
+    eps = 1e-2
+    base = (O.alt_corr_forward(f1.astype(np.float64), f2.astype(np.float64), coords, r) * gout).sum()
+    for (arr, grad) in ((f1, f1g), (f2, f2g)):
+        idx = tuple(rng.integers(0, s) for s in arr.shape)
+        a2 = arr.astype(np.float64).copy()
+        a2[idx] += eps
+        args = (a2, f2.astype(np.float64)) if arr is f1 else (f1.astype(np.float64), a2)
+        num = ((O.alt_corr_forward(*args, coords, r) * gout).sum() - base) / eps
+        assert abs(num - grad.cpu().numpy()[idx]) < 1e-3 * max(1.0, abs(num))
+    assert float(cg.abs().max()) == 0.0
+
+
+# ----------------------------------------------------------------------------- convolution
+
+
+CONV_CASES = [
+    # cin, cout, kh, kw, stride, pad, H, W, B
+    (324, 256, 1, 1, 1, (0, 0), 11, 13, 2),
+    (256, 192, 3, 3, 1, (1, 1), 9, 17, 1),
+    (2, 128, 7, 7, 1, (3, 3), 10, 12, 1),
+    (384, 256, 1, 5, 1, (0, 2), 8, 19, 1),
+    (384, 128, 5, 1, 1, (2, 0), 21, 6, 1),
+    (3, 64, 7, 7, 2, (3, 3), 37, 45, 2),
+    (64, 96, 3, 3, 2, (1, 1), 19, 24, 1),
+    (96, 96, 1, 1, 2, (0, 0), 19, 24, 1),
+    (256, 2, 3, 3, 1, (1, 1), 7, 9, 1),
+    (128, 576, 1, 1, 1, (0, 0), 5, 6, 1),
+    (256, 126, 3, 3, 1, (1, 1), 12, 12, 1),
+]
+
+
+@pytest.mark.parametrize("cin,cout,kh,kw,stride,pad,H,W,B", CONV_CASES)
+def test_conv2d_vs_torch_fp64(cin, cout, kh, kw, stride, pad, H, W, B):
+    from raft_optical_flow_amd import kernels as K
+    from raft_optical_flow_amd import _lib
+    g = torch.Generator().manual_seed(cin * 1000 + cout)
+    x = torch.randn(B, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, kh, kw, generator=g) / np.sqrt(cin * kh * kw)
+    b = torch.randn(cout, generator=g)
+    ref = F.conv2d(x.double(), w.double(), b.double(), stride, pad)
+    pc = K.pack_conv(w, b, stride, pad, device=DEV)
+    src = K.Rows(K.nchw_to_rows(x.to(DEV)))
+    ho, wo = ref.shape[-2:]
+    out = K.Rows(torch.empty(B * ho * wo, cout, device=DEV))
+    K.conv2d_rows(pc, src, B, H, W, out, epilogue=_lib.EPI_LINEAR)
+    y = K.rows_to_nchw(out, B, ho, wo)
+    err = maxabs(y, ref)
+    assert err < 1e-4 * max(1.0, float(ref.abs().max())), err
+
+
+def test_conv2d_two_segments_and_gru_epilogues():
+    """Virtual concat [RH | x] + the GRU z/r and q epilogues vs a torch restatement."""
+    from raft_optical_flow_amd import kernels as K
+    from raft_optical_flow_amd import _lib
+    g = torch.Generator().manual_seed(7)
+    B, H, W, hd, xd = 1, 9, 14, 128, 256
+    h = torch.tanh(torch.randn(B, hd, H, W, generator=g))
+    x = torch.randn(B, xd, H, W, generator=g)
+    wz = torch.randn(hd, hd + xd, 1, 5, generator=g) * 0.02
+    wr = torch.randn(hd, hd + xd, 1, 5, generator=g) * 0.02
+    wq = torch.randn(hd, hd + xd, 1, 5, generator=g) * 0.02
+    bz, br, bq = (torch.randn(hd, generator=g) * 0.1 for _ in range(3))
+    hx = torch.cat([h, x], 1).double()
+    z = torch.sigmoid(F.conv2d(hx, wz.double(), bz.double(), 1, (0, 2)))
+    r = torch.sigmoid(F.conv2d(hx, wr.double(), br.double(), 1, (0, 2)))
+    q = torch.tanh(F.conv2d(torch.cat([r * h.double(), x.double()], 1), wq.double(), bq.double(), 1, (0, 2)))
+    ref = (1 - z) * h.double() + z * q
+    HX = K.nchw_to_rows(torch.cat([h, x], 1).to(DEV))
+    Z = torch.empty(B * H * W, hd, device=DEV)
+    RH = torch.empty(B * H * W, hd, device=DEV)
+    pzr = K.pack_conv(torch.cat([wz, wr]), torch.cat([bz, br]), 1, (0, 2), device=DEV)
+    pq = K.pack_conv(wq, bq, 1, (0, 2), seg_real=[hd, xd], device=DEV)
+    hrows = K.Rows(HX, 0, hd)
+    K.conv2d_rows(pzr, K.Rows(HX), B, H, W, K.Rows(Z), epilogue=_lib.EPI_GRU_ZR, split=hd, aux0=hrows,
+                  out1=K.Rows(RH))
+    K.conv2d_rows(pq, K.Rows(RH), B, H, W, hrows, src1=K.Rows(HX, hd, xd), epilogue=_lib.EPI_GRU_Q, aux0=hrows,
+                  aux1=K.Rows(Z))
+    hn = K.rows_to_nchw(hrows, B, H, W)
+    assert maxabs(hn, ref) < 1e-5
+
+
+# ----------------------------------------------------------------------------- blocks
+
+
+@pytest.mark.parametrize("small", [False, True])
+def test_update_block_golden(small):
+    tag = "small" if small else "full"
+    g = load_golden(f"update_{tag}_16x24.npz")
+    m, _ = make_model(small)
+    net, mask, delta = m.update_block(t(g["net"]), t(g["inp"]), t(g["corr"]), t(g["flow"]))
+    assert maxabs(net, g["net_out"]) < 1e-4
+    assert maxabs(delta, g["delta_out"]) < 1e-4
+    if not small:
+        assert maxabs(mask, g["mask_out"]) < 1e-4
+
+
+def test_upsample_golden():
+    g = load_golden("upsample_16x24.npz")
+    m, _ = make_model(False)
+    assert maxabs(m.upsample_flow(t(g["flow"]), t(g["mask"])), g["flow_up"]) < 1e-4
+    from raft_optical_flow_amd.utils.utils import upflow8
+    g = load_golden("upflow8_5x7.npz")
+    assert maxabs(upflow8(t(g["flow"])), g["flow_up"]) < 1e-5
+
+
+def test_encoders_golden():
+    g = load_golden("encoders_64x96.npz")
+    m, _ = make_model(False)
+    ms, _ = make_model(True)
+    img = t(g["image"])
+    assert maxabs(m.fnet(img), g["fnet"]) < 1e-4
+    assert maxabs(m.cnet(img[:1]), g["cnet"]) < 1e-4
+    assert maxabs(ms.fnet(img), g["fnet_small"]) < 1e-4
+    assert maxabs(ms.cnet(img[:1]), g["cnet_small"]) < 1e-4
+    f1, f2 = m.fnet([img[:1], img[1:]])
+    assert maxabs(torch.cat([f1, f2]), g["fnet"]) < 1e-4
+
+
+# ----------------------------------------------------------------------------- end to end
+
+
+E2E = [("raft_full_smooth_b2_128x192_i12", False, False),
+       ("raft_full_rand_b1_128x192_i32", False, False),
+       ("raft_full_smooth_b2_128x192_i12", False, True),   # alternate_corr path, same reference flow
+       ("raft_small_smooth_b1_128x192_i12", True, False)]
+
+
+@pytest.mark.parametrize("name,small,alt", E2E)
+def test_raft_e2e_golden(name, small, alt):
+    g = load_golden(name + ".npz")
+    m, _ = make_model(small, int(g["seed"]), alternate=alt)
+    with torch.no_grad():
+        low, up = m(t(g["image1"]), t(g["image2"]), iters=int(g["iters"]), test_mode=True)
+    assert maxabs(low, g["flow_low"]) < 1e-3
+    assert maxabs(up, g["flow_up"]) < 1e-3
+
+
+def test_raft_train_mode_output_list_and_graph_replay():
+    g = load_golden("raft_full_smooth_b2_128x192_i12.npz")
+    m, _ = make_model(False, 0)
+    i1, i2 = t(g["image1"]), t(g["image2"])
+    with torch.no_grad():
+        preds = m(i1, i2, iters=12, test_mode=False)
+        assert isinstance(preds, list) and len(preds) == 12
+        assert maxabs(preds[-1], g["flow_up"]) < 1e-3
+        low0, up0 = m(i1, i2, iters=12, test_mode=True)
+        m.hip_graph = True
+        low1, up1 = m(i1, i2, iters=12, test_mode=True)
+        low2, up2 = m(i1, i2, iters=12, test_mode=True)
+    assert maxabs(low1, low0) == 0.0 and maxabs(up1, up0) == 0.0
+    assert maxabs(up2, up0) == 0.0
+
+
+def test_raft_flow_init_warm_start():
+    g = load_golden("raft_full_smooth_b2_128x192_i12.npz")
+    m, p = make_model(False, 0)
+    rng = np.random.default_rng(5)
+    finit = rng.uniform(-2, 2, (2, 2, 16, 24)).astype(np.float32)
+    with torch.no_grad():
+        low, up = m(t(g["image1"]), t(g["image2"]), iters=3, flow_init=t(finit), test_mode=True)
+    rlow, rup = O.raft_forward(p, g["image1"], g["image2"], iters=3, flow_init=finit)
+    assert maxabs(low, rlow) < 1e-3 and maxabs(up, rup) < 1e-3
+
+
+def test_raft_full_size_golden():
+    """Config 2 shape: B=1, 436x1024 padded to 440x1024, iters=32."""
+    from raft_optical_flow_amd.init import seeded_images
+    g = load_golden("raft_full_rand_b1_440x1024_i32.npz")
+    m, _ = make_model(False, int(g["seed"]))
+    i1, i2 = seeded_images(1, 440, 1024, seed=int(g["img_seed"]))
+    with torch.no_grad():
+        low, up = m(i1.to(DEV), i2.to(DEV), iters=32, test_mode=True)
+    assert maxabs(low, g["flow_low"]) < 1e-3
+    assert maxabs(up[:, :, ::8], g["flow_up_rows8"]) < 1e-3
+
+
+def test_raft_small_demo_frames_golden():
+    """Config 1: raft-small.pth on demo-frames 0016 -> 0017 (InputPadder, iters=12)."""
+    from PIL import Image
+    from raft_optical_flow_amd import RAFT, InputPadder
+    g = load_golden("raft_small_demo_0016_0017_i12.npz")
+    wts = load_golden("raft_small_weights.npz")
+    m = RAFT(argparse.Namespace(small=True, mixed_precision=False, alternate_corr=False))
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in wts.items()})
+    m.to(DEV).eval()
+
+    def load(key):
+        a = np.array(Image.open(io.BytesIO(g[key].tobytes()))).astype(np.uint8)
+        return torch.from_numpy(a).permute(2, 0, 1).float()[None].to(DEV)
+
+    i1, i2 = load("png1"), load("png2")
+    padder = InputPadder(i1.shape)
+    assert list(padder._pad) == list(g["pad"])
+    i1, i2 = padder.pad(i1, i2)
+    with torch.no_grad():
+        low, up = m(i1, i2, iters=12, test_mode=True)
+    assert maxabs(low, g["flow_low"]) < 1e-3
+    assert maxabs(up[:, :, ::4], g["flow_up_rows4"]) < 1e-3

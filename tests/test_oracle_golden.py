@@ -1,0 +1,125 @@
+"""Pin the numpy oracle (oracle/raft_oracle.py) to the reference's golden vectors.
+
+The fixtures were produced by tests/golden/make_golden.py from the reference's
+own core/ modules; no test here reads /root/reference.
+"""
+import argparse
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+from oracle import raft_oracle as O
+from raft_optical_flow_amd import RAFT
+from raft_optical_flow_amd.init import seeded_images, seeded_state_dict, smooth_images
+
+
+def params(small, seed=0):
+    m = RAFT(argparse.Namespace(small=small, mixed_precision=False))
+    return {k: v.numpy() for k, v in seeded_state_dict(m, seed).items()}
+
+
+def maxabs(a, b):
+    return float(np.max(np.abs(np.asarray(a, np.float64) - np.asarray(b, np.float64))))
+
+
+def test_pyramid_matches_reference():
+    g = load_golden("pyramid_b1c32_8x12.npz")
+    pyr = O.corr_pyramid(g["fmap1"], g["fmap2"], 4)
+    for i, p in enumerate(pyr):
+        assert p.shape == g[f"level{i}"].shape
+        assert maxabs(p, g[f"level{i}"]) < 1e-5
+
+
+@pytest.mark.parametrize("r", [4, 3])
+def test_lookup_matches_reference(r):
+    g = load_golden("lookup_b2c64_16x20.npz")
+    pyr = O.corr_pyramid(g["fmap1"], g["fmap2"], 4)
+    out = O.corr_lookup(pyr, g["coords"], r)
+    assert out.shape == g[f"corr_r{r}"].shape
+    assert maxabs(out, g[f"corr_r{r}"]) < 2e-5
+
+
+@pytest.mark.parametrize("r", [4, 3])
+def test_alternate_lookup_matches_reference(r):
+    """The alt_cuda_corr restatement against the reference's IterativeCorrBlock
+    (pure-PyTorch AlternateCorrBlock mimic) and against CorrBlock."""
+    g = load_golden("lookup_b2c64_16x20.npz")
+    pyr = O.alternate_corr_pyramid(g["fmap1"], g["fmap2"], 4)
+    out = O.alternate_corr_lookup(pyr, g["coords"], 4, r)
+    assert maxabs(out, g[f"iter_r{r}"]) < 5e-5
+    assert maxabs(out, g[f"corr_r{r}"]) < 5e-5
+
+
+def test_degenerate_one_pixel_level_is_nan_like_reference():
+    g = load_golden("lookup_degenerate_6x8.npz")
+    pyr = O.corr_pyramid(g["fmap1"], g["fmap2"], 3)
+    out = O.corr_lookup(pyr, g["coords"], 2)
+    ref = g["corr"]
+    np.testing.assert_array_equal(np.isnan(out), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    assert maxabs(out[ok], ref[ok]) < 1e-5
+
+
+@pytest.mark.parametrize("small", [False, True])
+def test_update_block_matches_reference(small):
+    tag = "small" if small else "full"
+    g = load_golden(f"update_{tag}_16x24.npz")
+    p = params(small)
+    fn = O.small_update_block if small else O.basic_update_block
+    net, mask, delta = fn(g["net"], g["inp"], g["corr"], g["flow"], p)
+    assert maxabs(net, g["net_out"]) < 1e-5
+    assert maxabs(delta, g["delta_out"]) < 1e-4
+    if not small:
+        assert maxabs(mask, g["mask_out"]) < 1e-4
+
+
+def test_upsample_matches_reference():
+    g = load_golden("upsample_16x24.npz")
+    assert maxabs(O.upsample_flow(g["flow"], g["mask"]), g["flow_up"]) < 1e-4
+    g = load_golden("upflow8_5x7.npz")
+    assert maxabs(O.upflow8(g["flow"]), g["flow_up"]) < 1e-5
+
+
+def test_encoders_match_reference():
+    g = load_golden("encoders_64x96.npz")
+    p = params(False)
+    ps = params(True)
+    assert maxabs(O.basic_encoder(g["image"], p, "fnet", "instance"), g["fnet"]) < 1e-4
+    assert maxabs(O.basic_encoder(g["image"][:1], p, "cnet", "batch"), g["cnet"]) < 1e-4
+    assert maxabs(O.small_encoder(g["image"], ps, "fnet", "instance"), g["fnet_small"]) < 1e-4
+    assert maxabs(O.small_encoder(g["image"][:1], ps, "cnet", "none"), g["cnet_small"]) < 1e-4
+
+
+@pytest.mark.parametrize("name,small", [
+    ("raft_full_smooth_b2_128x192_i12", False),
+    ("raft_full_rand_b1_128x192_i32", False),
+    ("raft_small_smooth_b1_128x192_i12", True),
+])
+def test_raft_e2e_matches_reference(name, small):
+    g = load_golden(name + ".npz")
+    p = params(small, int(g["seed"]))
+    low, up = O.raft_forward(p, g["image1"], g["image2"], iters=int(g["iters"]), small=small)
+    assert maxabs(low, g["flow_low"]) < 1e-3
+    assert maxabs(up, g["flow_up"]) < 1e-3
+
+
+def test_seeded_inputs_regenerate_golden_images():
+    g = load_golden("raft_full_rand_b1_128x192_i32.npz")
+    i1, i2 = seeded_images(1, 128, 192, seed=1)
+    np.testing.assert_array_equal(i1.numpy(), g["image1"])
+    np.testing.assert_array_equal(i2.numpy(), g["image2"])
+    g = load_golden("raft_full_smooth_b2_128x192_i12.npz")
+    i1, i2 = smooth_images(2, 128, 192, seed=3)
+    np.testing.assert_array_equal(i1.numpy(), g["image1"])
+
+
+@pytest.mark.slow
+def test_raft_full_size_matches_reference():
+    g = load_golden("raft_full_rand_b1_440x1024_i32.npz")
+    p = params(False, int(g["seed"]))
+    i1, i2 = seeded_images(1, 440, 1024, seed=int(g["img_seed"]))
+    low, up = O.raft_forward(p, i1.numpy(), i2.numpy(), iters=32)
+    assert maxabs(low, g["flow_low"]) < 1e-3
+    assert maxabs(up[:, :, ::8], g["flow_up_rows8"]) < 1e-3
