@@ -1,0 +1,235 @@
+"""Benchmark: RAFT inference image-pairs/s on MI355X (BASELINE.json config 2).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+A step = one RAFT-full forward (random-init weights, seeded) over one batch of
+synthetic frame pairs already resident in HBM: 436x1024 frames replicate-padded
+to 440x1024 (InputPadder), iters=32, all-pairs correlation, test_mode, replayed
+as one hipGraph.  Each rank processes its own batch (frame pairs shard across
+GPUs with no data-path collective; weights are broadcast once over RCCL), so
+scaling is weak.  Rank 0 prints one JSON line.
+
+The line also carries
+  roofline      the corr-lookup kernel (the metric's "corr-lookup GB/s vs HBM
+                peak"): algorithmic bytes P*2904 per pair-iteration / its
+                average launch time measured with HIP events on its stream;
+  update_gemm   the same accounting for the update-block convolutions (MFMA-bound);
+  cpu_baseline  the numpy oracle (oracle/raft_oracle.py) on the host cores for one
+                pair of the same workload (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_MFMA_PEAK_TF = 157.3  # dense f32 MFMA (= f32 vector) peak
+
+
+def lookup_bytes_per_pixel(levels=4, r=4):
+    """per query pixel L*(2r+2)^2*4 read + L*(2r+1)^2*4 written + 8 B coords."""
+    return levels * (2 * r + 2) ** 2 * 4 + levels * (2 * r + 1) ** 2 * 4 + 8
+
+
+def update_flops_per_pixel(pu, with_mask):
+    """2*MACs of the update-block convolutions per 1/8-res pixel (one iteration)."""
+    def f(pc):
+        return 2 * pc.n * pc.kh * pc.kw * pc.cin_real
+    tot = 0
+    for pc in [pu.convc1, pu.convc2, pu.convf1, pu.convf2, pu.conv]:
+        if pc is not None:
+            tot += f(pc)
+    for zr, q in pu.gru:
+        tot += f(zr) + f(q)
+    tot += f(pu.fh1_mask if with_mask else pu.fh1) + f(pu.fh2)
+    if with_mask:
+        tot += f(pu.mask2)
+    return tot
+
+
+def time_kernel_events(fn, reps):
+    """Average duration of fn() (one launch) with HIP events on the current stream."""
+    s = torch.cuda.current_stream()
+    start = torch.cuda.Event(enable_timing=True)
+    end = torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    start.record(s)
+    for _ in range(reps):
+        fn()
+    end.record(s)
+    end.synchronize()
+    return start.elapsed_time(end) / reps * 1e-3  # seconds
+
+
+def cpu_baseline(args):
+    """The oracle (numpy restatement of the reference path) on one pair of the same workload."""
+    import numpy as np
+    from oracle import raft_oracle as O
+    from raft_optical_flow_amd import RAFT
+    from raft_optical_flow_amd.init import seeded_images, seeded_state_dict
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    m = RAFT(argparse.Namespace(small=False, mixed_precision=False, alternate_corr=False))
+    p = {k: v.numpy() for k, v in seeded_state_dict(m, 0).items()}
+    i1, i2 = seeded_images(1, args.height, args.width, seed=1)
+    i1 = np.pad(i1.numpy(), ((0, 0), (0, 0), (2, 2), (0, 0)), mode="edge")
+    i2 = np.pad(i2.numpy(), ((0, 0), (0, 0), (2, 2), (0, 0)), mode="edge")
+    t0 = time.perf_counter()
+    O.raft_forward(p, i1, i2, iters=args.iters)
+    dt = time.perf_counter() - t0
+    return {"value": round(1.0 / dt, 4), "unit": "image-pairs/s", "cores": threads, "kind": "port",
+            "sample": f"1 pair {args.height}x{args.width} (padded to {i1.shape[2]}x{i1.shape[3]}), iters={args.iters}, "
+                      f"numpy oracle, {dt:.1f} s"}
+
+
+def load_traffic():
+    """HBM bytes per lookup launch from the committed PMC pass (profiles/), if present."""
+    path = os.path.join(ROOT, "profiles", "lookup_pmc.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1, help="frame pairs per GPU per step")
+    ap.add_argument("--height", type=int, default=436)
+    ap.add_argument("--width", type=int, default=1024)
+    ap.add_argument("--iters", type=int, default=32)
+    ap.add_argument("--alternate-corr", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from raft_optical_flow_amd import RAFT, InputPadder
+    from raft_optical_flow_amd.dist import broadcast_state_dict
+    from raft_optical_flow_amd.init import seeded_images, seeded_state_dict
+
+    model = RAFT(argparse.Namespace(small=False, mixed_precision=False, alternate_corr=args.alternate_corr))
+    if rank == 0:
+        model.load_state_dict(seeded_state_dict(model, 0))
+    model.to(dev).eval()
+    if world > 1:
+        broadcast_state_dict(model, src=0)  # one RCCL broadcast over xGMI
+
+    # synthetic frames resident in HBM: a pool of distinct pairs, cycled per step
+    pool = []
+    for k in range(4):
+        i1, i2 = seeded_images(args.batch, args.height, args.width, seed=1 + 1000 * rank + k)
+        i1, i2 = i1.to(dev), i2.to(dev)
+        padder = InputPadder(i1.shape)
+        pool.append(padder.pad(i1, i2))
+    H, W = pool[0][0].shape[-2:]
+    plan = model.plan(args.batch, H, W, args.iters, test_mode=True, device=dev)
+
+    def step(k):
+        plan.set_inputs(*pool[k % len(pool)])
+        if args.no_graph:
+            plan.run()
+        else:
+            plan.replay()
+
+    if not args.no_graph:
+        plan.capture()
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    pairs = world * args.batch * args.steps
+    value = pairs / elapsed
+
+    # ---- per-kernel live timing (HIP events on the launch stream) -------------------
+    from raft_optical_flow_amd import kernels as K
+    s = K.stream_handle()
+    lk = [l for l in plan.launches[plan.loop_start:plan.loop_end] if l.name in
+          ("raft_corr_lookup", "raft_alt_corr_lookup_nhwc")]
+    reps = 200
+    t_lookup = time_kernel_events(lambda: [l(s) for l in lk[:1 if not args.alternate_corr else 4]], reps)
+    h8, w8 = H // 8, W // 8
+    P = args.batch * h8 * w8
+    bytes_per_launch = P * lookup_bytes_per_pixel()
+    achieved = bytes_per_launch / t_lookup / 1e9
+    traffic = load_traffic()
+    roof = {"kernel": "raft_corr_lookup" if not args.alternate_corr else "raft_alt_corr_lookup_nhwc x4",
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
+            "algorithmic_bytes_per_launch": bytes_per_launch, "launch_us": round(t_lookup * 1e6, 2)}
+
+    it_launches = plan.launches[plan.loop_start:plan.loop_end]
+    upd = [l for l in it_launches if l.name == "raft_conv2d"]
+    n_iter_convs = len(upd) // args.iters
+    # one non-final iteration's conv GEMMs (no mask head)
+    one_iter = upd[:n_iter_convs - 0]
+    pu = plan.pk.update
+    t_upd = time_kernel_events(lambda: [l(s) for l in one_iter], 50)
+    fl = P * update_flops_per_pixel(pu, with_mask=False)
+    upd_tf = fl / t_upd / 1e12
+    update_roof = {"kernel": "raft_conv2d (update block, one iteration)", "bound": "mfma",
+                   "achieved": round(upd_tf, 2), "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                   "frac": round(upd_tf / FP32_MFMA_PEAK_TF, 4), "iteration_us": round(t_upd * 1e6, 1),
+                   "flops_per_iteration": fl}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+
+    if rank == 0:
+        out = {
+            "metric": "image-pairs/s at Sintel 436x1024, 32 iters; corr-lookup GB/s vs HBM peak",
+            "value": round(value, 3), "unit": "image-pairs/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (seeded uint8-valued frames, random-init seeded weights)",
+            "config": {"workload": f"RAFT-full inference, {args.height}x{args.width} padded to {H}x{W}, "
+                                   f"{args.batch} pair(s)/GPU/step, iters={args.iters}, "
+                                   f"{'alternate' if args.alternate_corr else 'all-pairs'} corr, "
+                                   f"{'eager' if args.no_graph else 'hipGraph'}",
+                       "global_batch": world * args.batch, "parallelism": f"frame-pair sharding x{world}"},
+            "roofline": roof,
+            "update_gemm": update_roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -53,7 +53,7 @@ const char* raft_hip_last_error(void);  /* message of the last failure on this t
 /* ---------------------------------------------------------------------------
  * All-pairs correlation pyramid (CorrBlock)
  *
- * fmap1, fmap2: NHWC rows [B*H*W][ld] (channels 0..C-1 used).
+ * fmap1, fmap2: NHWC rows [B*H*W][ld] (channels 0..C-1 used, C % 4 == 0, 16-B aligned).
  * pyramid: num_levels levels stored back to back; level l is
  *   [B][H*W][H_l][W_l] with H_0 = H, H_{l+1} = floor(H_l / 2) (same for W),
  *   i.e. for query pixel p of batch b the level-l map starts at

@@ -33,8 +33,8 @@ class CorrBlock:
             if lh < 1 or lw < 1:
                 # F.avg_pool2d raises on an empty output (core/corr.py:53)
                 raise RuntimeError(f"CorrBlock: {h}x{w} feature map too small for {num_levels} pyramid levels")
-        if c % 32:
-            raise ValueError(f"CorrBlock HIP path needs C % 32 == 0 (got C={c})")
+        if c % 4:
+            raise ValueError(f"CorrBlock HIP path needs C % 4 == 0 (got C={c})")
         f1 = K.nchw_to_rows(fmap1)
         f2 = K.nchw_to_rows(fmap2)
         self.pyramid_flat = torch.empty(K.pyramid_floats(b, h, w, num_levels), device=fmap1.device)

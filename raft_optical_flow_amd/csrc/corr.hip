@@ -59,8 +59,9 @@ __global__ __launch_bounds__(256) void corr_build_kernel(CorrBuildArgs a) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-      ra[i] = av_[i] ? *reinterpret_cast<const f32x4*>(arow[i] + kc * CB_BK) : z;
-      rb[i] = bv_[i] ? *reinterpret_cast<const f32x4*>(brow[i] + kc * CB_BK) : z;
+      const bool cin = kc * CB_BK + lq * 4 < a.C;  // C % 4 == 0; zero-fill the K tail
+      ra[i] = (av_[i] && cin) ? *reinterpret_cast<const f32x4*>(arow[i] + kc * CB_BK) : z;
+      rb[i] = (bv_[i] && cin) ? *reinterpret_cast<const f32x4*>(brow[i] + kc * CB_BK) : z;
     }
   };
   auto sstore = [&](int buf) {
@@ -71,7 +72,7 @@ __global__ __launch_bounds__(256) void corr_build_kernel(CorrBuildArgs a) {
     *reinterpret_cast<f32x4*>(Bt + lr * CB_LDSK + lq * 4) = rb[0];
     *reinterpret_cast<f32x4*>(Bt + (lr + 32) * CB_LDSK + lq * 4) = rb[1];
   };
-  const int nk = a.C / CB_BK;
+  const int nk = cdiv(a.C, CB_BK);
   gload(0);
   sstore(0);
   __syncthreads();
@@ -520,7 +521,7 @@ extern "C" int raft_corr_build(const float* fmap1, const float* fmap2, int ld, i
                                float sqrt_c, float* pyramid, raft_stream_t stream) {
   RAFT_REQUIRE(fmap1 && fmap2 && pyramid, "raft_corr_build: null pointer");
   RAFT_REQUIRE(B > 0 && H > 0 && W > 0 && C > 0 && L >= 1 && L <= LK_MAXL, "raft_corr_build: bad sizes");
-  RAFT_REQUIRE(C % 32 == 0, "raft_corr_build: C must be a multiple of 32 (got %d)", C);
+  RAFT_REQUIRE(C % 4 == 0, "raft_corr_build: C must be a multiple of 4 (got %d)", C);
   RAFT_REQUIRE(ld % 4 == 0 && ld >= C, "raft_corr_build: ld must be >= C and a multiple of 4");
   RAFT_REQUIRE((((uintptr_t)fmap1 | (uintptr_t)fmap2) & 15) == 0, "raft_corr_build: fmaps must be 16-byte aligned");
   int hs[LK_MAXL], ws[LK_MAXL];

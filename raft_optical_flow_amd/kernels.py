@@ -79,6 +79,7 @@ class PackedConv:
     stride: tuple
     pad: tuple
     mode: int
+    cin_real: int = 0         # input channels of the original weight (FLOP accounting)
 
 
 def pack_conv(weight: torch.Tensor, bias: torch.Tensor | None, stride=1, padding=0,
@@ -121,7 +122,7 @@ def pack_conv(weight: torch.Tensor, bias: torch.Tensor | None, stride=1, padding
     b = None if bias is None else bias.detach().to(device=device, dtype=torch.float32).contiguous()
     st = (stride, stride) if isinstance(stride, int) else tuple(stride)
     pd = (padding, padding) if isinstance(padding, int) else tuple(padding)
-    return PackedConv(wt, b, o, cin, kh, kw, st, pd, mode)
+    return PackedConv(wt, b, o, cin, kh, kw, st, pd, mode, i)
 
 
 def fold_bn(weight, bias, bn: torch.nn.BatchNorm2d):

@@ -53,5 +53,5 @@ def test_argument_errors_are_reported_without_launch():
     rc = lib.raft_corr_lookup(None, 1, 8, 8, 4, 4, None, 0, None, 0, 0, None, 0, None)
     assert rc == -1
     assert b"null" in lib.raft_hip_last_error()
-    rc = lib.raft_corr_build(1, 1, 256, 1, 8, 8, 100, 4, 10.0, 1, None)  # C % 32 != 0
-    assert rc == -1 and b"multiple of 32" in lib.raft_hip_last_error()
+    rc = lib.raft_corr_build(16, 16, 256, 1, 8, 8, 102, 4, 10.0, 16, None)  # C % 4 != 0
+    assert rc == -1 and b"multiple of 4" in lib.raft_hip_last_error()

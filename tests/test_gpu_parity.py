@@ -241,7 +241,8 @@ def test_upsample_golden():
     assert maxabs(m.upsample_flow(t(g["flow"]), t(g["mask"])), g["flow_up"]) < 1e-4
     from raft_optical_flow_amd.utils.utils import upflow8
     g = load_golden("upflow8_5x7.npz")
-    assert maxabs(upflow8(t(g["flow"])), g["flow_up"]) < 1e-5
+    # the kernel works on coords = grid + flow (RAFT's state), so the API round trip adds one rounding
+    assert maxabs(upflow8(t(g["flow"])), g["flow_up"]) < 2e-6 * float(np.abs(g["flow_up"]).max())
 
 
 def test_encoders_golden():
