@@ -49,7 +49,7 @@ def update_flops_per_pixel(pu, with_mask):
     for pc in [pu.convc1, pu.convc2, pu.convf1, pu.convf2, pu.conv]:
         if pc is not None:
             tot += f(pc)
-    for zr, q in pu.gru:
+    for zr, q, _ctx in pu.gru:  # the inp context GEMM runs once per pair, not per iteration
         tot += f(zr) + f(q)
     tot += f(pu.fh1_mask if with_mask else pu.fh1) + f(pu.fh2)
     if with_mask:
@@ -177,7 +177,7 @@ def main():
     # ---- per-kernel live timing (HIP events on the launch stream) -------------------
     from raft_optical_flow_amd import kernels as K
     s = K.stream_handle()
-    lk = [l for l in plan.launches[plan.loop_start:plan.loop_end] if l.name in
+    lk = [l for l in plan.launches[plan.loop_start:plan.loop_end] if getattr(l, "name", None) in
           ("raft_corr_lookup", "raft_alt_corr_lookup_nhwc")]
     reps = 200
     t_lookup = time_kernel_events(lambda: [l(s) for l in lk[:1 if not args.alternate_corr else 4]], reps)
@@ -193,7 +193,7 @@ def main():
             "algorithmic_bytes_per_launch": bytes_per_launch, "launch_us": round(t_lookup * 1e6, 2)}
 
     it_launches = plan.launches[plan.loop_start:plan.loop_end]
-    upd = [l for l in it_launches if l.name == "raft_conv2d"]
+    upd = [l for l in it_launches if getattr(l, "name", None) == "raft_conv2d"]
     n_iter_convs = len(upd) // args.iters
     # one non-final iteration's conv GEMMs (no mask head)
     one_iter = upd[:n_iter_convs - 0]

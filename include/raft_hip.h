@@ -154,6 +154,9 @@ typedef struct raft_conv2d_params {
   const float* aux0; int aux0_ld;
   const float* aux1; int aux1_ld;
   float* out1; int out1_ld;
+  const float* add0; int add0_ld;           /* optional addend rows: v = acc + bias[n] + add0[m,n]
+                                               (a precomputed partial sum, e.g. the GRU's
+                                               iteration-invariant context term) */
 } raft_conv2d_params;
 
 /* Packed weight geometry for a conv (n_pad, k_pad in floats per row). */

@@ -49,6 +49,7 @@ class ConvParams(ctypes.Structure):
         ("aux0", P), ("aux0_ld", c_int),
         ("aux1", P), ("aux1_ld", c_int),
         ("out1", P), ("out1_ld", c_int),
+        ("add0", P), ("add0_ld", c_int),
     ]
 
 

@@ -12,9 +12,17 @@
 // the MFMA's A/B operand maps assign to k = 0 / 1, so each lane reads its 16
 // operand floats with four ds_read_b128 from a row-major [row][32+4] LDS tile
 // (the +4 pad makes any 16 consecutive rows hit distinct 16-B bank slots).
-// Global -> LDS staging is register double-buffered: the next K-step's loads
-// are issued before the current step's MFMAs and written to the other LDS
-// buffer afterwards; one barrier per K-step.
+//
+// Pipeline: two register staging sets and two LDS buffers.  The global loads
+// of K-step k+2 are issued right after the barrier that publishes step k+1,
+// so every load has two MFMA phases (2 x 16 MFMAs = 2 x 1024 cycles per wave)
+// to land before its ds_write; one barrier per K-step.  The (tap, channel)
+// walk is incremental (no integer division in the loop).  GATHER mode (inputs
+// with < 4 or unaligned channels: the 3-channel stem, the 2-channel flow)
+// decodes k -> (ky, kx, c) through a per-workgroup LDS table.
+//
+// N <= 4 outputs (the flow head's 256 -> 2 conv) use conv_smalln_kernel: one
+// wave per output pixel, channels across lanes, wave reduction per output.
 #include "common.hpp"
 
 namespace raft {
@@ -24,37 +32,84 @@ constexpr int BM = 64;
 constexpr int BN = 64;
 constexpr int BK = 32;
 constexpr int LDSK = BK + 4;
+constexpr int STAGE = (BM + BN) * LDSK;       // floats per LDS buffer
+constexpr int MAX_GATHER_K = 1024;            // k_pad limit of GATHER mode (LDS table)
 
 struct ConvArgs {
   raft_conv2d_params p;
   int M;        // batch * out_h * out_w
   int K;        // packed row length (k_pad)
   int ctot;     // in0_c + in1_c
-  int cpt;      // VEC: K-steps per tap (c_pad / BK)
+  int cpad;     // VEC: channels per tap in the packed weight (multiple of BK)
   int taps;     // kh * kw
 };
 
 __device__ __forceinline__ float sigmoidf_(float v) { return 1.0f / (1.0f + expf(-v)); }
 
+__device__ __forceinline__ void epilogue(const raft_conv2d_params& p, long m, int n, float v) {
+  if (p.add0) v += p.add0[m * p.add0_ld + n];
+  float* o = p.out + m * p.out_ld + n;
+  switch (p.epilogue) {
+    case RAFT_EPI_LINEAR:
+      *o = p.alpha * v;
+      break;
+    case RAFT_EPI_RELU:
+      *o = fmaxf(v, 0.f);
+      break;
+    case RAFT_EPI_RESID_RELU:
+      *o = fmaxf(p.aux0[m * p.aux0_ld + n] + fmaxf(v, 0.f), 0.f);
+      break;
+    case RAFT_EPI_GRU_ZR:
+      if (n < p.split) {
+        *o = sigmoidf_(v);
+      } else {
+        const int c = n - p.split;
+        p.out1[m * p.out1_ld + c] = sigmoidf_(v) * p.aux0[m * p.aux0_ld + c];
+      }
+      break;
+    case RAFT_EPI_GRU_Q: {
+      const float q = tanhf(v);
+      const float z = p.aux1[m * p.aux1_ld + n];
+      const float h = p.aux0[m * p.aux0_ld + n];
+      *o = (1.0f - z) * h + z * q;
+      break;
+    }
+    case RAFT_EPI_TANH_RELU:
+      if (n < p.split)
+        *o = tanhf(v);
+      else
+        p.out1[m * p.out1_ld + (n - p.split)] = fmaxf(v, 0.f);
+      break;
+    case RAFT_EPI_ADD_TO_OUT:
+      *o = *o + v;
+      break;
+    default:
+      break;
+  }
+}
+
+// Per-thread staging state: two A rows (pixels) and the incremental K walk.
+struct AWalk {
+  int pb[2], py[2], px[2];
+  bool pv[2];
+  int ky, kx, c;  // VEC: current tap and channel base of this thread's quad
+};
+
 template <int MODE>
-__device__ __forceinline__ void load_a(const ConvArgs& a, int kc, const int (&pb)[2], const int (&py)[2],
-                                       const int (&px)[2], const bool (&pv)[2], int lq, f32x4 (&ra)[2]) {
+__device__ __forceinline__ void load_a(const ConvArgs& a, const AWalk& w, int kc, int lq, const int* ktab,
+                                       f32x4 (&ra)[2]) {
   const raft_conv2d_params& p = a.p;
   if constexpr (MODE == RAFT_CONV_VEC) {
-    const int tap = kc / a.cpt;
-    const int c = (kc - tap * a.cpt) * BK + lq * 4;
-    const int ky = tap / p.kw, kx = tap - ky * p.kw;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      const int iy = py[i] + ky, ix = px[i] + kx;
-      if (pv[i] && iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w) {
-        const long pix = ((long)pb[i] * p.in_h + iy) * p.in_w + ix;
-        if (c < p.in0_c) {
-          v = *reinterpret_cast<const f32x4*>(p.in0 + pix * p.in0_ld + c);
-        } else if (c - p.in0_c < p.in1_c) {
-          v = *reinterpret_cast<const f32x4*>(p.in1 + pix * p.in1_ld + (c - p.in0_c));
-        }
+      const int iy = w.py[i] + w.ky, ix = w.px[i] + w.kx;
+      if (w.pv[i] && (unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w) {
+        const long pix = ((long)w.pb[i] * p.in_h + iy) * p.in_w + ix;
+        if (w.c < p.in0_c)
+          v = *reinterpret_cast<const f32x4*>(p.in0 + pix * p.in0_ld + w.c);
+        else if (w.c - p.in0_c < p.in1_c)
+          v = *reinterpret_cast<const f32x4*>(p.in1 + pix * p.in1_ld + (w.c - p.in0_c));
       }
       ra[i] = v;
     }
@@ -64,15 +119,13 @@ __device__ __forceinline__ void load_a(const ConvArgs& a, int kc, const int (&pb
       float e[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int k = kc * BK + lq * 4 + j;
-        const int tap = k / a.ctot;
-        const int c = k - tap * a.ctot;
+        const int code = ktab[kc * BK + lq * 4 + j];  // (ky << 20) | (kx << 10) | c, or -1 for padding
         float v = 0.f;
-        if (pv[i] && tap < a.taps) {
-          const int ky = tap / p.kw, kx = tap - ky * p.kw;
-          const int iy = py[i] + ky, ix = px[i] + kx;
-          if (iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w) {
-            const long pix = ((long)pb[i] * p.in_h + iy) * p.in_w + ix;
+        if (w.pv[i] && code >= 0) {
+          const int ky = code >> 20, kx = (code >> 10) & 1023, c = code & 1023;
+          const int iy = w.py[i] + ky, ix = w.px[i] + kx;
+          if ((unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w) {
+            const long pix = ((long)w.pb[i] * p.in_h + iy) * p.in_w + ix;
             v = (c < p.in0_c) ? p.in0[pix * p.in0_ld + c] : p.in1[pix * p.in1_ld + (c - p.in0_c)];
           }
         }
@@ -84,43 +137,88 @@ __device__ __forceinline__ void load_a(const ConvArgs& a, int kc, const int (&pb
 }
 
 template <int MODE>
-__global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
-  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LDSK];
-  // buffer b: A tile at smem + b*STAGE, B tile right after it
-  constexpr int STAGE = (BM + BN) * LDSK;
-  const raft_conv2d_params& p = a.p;
+__device__ __forceinline__ void advance(const ConvArgs& a, AWalk& w) {
+  if constexpr (MODE == RAFT_CONV_VEC) {
+    w.c += BK;
+    if (w.c >= a.cpad) {
+      w.c -= a.cpad;
+      if (++w.kx == a.p.kw) {
+        w.kx = 0;
+        ++w.ky;
+      }
+    }
+  }
+}
 
+// KG = number of K-groups: the work-group holds KG x 4 waves; group g runs the
+// K-steps g, g+KG, g+2KG, ... of the same 64x64 output tile with its own LDS
+// double buffer, so each SIMD carries KG waves of the tile that interleave
+// (one group's MFMAs cover the other's LDS reads, barrier skew and staging).
+// The groups' accumulators are summed through LDS before the epilogue.
+template <int MODE, int KG>
+__global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) float
+      smem[KG * 2 * STAGE + (MODE == RAFT_CONV_GATHER ? MAX_GATHER_K : 0)];
+  const raft_conv2d_params& p = a.p;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave & 1, wn = wave >> 1;
+  const int g = wave >> 2;          // K-group
+  const int wl = wave & 3;          // wave within the group
+  const int wm = wl & 1, wn = wl >> 1;
+  const int lt = tid & 255;         // thread within the group
   const int m0 = blockIdx.x * BM;
   const int n0 = blockIdx.y * BN;
+  int* ktab = reinterpret_cast<int*>(smem + KG * 2 * STAGE);
+  float* gsm = smem + g * 2 * STAGE;  // this group's two LDS buffers
+
+  if constexpr (MODE == RAFT_CONV_GATHER) {
+    for (int k = tid; k < a.K; k += 256 * KG) {
+      const int tap = k / a.ctot;
+      const int c = k - tap * a.ctot;
+      const int ky = tap / p.kw, kx = tap - ky * p.kw;
+      ktab[k] = tap < a.taps ? ((ky << 20) | (kx << 10) | c) : -1;
+    }
+    __syncthreads();
+  }
 
   // staging assignment: rows lr and lr+32, 4-float quad lq of the 32-float K-step
-  const int lr = tid >> 3, lq = tid & 7;
-  int pb[2], py[2], px[2];
-  bool pv[2];
+  const int lr = lt >> 3, lq = lt & 7;
+  AWalk w;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int m = m0 + lr + 32 * i;
-    pv[i] = m < a.M;
-    const int mm = pv[i] ? m : 0;
+    w.pv[i] = m < a.M;
+    const int mm = w.pv[i] ? m : 0;
     const int ox = mm % p.out_w;
     const int t = mm / p.out_w;
     const int oy = t % p.out_h;
-    pb[i] = t / p.out_h;
-    py[i] = oy * p.stride_h - p.pad_h;
-    px[i] = ox * p.stride_w - p.pad_w;
+    w.pb[i] = t / p.out_h;
+    w.py[i] = oy * p.stride_h - p.pad_h;
+    w.px[i] = ox * p.stride_w - p.pad_w;
   }
+  w.ky = 0;
+  w.kx = 0;
+  w.c = lq * 4;
+  for (int i = 0; i < g; ++i) advance<MODE>(a, w);  // group g starts at K-step g
   const float* wrow0 = p.weight + (long)(n0 + lr) * a.K + lq * 4;
   const float* wrow1 = wrow0 + 32L * a.K;
 
-  f32x4 ra[2], rb[2];
   const int nk = a.K / BK;
+  const int cnt = g < nk ? (nk - g + KG - 1) / KG : 0;  // this group's K-steps
+  const int nj = (nk + KG - 1) / KG;                     // phases (group 0's count)
+  f32x4 ra0[2], rb0[2], ra1[2], rb1[2];  // two staging register sets (phases of even / odd parity)
 
-  auto stage_store = [&](int buf) {
-    float* A = smem + buf * STAGE;
+  auto issue = [&](int j, f32x4(&ra)[2], f32x4(&rb)[2]) {
+    const int kc = g + KG * j;
+    load_a<MODE>(a, w, kc, lq, ktab, ra);
+#pragma unroll
+    for (int i = 0; i < KG; ++i) advance<MODE>(a, w);
+    rb[0] = *reinterpret_cast<const f32x4*>(wrow0 + kc * BK);
+    rb[1] = *reinterpret_cast<const f32x4*>(wrow1 + kc * BK);
+  };
+  auto stage = [&](int buf, const f32x4(&ra)[2], const f32x4(&rb)[2]) {
+    float* A = gsm + buf * STAGE;
     float* B = A + BM * LDSK;
     *reinterpret_cast<f32x4*>(A + lr * LDSK + lq * 4) = ra[0];
     *reinterpret_cast<f32x4*>(A + (lr + 32) * LDSK + lq * 4) = ra[1];
@@ -128,25 +226,11 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
     *reinterpret_cast<f32x4*>(B + (lr + 32) * LDSK + lq * 4) = rb[1];
   };
 
-  load_a<MODE>(a, 0, pb, py, px, pv, lq, ra);
-  rb[0] = *reinterpret_cast<const f32x4*>(wrow0);
-  rb[1] = *reinterpret_cast<const f32x4*>(wrow1);
-  stage_store(0);
-  __syncthreads();
-
   f32x16 acc = {};
   const int arow = (wm * 32 + (lane & 31)) * LDSK + (lane >> 5) * 16;
   const int brow = (wn * 32 + (lane & 31)) * LDSK + (lane >> 5) * 16;
-
-  for (int kc = 0; kc < nk; ++kc) {
-    const int cur = kc & 1;
-    const bool more = kc + 1 < nk;
-    if (more) {
-      load_a<MODE>(a, kc + 1, pb, py, px, pv, lq, ra);
-      rb[0] = *reinterpret_cast<const f32x4*>(wrow0 + (kc + 1) * BK);
-      rb[1] = *reinterpret_cast<const f32x4*>(wrow1 + (kc + 1) * BK);
-    }
-    const float* A = smem + cur * STAGE;
+  auto compute = [&](int buf) {
+    const float* A = gsm + buf * STAGE;
     const float* B = A + BM * LDSK;
     f32x4 av[4], bv[4];
 #pragma unroll
@@ -155,11 +239,48 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
       bv[j] = *reinterpret_cast<const f32x4*>(B + brow + 4 * j);
     }
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
+    for (int s = 0; s < 16; ++s)
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s >> 2][s & 3], bv[s >> 2][s & 3], acc, 0, 0, 0);
-    }
-    if (more) stage_store(cur ^ 1);
+  };
+
+  // prologue: phases 0 and 1 in flight, phase 0 staged
+  if (cnt > 0) issue(0, ra0, rb0);
+  if (cnt > 1) issue(1, ra1, rb1);
+  if (cnt > 0) stage(0, ra0, rb0);
+  __syncthreads();
+  if (cnt > 2) issue(2, ra0, rb0);
+
+  // steady state, unrolled by two so the register sets are static
+  int j = 0;
+  for (; j + 2 <= nj; j += 2) {
+    if (j < cnt) compute(0);
+    if (j + 1 < cnt) stage(1, ra1, rb1);
     __syncthreads();
+    if (j + 3 < cnt) issue(j + 3, ra1, rb1);
+    if (j + 1 < cnt) compute(1);
+    if (j + 2 < cnt) stage(0, ra0, rb0);
+    __syncthreads();
+    if (j + 4 < cnt) issue(j + 4, ra0, rb0);
+  }
+  if (j < cnt) compute(0);  // odd phase count: the last phase sits in buffer 0
+
+  if constexpr (KG > 1) {
+    // sum the K-groups' accumulators through LDS: red[r][wave-in-group][lane]
+    __syncthreads();
+    float* red = smem;
+    for (int gg = 1; gg < KG; ++gg) {
+      if (g == gg) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) red[(r * 4 + wl) * 64 + lane] = acc[r];
+      }
+      __syncthreads();
+      if (g == 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] += red[(r * 4 + wl) * 64 + lane];
+      }
+      __syncthreads();
+    }
+    if (g != 0) return;
   }
 
   // ---- epilogue: lane owns column n, rows (r&3) + 8*(r>>2) + 4*(lane>>5)
@@ -169,46 +290,54 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (m >= a.M) continue;
-    const float v = acc[r] + bias;
-    float* o = p.out + (long)m * p.out_ld + n;
-    switch (p.epilogue) {
-      case RAFT_EPI_LINEAR:
-        *o = p.alpha * v;
-        break;
-      case RAFT_EPI_RELU:
-        *o = fmaxf(v, 0.f);
-        break;
-      case RAFT_EPI_RESID_RELU:
-        *o = fmaxf(p.aux0[(long)m * p.aux0_ld + n] + fmaxf(v, 0.f), 0.f);
-        break;
-      case RAFT_EPI_GRU_ZR:
-        if (n < p.split) {
-          *o = sigmoidf_(v);
-        } else {
-          const int c = n - p.split;
-          p.out1[(long)m * p.out1_ld + c] = sigmoidf_(v) * p.aux0[(long)m * p.aux0_ld + c];
+    if (m < a.M) epilogue(p, m, n, acc[r] + bias);
+  }
+}
+
+// Small-N convolution (N <= 4, VEC inputs): one wave per output pixel.
+template <int NOUT>
+__global__ __launch_bounds__(256) void conv_smalln_kernel(ConvArgs a) {
+  const raft_conv2d_params& p = a.p;
+  const int lane = threadIdx.x & 63;
+  const long m = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= a.M) return;
+  const int ox = m % p.out_w;
+  const long t = m / p.out_w;
+  const int oy = t % p.out_h;
+  const int b = t / p.out_h;
+  float acc[NOUT];
+#pragma unroll
+  for (int j = 0; j < NOUT; ++j) acc[j] = 0.f;
+  for (int ky = 0; ky < p.kh; ++ky) {
+    const int iy = oy * p.stride_h - p.pad_h + ky;
+    if ((unsigned)iy >= (unsigned)p.in_h) continue;
+    for (int kx = 0; kx < p.kw; ++kx) {
+      const int ix = ox * p.stride_w - p.pad_w + kx;
+      if ((unsigned)ix >= (unsigned)p.in_w) continue;
+      const long pix = ((long)b * p.in_h + iy) * p.in_w + ix;
+      const float* wt = p.weight + (ky * p.kw + kx) * a.cpad;
+      for (int c = lane * 4; c < a.ctot; c += 256) {
+        const f32x4 v = c < p.in0_c ? *reinterpret_cast<const f32x4*>(p.in0 + pix * p.in0_ld + c)
+                                    : *reinterpret_cast<const f32x4*>(p.in1 + pix * p.in1_ld + (c - p.in0_c));
+#pragma unroll
+        for (int j = 0; j < NOUT; ++j) {
+          const f32x4 wv = *reinterpret_cast<const f32x4*>(wt + (long)j * a.K + c);
+          acc[j] += v[0] * wv[0] + v[1] * wv[1] + v[2] * wv[2] + v[3] * wv[3];
         }
-        break;
-      case RAFT_EPI_GRU_Q: {
-        const float q = tanhf(v);
-        const float z = p.aux1[(long)m * p.aux1_ld + n];
-        const float h = p.aux0[(long)m * p.aux0_ld + n];
-        *o = (1.0f - z) * h + z * q;
-        break;
       }
-      case RAFT_EPI_TANH_RELU:
-        if (n < p.split)
-          *o = tanhf(v);
-        else
-          p.out1[(long)m * p.out1_ld + (n - p.split)] = fmaxf(v, 0.f);
-        break;
-      case RAFT_EPI_ADD_TO_OUT:
-        *o = *o + v;
-        break;
-      default:
-        break;
     }
+  }
+#pragma unroll
+  for (int j = 0; j < NOUT; ++j) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc[j] += __shfl_xor(acc[j], off);
+  }
+  if (lane < p.n) {
+    float v = acc[0];
+#pragma unroll
+    for (int j = 1; j < NOUT; ++j)
+      if (lane == j) v = acc[j];
+    epilogue(p, m, lane, v + (p.bias ? p.bias[lane] : 0.f));
   }
 }
 
@@ -253,13 +382,16 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
   int rc = raft_conv2d_packed_shape(p.mode, p.n, p.kh, p.kw, ctot, &n_pad, &k_pad);
   if (rc) return rc;
   a.K = k_pad;
-  a.cpt = round_up(ctot, BK) / BK;
+  a.cpad = round_up(ctot, BK);
   if (p.mode == RAFT_CONV_VEC) {
     RAFT_REQUIRE(p.in0_c % 4 == 0 && p.in1_c % 4 == 0, "raft_conv2d VEC: channel counts must be multiples of 4");
     RAFT_REQUIRE(p.in1_c == 0 || p.in0_c % BK == 0, "raft_conv2d VEC: seg0 channels must be a multiple of 32 with seg1");
     RAFT_REQUIRE(p.in0_ld % 4 == 0 && (p.in1_c == 0 || p.in1_ld % 4 == 0), "raft_conv2d VEC: ld must be a multiple of 4");
     RAFT_REQUIRE(((uintptr_t)p.in0 & 15) == 0 && ((uintptr_t)p.in1 & 15) == 0,
                  "raft_conv2d VEC: inputs must be 16-byte aligned");
+  } else {
+    RAFT_REQUIRE(k_pad <= MAX_GATHER_K && ctot < 1024 && p.kw < 1024,
+                 "raft_conv2d GATHER: kh*kw*cin must be <= %d (got %d)", MAX_GATHER_K, p.kh * p.kw * ctot);
   }
   RAFT_REQUIRE(((uintptr_t)p.weight & 15) == 0, "raft_conv2d: weight must be 16-byte aligned");
   switch (p.epilogue) {
@@ -282,11 +414,28 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
     default:
       return set_error(RAFT_E_INVALID, "raft_conv2d: unknown epilogue %d", p.epilogue);
   }
-  dim3 grid(cdiv(a.M, BM), n_pad / BN);
   hipStream_t s = as_stream(stream);
-  if (p.mode == RAFT_CONV_VEC)
-    hipLaunchKernelGGL(conv_gemm_kernel<RAFT_CONV_VEC>, grid, dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL(conv_gemm_kernel<RAFT_CONV_GATHER>, grid, dim3(256), 0, s, a);
+  if (p.n <= 4 && p.mode == RAFT_CONV_VEC) {
+    dim3 grid((unsigned)cdiv_l(a.M, 4));
+    if (p.n <= 2)
+      hipLaunchKernelGGL(conv_smalln_kernel<2>, grid, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL(conv_smalln_kernel<4>, grid, dim3(256), 0, s, a);
+    return check_launch("raft_conv2d(small n)");
+  }
+  dim3 grid(cdiv(a.M, BM), n_pad / BN);
+  // few tiles (fewer than ~4 per CU): two K-groups per tile give every SIMD two waves
+  const bool two = (long)grid.x * grid.y < 1024 && a.K / BK >= 4;
+  if (p.mode == RAFT_CONV_VEC) {
+    if (two)
+      hipLaunchKernelGGL((conv_gemm_kernel<RAFT_CONV_VEC, 2>), grid, dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv_gemm_kernel<RAFT_CONV_VEC, 1>), grid, dim3(256), 0, s, a);
+  } else {
+    if (two)
+      hipLaunchKernelGGL((conv_gemm_kernel<RAFT_CONV_GATHER, 2>), grid, dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv_gemm_kernel<RAFT_CONV_GATHER, 1>), grid, dim3(256), 0, s, a);
+  }
   return check_launch("raft_conv2d");
 }

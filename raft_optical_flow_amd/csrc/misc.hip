@@ -164,7 +164,7 @@ __global__ void nhwc_to_nchw_kernel(const float* in, int ld, float* out, int B, 
 // InstanceNorm statistics, stage 1: per (image, pixel chunk) partial sums of
 // (x - shift[c]) and (x - shift[c])^2 with shift = the image's first pixel
 // (shifted data keeps E[x^2] - E[x]^2 well conditioned).
-constexpr int IN_CHUNK = 2048;
+constexpr int IN_CHUNK = 256;  // pixels per partial-sum block: >= 2 blocks per CU at full res
 
 __global__ __launch_bounds__(256) void instnorm_partial_kernel(const float* x, int ld, int HW, int C, float* part) {
   __shared__ float red[2][256];
@@ -202,17 +202,33 @@ __global__ __launch_bounds__(256) void instnorm_partial_kernel(const float* x, i
   }
 }
 
-__global__ void instnorm_finalize_kernel(const float* x, int ld, int HW, int C, int nchunk, const float* part,
-                                         float eps, float* stats, int B) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * C) return;
-  const int b = i / C, c = i - b * C;
+// stage 2: one 256-thread block per (image, 16-channel group); 16 chunk rows per
+// channel summed in double, then a fixed-order LDS reduction (deterministic).
+__global__ __launch_bounds__(256) void instnorm_finalize_kernel(const float* x, int ld, int HW, int C, int nchunk,
+                                                                const float* part, float eps, float* stats, int B) {
+  __shared__ double red[2][16][17];
+  const int b = blockIdx.y;
+  const int cl = threadIdx.x & 15, row = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   double S = 0.0, SS = 0.0;
-  for (int k = 0; k < nchunk; ++k) {
-    const float* o = part + (((long)b * nchunk + k) * C + c) * 2;
-    S += o[0];
-    SS += o[1];
+  if (c < C) {
+    for (int k = row; k < nchunk; k += 16) {
+      const float* o = part + (((long)b * nchunk + k) * C + c) * 2;
+      S += o[0];
+      SS += o[1];
+    }
   }
+  red[0][row][cl] = S;
+  red[1][row][cl] = SS;
+  __syncthreads();
+  if (row != 0 || c >= C) return;
+  S = 0.0;
+  SS = 0.0;
+  for (int k = 0; k < 16; ++k) {
+    S += red[0][k][cl];
+    SS += red[1][k][cl];
+  }
+  const int i = b * C + c;
   const double n = (double)HW;
   const double md = S / n;
   double var = SS / n - md * md;
@@ -328,7 +344,7 @@ extern "C" int raft_instnorm_stats(const float* x, int ld, int B, int HW, int C,
   hipLaunchKernelGGL(instnorm_partial_kernel, dim3(nchunk, B), dim3(256), 0, s, x, ld, HW, C, workspace);
   int rc = check_launch("raft_instnorm_stats(partial)");
   if (rc) return rc;
-  hipLaunchKernelGGL(instnorm_finalize_kernel, dim3(cdiv(B * C, 256)), dim3(256), 0, s, x, ld, HW, C, nchunk,
+  hipLaunchKernelGGL(instnorm_finalize_kernel, dim3(cdiv(C, 16), B), dim3(256), 0, s, x, ld, HW, C, nchunk,
                      workspace, eps, stats, B);
   return check_launch("raft_instnorm_stats(finalize)");
 }

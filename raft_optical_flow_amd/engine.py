@@ -9,16 +9,22 @@ on the current stream; `RaftPlan.capture()` records it into a hipGraph
 with no host work per kernel.
 
 Buffer layout of the recurrent state (P = B * H/8 * W/8 rows), RAFT-full:
-  HX   [P, 384]  = h (128) | inp (128) | motion conv (126) | flow (2)
-                 -> hx = cat[h, x] of core/update.py:106 without a copy,
-                    x = cat[inp, motion, flow] of core/update.py:318
+  HX   [P, 384]  = h (128) | motion conv (126) | flow (2) | inp (128)
+                 -> hx = cat[h, x] of core/update.py:106 without a copy
+                    (x = cat[inp, motion, flow], core/update.py:318, with its
+                    channels permuted; the packed GRU weights follow)
+  CTX1, CTX2 [P, 384]  iteration-invariant GRU term W_inp * inp + b of each
+                 half-step's z | r | q convs, computed once per pair: inp never
+                 changes inside the loop, so the per-iteration GRU GEMMs only
+                 contract over h | motion | flow (K = 5*256 instead of 5*384)
   CORR [P, 324]  lookup output, channel lvl*81 + ix*9 + iy
   COR1 [P, 256], CF [P, 256] = cor (192) | flo (64), FLO1 [P, 128]
   Z, RH [P, 128] GRU gate z and r*h
   FH   [P, 512]  flow-head conv1 (256) | mask conv1 (256), one fused GEMM
   MASK [P, 576], coords1 [P, 2]
-RAFT-small uses the same scheme with hdim 96 / cdim 64 (HX ld 244, two zero
-pad channels keep every row 16-byte aligned).
+RAFT-small uses the same scheme with hdim 96 / cdim 64: HX [P, 244] =
+h (96) | motion (80) | flow (2) | 2 zero pad channels | inp (64) (rows and the
+inp slot stay 16-byte aligned).
 """
 from __future__ import annotations
 
@@ -68,41 +74,52 @@ class PackedEncoder:
 
 
 class PackedUpdate:
-    """BasicUpdateBlock (core/update.py:265-325) / SmallUpdateBlock (:218-263) weights, packed,
-    with the z/r gates of each GRU step fused into one GEMM and, for the basic
-    block, the flow-head and mask-head first convs fused into one GEMM."""
+    """BasicUpdateBlock (core/update.py:265-325) / SmallUpdateBlock (:218-263) weights, packed.
+
+    * each GRU half-step's z and r convs are one GEMM (N = 2*hdim, sigmoid / r*h epilogue);
+    * the GRU convs are split by input channel: the columns acting on `inp`
+      (constant over the iterations) form the once-per-pair context GEMM `ctx`
+      (N = 3*hdim: z | r | q, bias folded in), the rest the per-iteration GEMMs
+      over HX's h | motion | flow prefix (reference column order
+      h | inp | motion | flow, core/update.py:106 + :318, permuted to match);
+    * the basic block's flow-head and mask-head first convs are one GEMM (N = 512).
+    """
 
     def __init__(self, ub, small, device):
         e, g, fh = ub.encoder, ub.gru, ub.flow_head
         self.small = small
         if small:
-            hd, cd = 96, 64
-            self.hdim, self.cdim, self.ld = hd, cd, 244
-            x_real, x_decl = 146, 148
-            self.convc1 = pack_conv(e.convc1.weight, e.convc1.bias, 1, 0, device=device)
-            self.convc2 = None
-            self.convf1 = pack_conv(e.convf1.weight, e.convf1.bias, 1, 3, device=device, mode=_lib.RAFT_CONV_GATHER)
-            self.convf2 = pack_conv(e.convf2.weight, e.convf2.bias, 1, 1, device=device)
-            self.conv = pack_conv(e.conv.weight, e.conv.bias, 1, 1, device=device)
-            steps = [(g.convz, g.convr, g.convq, 1)]
+            hd, cd, mc, pad = 96, 64, 80, 2
+            steps = [(g.convz, g.convr, g.convq)]
         else:
-            hd, cd = 128, 128
-            self.hdim, self.cdim, self.ld = hd, cd, 384
-            x_real, x_decl = 256, 256
-            self.convc1 = pack_conv(e.convc1.weight, e.convc1.bias, 1, 0, device=device)
-            self.convc2 = pack_conv(e.convc2.weight, e.convc2.bias, 1, 1, device=device)
-            self.convf1 = pack_conv(e.convf1.weight, e.convf1.bias, 1, 3, device=device, mode=_lib.RAFT_CONV_GATHER)
-            self.convf2 = pack_conv(e.convf2.weight, e.convf2.bias, 1, 1, device=device)
-            self.conv = pack_conv(e.conv.weight, e.conv.bias, 1, 1, device=device)
-            steps = [(g.convz1, g.convr1, g.convq1, 1), (g.convz2, g.convr2, g.convq2, 1)]
+            hd, cd, mc, pad = 128, 128, 126, 0
+            steps = [(g.convz1, g.convr1, g.convq1), (g.convz2, g.convr2, g.convq2)]
+        self.hdim, self.cdim, self.mc, self.pad = hd, cd, mc, pad
+        self.inp_off = hd + mc + 2 + pad          # HX: h | motion | flow | pad | inp
+        self.ld = self.inp_off + cd
+        self.convc1 = pack_conv(e.convc1.weight, e.convc1.bias, 1, 0, device=device)
+        self.convc2 = None if small else pack_conv(e.convc2.weight, e.convc2.bias, 1, 1, device=device)
+        self.convf1 = pack_conv(e.convf1.weight, e.convf1.bias, 1, 3, device=device, mode=_lib.RAFT_CONV_GATHER)
+        self.convf2 = pack_conv(e.convf2.weight, e.convf2.bias, 1, 1, device=device)
+        self.conv = pack_conv(e.conv.weight, e.conv.bias, 1, 1, device=device)
+        # reference input columns of a GRU conv: h [0,hd) | inp [hd,hd+cd) | motion | flow
+        hcols = slice(0, hd)
+        icols = slice(hd, hd + cd)
+        mcols = slice(hd + cd, hd + cd + mc + 2)   # motion + flow, contiguous
         self.gru = []
-        for cz, cr, cq, _ in steps:
-            wzr = torch.cat([cz.weight, cr.weight], 0)
-            bzr = torch.cat([cz.bias, cr.bias], 0)
-            zr = pack_conv(wzr, bzr, 1, cz.padding, seg_real=[hd + x_real], seg_decl=[hd + x_decl], device=device)
-            q = pack_conv(cq.weight, cq.bias, 1, cq.padding, seg_real=[hd, x_real], seg_decl=[hd, x_decl],
-                          device=device)
-            self.gru.append((zr, q))
+        for cz, cr, cq in steps:
+            wzr = torch.cat([cz.weight, cr.weight], 0).detach()
+            wq = cq.weight.detach()
+            # per iteration: [h | motion | flow (| pad)] for z,r ; [r*h | motion | flow (| pad)] for q
+            zr = pack_conv(torch.cat([wzr[:, hcols], wzr[:, mcols]], 1), None, 1, cz.padding,
+                           seg_real=[hd + mc + 2], seg_decl=[hd + mc + 2 + pad], device=device)
+            q = pack_conv(torch.cat([wq[:, hcols], wq[:, mcols]], 1), None, 1, cq.padding,
+                          seg_real=[hd, mc + 2], seg_decl=[hd, mc + 2 + pad], device=device)
+            # once per pair: inp -> z | r | q pre-activations (+ biases)
+            wctx = torch.cat([wzr[:, icols], wq[:, icols]], 0)
+            bctx = torch.cat([cz.bias, cr.bias, cq.bias], 0)
+            ctx = pack_conv(wctx, bctx, 1, cz.padding, device=device)
+            self.gru.append((zr, q, ctx))
         self.fh1 = pack_conv(fh.conv1.weight, fh.conv1.bias, 1, 1, device=device)
         self.fh2 = pack_conv(fh.conv2.weight, fh.conv2.bias, 1, 1, device=device)
         if not small:
@@ -165,8 +182,8 @@ def _in_apply(L, A: Arena, x: Rows, st, n_img, hw, mode, resid: Rows | None = No
     return out
 
 
-def _conv(L, pc: PackedConv, src: Rows, n_img, h, w, out: Rows, **kw):
-    L.append(conv_launch(conv_params(pc, src, n_img, h, w, out, **kw)))
+def _conv(L, pc: PackedConv, src: Rows, n_img, h, w, out: Rows, side=False, **kw):
+    L.append(conv_launch(conv_params(pc, src, n_img, h, w, out, **kw), side=side))
 
 
 def plan_encoder_trunk(L, A: Arena, pe: PackedEncoder, x: Rows, n_img, h, w):
@@ -278,56 +295,64 @@ class UpdateBuffers:
             self.mask = A.rows(P, 576)
         self.z = A.rows(P, hd)
         self.rh = A.rows(P, hd)
+        self.ctx = [A.rows(P, 3 * hd) for _ in pu.gru]   # z | r | q context terms per half-step
         self.coords = A.rows(P, 2)
 
     # channel slots of HX
     def h(self, pu):
         return Rows(self.hx, 0, pu.hdim)
 
-    def inp(self, pu):
-        return Rows(self.hx, pu.hdim, pu.cdim)
-
     def motion(self, pu):
-        return Rows(self.hx, pu.hdim + pu.cdim, self.motion_c(pu))
-
-    @staticmethod
-    def motion_c(pu):
-        return 80 if pu.small else 126
+        return Rows(self.hx, pu.hdim, pu.mc)
 
     def flow_off(self, pu):
-        return pu.hdim + pu.cdim + self.motion_c(pu)
+        return pu.hdim + pu.mc
 
-    def x(self, pu):
-        """x = cat[inp, motion, flow] (+ zero pad for the small model)."""
-        return Rows(self.hx, pu.hdim, pu.ld - pu.hdim)
+    def inp(self, pu):
+        return Rows(self.hx, pu.inp_off, pu.cdim)
+
+    def gru_in(self, pu):
+        """h | motion | flow (| pad): the per-iteration input of the z/r GEMM."""
+        return Rows(self.hx, 0, pu.inp_off)
+
+    def x_dyn(self, pu):
+        """motion | flow (| pad): the second segment of the q GEMM's input."""
+        return Rows(self.hx, pu.hdim, pu.inp_off - pu.hdim)
+
+
+def plan_gru_context(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w):
+    """Once per pair: W_inp * inp + b for the z | r | q convs of every GRU half-step."""
+    for (zr, q, ctx), buf in zip(pu.gru, ub.ctx):
+        _conv(L, ctx, ub.inp(pu), B, h, w, Rows(buf), epilogue=_lib.EPI_LINEAR)
 
 
 def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool):
     """One BasicUpdateBlock / SmallUpdateBlock step (core/update.py:297-325 / :250-263)
     followed by coords1 += delta_flow (core/raft.py:232).  Assumes ub.corr and the
-    flow slot of HX were filled by the lookup."""
-    P = B * h * w
-    hx = Rows(ub.hx)
+    flow slot of HX were filled by the lookup and plan_gru_context ran for this pair."""
     flow = Rows(ub.hx, ub.flow_off(pu), 2)
+    # the flow branch (convf1 -> convf2) runs on the side stream beside the corr branch
+    cf = Rows(ub.cf)
+    L.append(K.FORK)
     if pu.small:
-        cf = Rows(ub.cf)
+        _conv(L, pu.convf1, flow, B, h, w, Rows(ub.flo1), epilogue=_lib.EPI_RELU, side=True)
+        _conv(L, pu.convf2, Rows(ub.flo1), B, h, w, cf.sub(96, 32), epilogue=_lib.EPI_RELU, side=True)
         _conv(L, pu.convc1, Rows(ub.corr), B, h, w, cf.sub(0, 96), epilogue=_lib.EPI_RELU)
-        _conv(L, pu.convf1, flow, B, h, w, Rows(ub.flo1), epilogue=_lib.EPI_RELU)
-        _conv(L, pu.convf2, Rows(ub.flo1), B, h, w, cf.sub(96, 32), epilogue=_lib.EPI_RELU)
-        _conv(L, pu.conv, cf, B, h, w, ub.motion(pu), epilogue=_lib.EPI_RELU)
     else:
-        cf = Rows(ub.cf)
+        _conv(L, pu.convf1, flow, B, h, w, Rows(ub.flo1), epilogue=_lib.EPI_RELU, side=True)
+        _conv(L, pu.convf2, Rows(ub.flo1), B, h, w, cf.sub(192, 64), epilogue=_lib.EPI_RELU, side=True)
         _conv(L, pu.convc1, Rows(ub.corr), B, h, w, Rows(ub.cor1), epilogue=_lib.EPI_RELU)
         _conv(L, pu.convc2, Rows(ub.cor1), B, h, w, cf.sub(0, 192), epilogue=_lib.EPI_RELU)
-        _conv(L, pu.convf1, flow, B, h, w, Rows(ub.flo1), epilogue=_lib.EPI_RELU)
-        _conv(L, pu.convf2, Rows(ub.flo1), B, h, w, cf.sub(192, 64), epilogue=_lib.EPI_RELU)
-        _conv(L, pu.conv, cf, B, h, w, ub.motion(pu), epilogue=_lib.EPI_RELU)
+    L.append(K.JOIN)
+    _conv(L, pu.conv, cf, B, h, w, ub.motion(pu), epilogue=_lib.EPI_RELU)
     hd = pu.hdim
     hrows = ub.h(pu)
-    for zr, q in pu.gru:
-        _conv(L, zr, hx, B, h, w, Rows(ub.z), epilogue=_lib.EPI_GRU_ZR, split=hd, aux0=hrows, out1=Rows(ub.rh))
-        _conv(L, q, Rows(ub.rh), B, h, w, hrows, src1=ub.x(pu), epilogue=_lib.EPI_GRU_Q, aux0=hrows,
-              aux1=Rows(ub.z))
+    for (zr, q, _), ctx in zip(pu.gru, ub.ctx):
+        c = Rows(ctx)
+        _conv(L, zr, ub.gru_in(pu), B, h, w, Rows(ub.z), epilogue=_lib.EPI_GRU_ZR, split=hd, aux0=hrows,
+              out1=Rows(ub.rh), add0=c.sub(0, 2 * hd))
+        _conv(L, q, Rows(ub.rh), B, h, w, hrows, src1=ub.x_dyn(pu), epilogue=_lib.EPI_GRU_Q, aux0=hrows,
+              aux1=Rows(ub.z), add0=c.sub(2 * hd, hd))
     coords = Rows(ub.coords)
     if pu.small:
         _conv(L, pu.fh1, hrows, B, h, w, Rows(ub.fh), epilogue=_lib.EPI_RELU)
@@ -405,6 +430,7 @@ class RaftPlan:
         # context network (core/raft.py:193-200): tanh/relu split fused into its last conv
         xc, _, _ = plan_encoder_trunk(L, A, pk.cnet, Rows(prep.t[: B * H * W]), B, H, W)
         _conv(L, pk.cnet.head, xc, B, h, w, ub.h(pu), epilogue=_lib.EPI_TANH_RELU, split=pk.hdim, out1=ub.inp(pu))
+        plan_gru_context(L, pu, ub, B, h, w)
         L.append(Launch("raft_init_coords", ub.coords.data_ptr(),
                         self.flow_init.data_ptr() if self.flow_init is not None else None, B, h, w))
         self.loop_start = len(L)
@@ -434,12 +460,13 @@ class RaftPlan:
         self.flow_low = torch.empty(B, 2, h, w, device=device)
         L.append(Launch("raft_flow_from_coords", ub.coords.data_ptr(), self.flow_low.data_ptr(), B, h, w))
         self.graph = None
+        self.side_stream = None
 
     # -- execution --------------------------------------------------------
     def run(self):
-        s = K.stream_handle()
-        for l in self.launches:
-            l(s)
+        if self.side_stream is None:
+            self.side_stream = torch.cuda.Stream(device=self.device)
+        K.run(self.launches, self.side_stream)
 
     def capture(self):
         """Record the whole launch list into a hipGraph (static buffers, no allocation)."""
@@ -471,4 +498,4 @@ class RaftPlan:
         return [f(t) for t in self.flow_up]
 
     def kernel_names(self):
-        return [l.name for l in self.launches]
+        return [l.name for l in self.launches if isinstance(l, Launch)]

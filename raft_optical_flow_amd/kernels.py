@@ -136,7 +136,8 @@ def fold_bn(weight, bias, bn: torch.nn.BatchNorm2d):
 
 def conv_params(pc: PackedConv, src0: Rows, batch: int, in_h: int, in_w: int, out: Rows,
                 epilogue=_lib.EPI_LINEAR, src1: Rows | None = None, alpha=1.0, split=0,
-                aux0: Rows | None = None, aux1: Rows | None = None, out1: Rows | None = None) -> ConvParams:
+                aux0: Rows | None = None, aux1: Rows | None = None, out1: Rows | None = None,
+                add0: Rows | None = None) -> ConvParams:
     """Build (and validate shapes of) a raft_conv2d_params for one launch."""
     sh, sw = pc.stride
     ph, pw = pc.pad
@@ -148,7 +149,7 @@ def conv_params(pc: PackedConv, src0: Rows, batch: int, in_h: int, in_w: int, ou
     npix_in = batch * in_h * in_w
     npix_out = batch * out_h * out_w
     for r, n in ((src0, npix_in), (src1, npix_in), (out, npix_out), (aux0, npix_out), (aux1, npix_out),
-                 (out1, npix_out)):
+                 (out1, npix_out), (add0, npix_out)):
         if r is not None and r.t.shape[0] < n:
             raise ValueError(f"rows buffer has {r.t.shape[0]} pixels, need {n}")
     p = ConvParams()
@@ -169,6 +170,8 @@ def conv_params(pc: PackedConv, src0: Rows, batch: int, in_h: int, in_w: int, ou
         p.aux1, p.aux1_ld = aux1.ptr, aux1.ld
     if out1 is not None:
         p.out1, p.out1_ld = out1.ptr, out1.ld
+    if add0 is not None:
+        p.add0, p.add0_ld = add0.ptr, add0.ld
     return p
 
 
@@ -179,14 +182,15 @@ def conv_out_hw(pc: PackedConv, in_h: int, in_w: int):
 class Launch:
     """A pre-built kernel launch: fn(*args, stream)."""
 
-    __slots__ = ("fn", "args", "name", "keep")
+    __slots__ = ("fn", "args", "name", "keep", "side")
 
-    def __init__(self, name: str, *args, keep=None):
+    def __init__(self, name: str, *args, keep=None, side=False):
         lib = _lib.load()
         self.name = name
         self.fn = getattr(lib, name)
         self.args = args
         self.keep = keep  # objects whose lifetime the launch depends on (ConvParams structs)
+        self.side = side  # run on the plan's side stream (between a FORK and a JOIN)
 
     def __call__(self, stream: int):
         rc = self.fn(*self.args, stream)
@@ -194,14 +198,29 @@ class Launch:
             _lib.check(rc, self.name)
 
 
-def conv_launch(params: ConvParams) -> Launch:
-    return Launch("raft_conv2d", ctypes.byref(params), keep=params)
+def conv_launch(params: ConvParams, side=False) -> Launch:
+    return Launch("raft_conv2d", ctypes.byref(params), keep=params, side=side)
 
 
-def run(launches, stream: int | None = None):
-    s = stream_handle() if stream is None else stream
+FORK = "fork"   # side stream waits for the main stream
+JOIN = "join"   # main stream waits for the side stream
+
+
+def run(launches, side_stream: torch.cuda.Stream | None = None):
+    """Replay a launch list on the current stream; FORK/JOIN markers move the
+    `side` launches onto `side_stream` (captured as parallel graph branches)."""
+    main = torch.cuda.current_stream()
+    s = main.cuda_stream
+    ss = side_stream.cuda_stream if side_stream is not None else s
     for l in launches:
-        l(s)
+        if l is FORK:
+            if side_stream is not None:
+                side_stream.wait_stream(main)
+        elif l is JOIN:
+            if side_stream is not None:
+                main.wait_stream(side_stream)
+        else:
+            l(ss if l.side else s)
 
 
 # ----------------------------------------------------------------------------

@@ -73,7 +73,7 @@ class _UpdateBase(nn.Module):
     _small = False
 
     def forward(self, net, inp, corr, flow, upsample=True):
-        from .engine import Arena, PackedUpdate, UpdateBuffers, plan_update
+        from .engine import Arena, PackedUpdate, UpdateBuffers, plan_gru_context, plan_update
         K.require_device(net, inp, corr, flow)
         b, _, h, w = net.shape
         P = b * h * w
@@ -90,6 +90,7 @@ class _UpdateBase(nn.Module):
             _lib.check(lib.raft_nchw_to_nhwc(t.data_ptr(), rows.ptr, rows.ld, b, t.shape[1], h, w, s), "nchw_to_nhwc")
         ub.coords.zero_()  # coords1 += delta  ->  delta
         L = []
+        plan_gru_context(L, pu, ub, b, h, w)
         plan_update(L, pu, ub, b, h, w, with_mask=not self._small)
         K.run(L)
         net_out = K.rows_to_nchw(ub.h(pu), b, h, w)

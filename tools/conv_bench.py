@@ -1,0 +1,42 @@
+"""Time each update-block convolution shape of RAFT-full at B x 55 x 128 in isolation."""
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+from raft_optical_flow_amd import _lib
+from raft_optical_flow_amd import kernels as K
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+H, W = 55, 128
+dev = "cuda"
+SHAPES = [  # name, cin, cout, kh, kw, pad
+    ("convc1", 324, 256, 1, 1, (0, 0)), ("convc2", 256, 192, 3, 3, (1, 1)), ("convf2", 128, 64, 3, 3, (1, 1)),
+    ("conv", 256, 126, 3, 3, (1, 1)), ("zr", 384, 256, 1, 5, (0, 2)), ("q", 384, 128, 1, 5, (0, 2)),
+    ("fh1", 128, 256, 3, 3, (1, 1)), ("fh1mask", 128, 512, 3, 3, (1, 1)), ("mask2", 256, 576, 1, 1, (0, 0)),
+]
+tot_t = 0
+for name, cin, cout, kh, kw, pad in SHAPES:
+    x = torch.randn(B * H * W, cin, device=dev)
+    w = torch.randn(cout, cin, kh, kw) * 0.05
+    pc = K.pack_conv(w, torch.zeros(cout), 1, pad, device=dev)
+    out = torch.empty(B * H * W, cout, device=dev)
+    prm = K.conv_params(pc, K.Rows(x), B, H, W, K.Rows(out), epilogue=_lib.EPI_RELU)
+    L = [K.conv_launch(prm)]
+    s = K.stream_handle()
+    for _ in range(3):
+        L[0](s)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 50
+    e0.record()
+    for _ in range(reps):
+        L[0](s)
+    e1.record()
+    e1.synchronize()
+    us = e0.elapsed_time(e1) / reps * 1e3
+    fl = 2.0 * B * H * W * cout * cin * kh * kw
+    tot_t += us
+    print(f"{name:8s} M={B*H*W:6d} N={cout:4d} K={cin*kh*kw:5d}  {us:8.1f} us  {fl/us/1e6:7.1f} TF/s")
+print(f"total {tot_t:.1f} us")

@@ -1,0 +1,14 @@
+#!/bin/bash
+# GPU round trip used during development: parity tests, bench, kernel-trace profile.
+set -o pipefail
+cd "$(dirname "$0")/.."
+TAG=${1:-dev}
+timeout -k 10 500 python -m pytest tests/test_gpu_parity.py -q -m gpu -x > gpurun_out/gpu_$TAG.log 2>&1
+echo "tests rc=$?"; tail -3 gpurun_out/gpu_$TAG.log
+timeout -k 10 400 python bench.py --steps 20 --warmup 3 ${BENCH_ARGS} > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo bench failed; tail -20 gpurun_out/bench_$TAG.err; exit 1; }
+cat gpurun_out/bench_$TAG.json
+if [ -n "$PROFILE" ]; then
+  export TMPDIR=/tmp
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/prof_$TAG.log 2>&1
+  echo "prof rc=$?"
+fi
