@@ -1,0 +1,7 @@
+"""Shim for core/update.py -> raft_optical_flow_amd.update."""
+import os as _os
+import sys as _sys
+
+_sys.path.insert(0, _os.path.dirname(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))))
+from raft_optical_flow_amd.update import (  # noqa: E402,F401
+    BasicMotionEncoder, BasicUpdateBlock, ConvGRU, FlowHead, SepConvGRU, SmallMotionEncoder, SmallUpdateBlock)

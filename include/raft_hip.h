@@ -54,16 +54,22 @@ const char* raft_hip_last_error(void);  /* message of the last failure on this t
  * All-pairs correlation pyramid (CorrBlock)
  *
  * fmap1, fmap2: NHWC rows [B*H*W][ld] (channels 0..C-1 used, C % 4 == 0, 16-B aligned).
- * pyramid: num_levels levels stored back to back; level l is
- *   [B][H*W][H_l][W_l] with H_0 = H, H_{l+1} = floor(H_l / 2) (same for W),
- *   i.e. for query pixel p of batch b the level-l map starts at
- *   pyramid + off_l + (b*H*W + p) * H_l*W_l,  off_l = B*H*W * sum_{j<l} H_j*W_j.
+ * pyramid: num_levels levels stored back to back, H_0 = H, H_{l+1} = floor(H_l / 2)
+ *   (same for W).  Every query pixel's level-l map is stored in 4x4 TILES:
+ *   TH_l = ceil(H_l/4), TW_l = ceil(W_l/4), map size S_l = TH_l*TW_l*16 floats,
+ *   element (y, x) at ((y>>2)*TW_l + (x>>2))*16 + (y&3)*4 + (x&3), padding = 0;
+ *   the map of query pixel p of batch b starts at pyramid + off_l + (b*H*W + p)*S_l,
+ *   off_l = B*H*W * sum_{j<l} S_j.  (64-B tiles = the HBM read granule: a
+ *   radius-4 window touches ~10.6 tiles instead of ten straddling row runs.)
  * Level 0 = <fmap1[p], fmap2[q]> / sqrt_c (a division, as core/corr.py:127);
- * level l+1 = 2x2 average pool (floor) of level l.
+ * level l+1 = 2x2 average pool (floor) of level l.  16-byte aligned buffers.
  * --------------------------------------------------------------------------- */
 size_t raft_corr_pyramid_floats(int B, int H, int W, int num_levels);
 int raft_corr_build(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C,
                     int num_levels, float sqrt_c, float* pyramid, raft_stream_t stream);
+/* Row-major copy of one level, out [B*H*W][H_l][W_l] (the reference's corr_pyramid[l]). */
+int raft_corr_pyramid_level(const float* pyramid, int B, int H, int W, int num_levels, int level,
+                            float* out, raft_stream_t stream);
 
 /* Radius-r bilinear window lookup of every level (CorrBlock.__call__).
  * coords: (x, y) per query pixel; coords_layout 0 = NHWC [B*H*W][2],

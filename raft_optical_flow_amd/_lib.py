@@ -60,6 +60,7 @@ _PROTOS = {
     "raft_hip_last_error": (c_char_p, []),
     "raft_corr_pyramid_floats": (c_size_t, [c_int, c_int, c_int, c_int]),
     "raft_corr_build": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, P, P]),
+    "raft_corr_pyramid_level": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "raft_corr_lookup": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, c_int, c_int, P, c_int, P]),
     "raft_alt_corr_forward": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, P]),
     "raft_alt_corr_lookup_nhwc": (c_int, [P, P, P, c_int, c_float, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,

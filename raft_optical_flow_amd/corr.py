@@ -40,13 +40,20 @@ class CorrBlock:
         self.pyramid_flat = torch.empty(K.pyramid_floats(b, h, w, num_levels), device=fmap1.device)
         _lib.call("raft_corr_build", f1.data_ptr(), f2.data_ptr(), c, b, h, w, c, num_levels, K.sqrt_c(c),
                   self.pyramid_flat.data_ptr(), K.stream_handle())
-        # reference-shaped views: level i is [B*H*W, 1, H_i, W_i]
-        self.corr_pyramid = []
-        off = 0
-        for lh, lw in dims:
-            n = b * h * w * lh * lw
-            self.corr_pyramid.append(self.pyramid_flat[off:off + n].view(b * h * w, 1, lh, lw))
-            off += n
+        self._dims = dims
+
+    @property
+    def corr_pyramid(self):
+        """Reference-shaped copies of the levels, [B*H*W, 1, H_i, W_i] (the device
+        pyramid itself is stored in 4x4 tiles, include/raft_hip.h)."""
+        b, c, h, w = self.shape
+        out = []
+        for i, (lh, lw) in enumerate(self._dims):
+            t = torch.empty(b * h * w, 1, lh, lw, device=self.pyramid_flat.device)
+            _lib.call("raft_corr_pyramid_level", self.pyramid_flat.data_ptr(), b, h, w, self.num_levels, i,
+                      t.data_ptr(), K.stream_handle())
+            out.append(t)
+        return out
 
     def __call__(self, coords):
         K.require_device(coords)
@@ -65,7 +72,7 @@ class CorrBlock:
         """Level 0 of the volume, [B, H, W, 1, H, W] (core/corr.py:96-127)."""
         b, c, h, w = fmap1.shape
         cb = CorrBlock(fmap1, fmap2, num_levels=1, radius=1)
-        return cb.pyramid_flat.view(b, h, w, 1, h, w)
+        return cb.corr_pyramid[0].view(b, h, w, 1, h, w)
 
 
 class AlternateCorrBlock:

@@ -1,0 +1,326 @@
+// On-the-fly ("alternate") correlation of the alt_cuda_corr plugin and the NHWC
+// average pool of AlternateCorrBlock's feature pyramid (gfx950).
+#include "common.hpp"
+
+namespace raft {
+namespace {
+
+// ============================================================================
+// K3: on-the-fly correlation (alt_cuda_corr forward, correlation_kernel.cu:18-119)
+//
+// One wave per (query pixel, coordinate set).  fmap1[p] is held in registers,
+// 4 channels per lane per 256-channel slab.  The (2r+2)^2 integer taps
+// around floor(coords) - r are visited 64 at a time: every lane reads the
+// tap's fmap2 row slice (one coalesced 1 KiB read per tap per slab) and keeps
+// a private partial dot product per tap; a transposing butterfly (halving
+// exchange, 63 shuffles per 64 taps) leaves lane j holding tap j's full sum.
+// Tap sums go to LDS and the bilinear weights of frac(coords) scatter them
+// into the (2r+1)^2 bins exactly as the reference (bins gathered per lane).
+// ============================================================================
+struct AltArgs {
+  const float* f1;
+  const float* f2;
+  const float* coords;
+  int coords_layout;  // 0 = [B][N][H1][W1][2] (reference) / NHWC rows, 1 = NCHW [B][2][H1][W1]
+  float coord_div;
+  float* out;
+  int out_layout;  // 0 = [B][N][RD^2][H1][W1] (reference), 1 = NHWC rows out_ld
+  int out_ld;
+  int B, H1, W1, H2, W2, C, N, r;
+  float scale_div;
+  float* flow;
+  int flow_ld;
+};
+
+template <int NV>
+__device__ __forceinline__ float tap_partial(const f32x4 (&f1)[NV], const float* row, int lane, int C) {
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = k * 256 + lane * 4;
+    if (c < C) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(row + c);
+      s += f1[k][0] * v[0] + f1[k][1] * v[1] + f1[k][2] * v[2] + f1[k][3] * v[3];
+    }
+  }
+  return s;
+}
+
+// Reduce v[0..63] (one partial per tap, per lane) so that lane j ends with sum over lanes of v[j].
+__device__ __forceinline__ float transpose_reduce64(float (&v)[64], int lane) {
+#pragma unroll
+  for (int half = 32; half >= 1; half >>= 1) {
+    const bool hi = (lane & half) != 0;
+#pragma unroll
+    for (int i = 0; i < half; ++i) {
+      const float keep = hi ? v[i + half] : v[i];
+      const float send = hi ? v[i] : v[i + half];
+      v[i] = keep + __shfl_xor(send, half);
+    }
+  }
+  return v[0];
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void alt_corr_kernel(AltArgs a) {
+  __shared__ float tapsum[4][128];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int P1 = a.H1 * a.W1;
+  const long gid = (long)blockIdx.x * 4 + wv;  // ((b*N + n)*P1 + p)
+  const bool valid = gid < (long)a.B * a.N * P1;
+  const long bn = valid ? gid / P1 : 0;
+  const int p = valid ? (int)(gid - bn * P1) : 0;
+  const int b = (int)(bn / a.N);
+  const int rd = 2 * a.r + 1, wd = 2 * a.r + 2, ntaps = wd * wd;
+
+  float x = 0.f, y = 0.f;
+  if (valid) {
+    if (a.coords_layout == 0) {
+      x = a.coords[2 * gid];
+      y = a.coords[2 * gid + 1];
+    } else {
+      x = a.coords[((long)b * 2) * P1 + p];
+      y = a.coords[((long)b * 2 + 1) * P1 + p];
+    }
+    x = x / a.coord_div;
+    y = y / a.coord_div;
+  }
+  const float fx = floorf(x), fy = floorf(y);
+  const float dx = x - fx, dy = y - fy;
+  const int x0 = (int)fx - a.r, y0 = (int)fy - a.r;
+
+  f32x4 f1[NV];
+  const float* f1row = a.f1 + ((long)b * P1 + p) * a.C;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = k * 256 + lane * 4;
+    f1[k] = (valid && c < a.C) ? *reinterpret_cast<const f32x4*>(f1row + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const float* f2b = a.f2 + (long)b * a.H2 * a.W2 * a.C;
+  for (int g = 0; g < ntaps; g += 64) {
+    float v[64];
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+      const int t = g + j;
+      const int iy = t / wd, ix = t - iy * wd;
+      const int h2 = y0 + iy, w2 = x0 + ix;
+      float s = 0.f;
+      if (valid && t < ntaps && h2 >= 0 && h2 < a.H2 && w2 >= 0 && w2 < a.W2)
+        s = tap_partial<NV>(f1, f2b + ((long)h2 * a.W2 + w2) * a.C, lane, a.C);
+      v[j] = s;
+    }
+    const float tot = transpose_reduce64(v, lane);
+    if (g + lane < ntaps) tapsum[wv][g + lane] = tot;
+  }
+  __syncthreads();
+  if (!valid) return;
+  for (int o = lane; o < rd * rd; o += 64) {
+    const int ox = o / rd, oy = o - ox * rd;  // channel = oy + rd*ox
+    const float* ts = tapsum[wv];
+    const float s00 = ts[oy * wd + ox], s01 = ts[oy * wd + ox + 1];
+    const float s10 = ts[(oy + 1) * wd + ox], s11 = ts[(oy + 1) * wd + ox + 1];
+    float val = s00 * ((1.f - dy) * (1.f - dx));
+    val += s01 * ((1.f - dy) * dx);
+    val += s10 * (dy * (1.f - dx));
+    val += s11 * (dy * dx);
+    val = val / a.scale_div;
+    if (a.out_layout == 0)
+      a.out[(bn * (rd * rd) + o) * P1 + p] = val;
+    else
+      a.out[((long)b * P1 + p) * a.out_ld + o] = val;
+  }
+  if (a.flow && lane < 2) {
+    const float gx = lane == 0 ? (float)(p % a.W1) : (float)(p / a.W1);
+    a.flow[((long)b * P1 + p) * a.flow_ld + lane] = (lane == 0 ? x : y) * a.coord_div - gx;
+  }
+}
+
+int launch_alt(const AltArgs& a, raft_stream_t stream) {
+  const long waves = (long)a.B * a.N * a.H1 * a.W1;
+  dim3 grid((unsigned)cdiv_l(waves, 4));
+  hipStream_t s = as_stream(stream);
+  if (a.C <= 256)
+    hipLaunchKernelGGL(alt_corr_kernel<1>, grid, dim3(256), 0, s, a);
+  else if (a.C <= 512)
+    hipLaunchKernelGGL(alt_corr_kernel<2>, grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(alt_corr_kernel<4>, grid, dim3(256), 0, s, a);
+  return check_launch("raft_alt_corr");
+}
+
+// ---------------------------------------------------------------------------
+// alt backward (training path, correlation_kernel.cu:122-256):
+// g(tap) = sum of the corr_grad bins the tap fed, weighted as in forward;
+// fmap1_grad[p] = sum_tap g * fmap2[tap] (gather, deterministic);
+// fmap2_grad[q] += g * fmap1[p] (float atomics, as the reference).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void alt_corr_bwd_kernel(const float* f1, const float* f2, const float* coords,
+                                                         const float* cg, float* f1g, float* f2g, int B, int H1,
+                                                         int W1, int H2, int W2, int C, int N, int r) {
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int P1 = H1 * W1;
+  const long gid = (long)blockIdx.x * 4 + wv;  // b*P1 + p
+  if (gid >= (long)B * P1) return;
+  const int b = (int)(gid / P1);
+  const int p = (int)(gid - (long)b * P1);
+  const int rd = 2 * r + 1, wd = 2 * r + 2;
+  for (int c0 = lane * 4; c0 < C; c0 += 256) {
+    f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 a1 = *reinterpret_cast<const f32x4*>(f1 + gid * C + c0);
+    for (int n = 0; n < N; ++n) {
+      const long bn = (long)b * N + n;
+      const float x = coords[2 * (bn * P1 + p)], y = coords[2 * (bn * P1 + p) + 1];
+      const float fx = floorf(x), fy = floorf(y);
+      const float dx = x - fx, dy = y - fy;
+      const int x0 = (int)fx - r, y0 = (int)fy - r;
+      const float* g = cg + bn * rd * rd * P1 + p;
+      for (int iy = 0; iy < wd; ++iy) {
+        for (int ix = 0; ix < wd; ++ix) {
+          const int h2 = y0 + iy, w2 = x0 + ix;
+          if (h2 < 0 || h2 >= H2 || w2 < 0 || w2 >= W2) continue;
+          float gt = 0.f;
+          if (iy > 0 && ix > 0) gt += g[(long)((iy - 1) + rd * (ix - 1)) * P1] * dy * dx;
+          if (iy > 0 && ix < rd) gt += g[(long)((iy - 1) + rd * ix) * P1] * dy * (1.f - dx);
+          if (iy < rd && ix > 0) gt += g[(long)(iy + rd * (ix - 1)) * P1] * (1.f - dy) * dx;
+          if (iy < rd && ix < rd) gt += g[(long)(iy + rd * ix) * P1] * (1.f - dy) * (1.f - dx);
+          float* q2 = f2g + (((long)b * H2 + h2) * W2 + w2) * C + c0;
+          const f32x4 b2 = *reinterpret_cast<const f32x4*>(f2 + (((long)b * H2 + h2) * W2 + w2) * C + c0);
+          acc1 += gt * b2;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) atomicAdd(q2 + j, gt * a1[j]);
+        }
+      }
+    }
+    *reinterpret_cast<f32x4*>(f1g + gid * C + c0) = acc1;
+  }
+}
+
+__global__ void zero_kernel(float* p, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) p[i] = 0.f;
+}
+
+__global__ void avgpool2_nhwc_kernel(const float* in, float* out, int B, int H, int W, int C, int Ho, int Wo) {
+  const long total = (long)B * Ho * Wo * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = i % C;
+    long t = i / C;
+    const int x = t % Wo;
+    t /= Wo;
+    const int y = t % Ho;
+    const int b = t / Ho;
+    const float* p = in + (((long)b * H + 2 * y) * W + 2 * x) * C + c;
+    out[i] = (((p[0] + p[C]) + p[(long)W * C]) + p[(long)W * C + C]) / 4.0f;
+  }
+}
+
+}  // namespace
+}  // namespace raft
+
+using namespace raft;
+
+static int grid_for(long n, int block = 256) {
+  long g = (n + block - 1) / block;
+  if (g > 65536) g = 65536;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+static int alt_checks(const float* f1, const float* f2, const float* coords, const float* out, int B, int H1, int W1,
+                      int H2, int W2, int C, int N, int r) {
+  RAFT_REQUIRE(f1 && f2 && coords && out, "raft_alt_corr: null pointer");
+  RAFT_REQUIRE(B > 0 && H1 > 0 && W1 > 0 && H2 > 0 && W2 > 0 && C > 0 && N > 0, "raft_alt_corr: bad sizes");
+  RAFT_REQUIRE(C % 4 == 0 && C <= 1024, "raft_alt_corr: C must be a multiple of 4 and <= 1024 (got %d)", C);
+  RAFT_REQUIRE(r >= 0 && (2 * r + 2) * (2 * r + 2) <= 128, "raft_alt_corr: radius must be 0..4 (got %d)", r);
+  RAFT_REQUIRE((((uintptr_t)f1 | (uintptr_t)f2) & 15) == 0, "raft_alt_corr: fmaps must be 16-byte aligned");
+  return 0;
+}
+
+extern "C" int raft_alt_corr_forward(const float* fmap1, const float* fmap2, const float* coords, float* corr, int B,
+                                     int H1, int W1, int H2, int W2, int C, int N, int radius, float scale_div,
+                                     raft_stream_t stream) {
+  int rc = alt_checks(fmap1, fmap2, coords, corr, B, H1, W1, H2, W2, C, N, radius);
+  if (rc) return rc;
+  AltArgs a;
+  a.f1 = fmap1;
+  a.f2 = fmap2;
+  a.coords = coords;
+  a.coords_layout = 0;
+  a.coord_div = 1.0f;
+  a.out = corr;
+  a.out_layout = 0;
+  a.out_ld = 0;
+  a.B = B;
+  a.H1 = H1;
+  a.W1 = W1;
+  a.H2 = H2;
+  a.W2 = W2;
+  a.C = C;
+  a.N = N;
+  a.r = radius;
+  a.scale_div = scale_div;
+  a.flow = nullptr;
+  a.flow_ld = 0;
+  return launch_alt(a, stream);
+}
+
+extern "C" int raft_alt_corr_lookup_nhwc(const float* fmap1, const float* fmap2, const float* coords,
+                                         int coords_layout, float coord_div, float* out, int out_ld, int B, int H1,
+                                         int W1, int H2, int W2, int C, int radius, float scale_div, float* flow_out,
+                                         int flow_ld, raft_stream_t stream) {
+  int rc = alt_checks(fmap1, fmap2, coords, out, B, H1, W1, H2, W2, C, 1, radius);
+  if (rc) return rc;
+  RAFT_REQUIRE(coords_layout == 0 || coords_layout == 1, "raft_alt_corr_lookup_nhwc: bad coords_layout");
+  RAFT_REQUIRE(coord_div > 0.f, "raft_alt_corr_lookup_nhwc: coord_div must be > 0");
+  RAFT_REQUIRE(out_ld >= (2 * radius + 1) * (2 * radius + 1), "raft_alt_corr_lookup_nhwc: out_ld too small");
+  AltArgs a;
+  a.f1 = fmap1;
+  a.f2 = fmap2;
+  a.coords = coords;
+  a.coords_layout = coords_layout;
+  a.coord_div = coord_div;
+  a.out = out;
+  a.out_layout = 1;
+  a.out_ld = out_ld;
+  a.B = B;
+  a.H1 = H1;
+  a.W1 = W1;
+  a.H2 = H2;
+  a.W2 = W2;
+  a.C = C;
+  a.N = 1;
+  a.r = radius;
+  a.scale_div = scale_div;
+  a.flow = flow_out;
+  a.flow_ld = flow_ld;
+  return launch_alt(a, stream);
+}
+
+extern "C" size_t raft_alt_corr_backward_workspace_floats(int, int, int, int, int, int, int, int) { return 0; }
+
+extern "C" int raft_alt_corr_backward(const float* fmap1, const float* fmap2, const float* coords,
+                                      const float* corr_grad, float* fmap1_grad, float* fmap2_grad,
+                                      float* coords_grad, int B, int H1, int W1, int H2, int W2, int C, int N,
+                                      int radius, float*, size_t, raft_stream_t stream) {
+  int rc = alt_checks(fmap1, fmap2, coords, corr_grad, B, H1, W1, H2, W2, C, N, radius);
+  if (rc) return rc;
+  RAFT_REQUIRE(fmap1_grad && fmap2_grad && coords_grad, "raft_alt_corr_backward: null gradient pointer");
+  hipStream_t s = as_stream(stream);
+  const long n2 = (long)B * H2 * W2 * C;
+  const long nc = (long)B * N * H1 * W1 * 2;
+  hipLaunchKernelGGL(zero_kernel, dim3(grid_for(n2)), dim3(256), 0, s, fmap2_grad, n2);
+  hipLaunchKernelGGL(zero_kernel, dim3(grid_for(nc)), dim3(256), 0, s, coords_grad, nc);
+  hipLaunchKernelGGL(alt_corr_bwd_kernel, dim3((unsigned)cdiv_l((long)B * H1 * W1, 4)), dim3(256), 0, s, fmap1,
+                     fmap2, coords, corr_grad, fmap1_grad, fmap2_grad, B, H1, W1, H2, W2, C, N, radius);
+  return check_launch("raft_alt_corr_backward");
+}
+
+extern "C" int raft_avgpool2_nhwc(const float* in, float* out, int B, int H, int W, int C, raft_stream_t stream) {
+  RAFT_REQUIRE(in && out && B > 0 && H >= 2 && W >= 2 && C > 0, "raft_avgpool2_nhwc: bad arguments");
+  const int Ho = H / 2, Wo = W / 2;
+  const long n = (long)B * Ho * Wo * C;
+  hipLaunchKernelGGL(avgpool2_nhwc_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), in, out, B, H, W, C,
+                     Ho, Wo);
+  return check_launch("raft_avgpool2_nhwc");
+}

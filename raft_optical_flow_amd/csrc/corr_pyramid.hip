@@ -1,0 +1,473 @@
+// All-pairs correlation pyramid and its radius-r window lookup (gfx950).
+//
+// Pyramid layout (include/raft_hip.h): every query pixel's level-l map is
+// stored as 4x4 tiles of 16 floats (64 B = one HBM read granule), tiles
+// row-major, zero in the padding beyond H_l x W_l.  A 10x10 lookup window
+// then touches 3.25^2 ~ 10.6 tiles on average (~680 B) instead of ten
+// row-major 40-B runs that straddle 64-B sectors (~1050 B measured): the
+// lookup is a gather whose cost is the bytes it drags in.
+#include "common.hpp"
+
+namespace raft {
+namespace {
+
+constexpr int LK_MAXL = 6;
+
+struct Level {
+  int h, w;       // valid size
+  int th, tw;     // tiles
+  long off;       // float offset of the level in the pyramid
+  long mapsz;     // floats per query pixel (th*tw*16)
+};
+
+__host__ __device__ inline long tiled_index(int y, int x, int tw) {
+  return ((long)(y >> 2) * tw + (x >> 2)) * 16 + (y & 3) * 4 + (x & 3);
+}
+
+// ============================================================================
+// K2: all-pairs correlation volume + levels 0 and 1
+//     (CorrBlock.corr core/corr.py:96-127 and CorrBlock.__init__ :25-54)
+//
+// GEMM per batch b: C[p1, p2] = <fmap1[p1], fmap2[p2]> / sqrt_c (a division,
+// as the reference), M = N = H*W, K = C, on fp32 MFMA 32x32x2.  The N tile is
+// an 8x8 block of the (h2, w2) grid: its epilogue writes 2x2 whole level-0
+// tiles (two 128-B runs per query pixel) and pools the block into one whole
+// level-1 tile.  Deeper levels come from pool2_tiled_kernel.
+// ============================================================================
+constexpr int CB_BM = 64, CB_BN = 64, CB_BK = 32, CB_LDSK = CB_BK + 4;
+
+struct CorrBuildArgs {
+  const float* f1;
+  const float* f2;
+  int ld, H, W, C, P;
+  float sqrt_c;
+  float* pyr;
+  Level l0, l1;
+  int has_l1;
+  int nbx;  // 8x8 blocks along w2
+};
+
+__global__ __launch_bounds__(256) void corr_build_kernel(CorrBuildArgs a) {
+  constexpr int STAGE = (CB_BM + CB_BN) * CB_LDSK;
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int b = blockIdx.z;
+  const int m0 = blockIdx.x * CB_BM;
+  const int by = blockIdx.y / a.nbx, bx = blockIdx.y - (blockIdx.y / a.nbx) * a.nbx;
+
+  const int lr = tid >> 3, lq = tid & 7;
+  const float* arow[2];
+  const float* brow[2];
+  bool av_[2], bv_[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = lr + 32 * i;
+    const int p1 = m0 + r;
+    av_[i] = p1 < a.P;
+    arow[i] = a.f1 + ((long)b * a.P + (av_[i] ? p1 : 0)) * a.ld + lq * 4;
+    const int h2 = by * 8 + (r >> 3), w2 = bx * 8 + (r & 7);
+    bv_[i] = h2 < a.H && w2 < a.W;
+    brow[i] = a.f2 + ((long)b * a.P + (bv_[i] ? h2 * a.W + w2 : 0)) * a.ld + lq * 4;
+  }
+  f32x4 ra[2], rb[2];
+  auto gload = [&](int kc) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      const bool cin = kc * CB_BK + lq * 4 < a.C;  // C % 4 == 0; zero-fill the K tail
+      ra[i] = (av_[i] && cin) ? *reinterpret_cast<const f32x4*>(arow[i] + kc * CB_BK) : z;
+      rb[i] = (bv_[i] && cin) ? *reinterpret_cast<const f32x4*>(brow[i] + kc * CB_BK) : z;
+    }
+  };
+  auto sstore = [&](int buf) {
+    float* A = smem + buf * STAGE;
+    float* Bt = A + CB_BM * CB_LDSK;
+    *reinterpret_cast<f32x4*>(A + lr * CB_LDSK + lq * 4) = ra[0];
+    *reinterpret_cast<f32x4*>(A + (lr + 32) * CB_LDSK + lq * 4) = ra[1];
+    *reinterpret_cast<f32x4*>(Bt + lr * CB_LDSK + lq * 4) = rb[0];
+    *reinterpret_cast<f32x4*>(Bt + (lr + 32) * CB_LDSK + lq * 4) = rb[1];
+  };
+  const int nk = cdiv(a.C, CB_BK);
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  f32x16 acc = {};
+  const int ao = (wm * 32 + (lane & 31)) * CB_LDSK + (lane >> 5) * 16;
+  const int bo = (wn * 32 + (lane & 31)) * CB_LDSK + (lane >> 5) * 16;
+  for (int kc = 0; kc < nk; ++kc) {
+    const int cur = kc & 1;
+    const bool more = kc + 1 < nk;
+    if (more) gload(kc + 1);
+    const float* A = smem + cur * STAGE;
+    const float* Bt = A + CB_BM * CB_LDSK;
+    f32x4 x[4], y[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      x[j] = *reinterpret_cast<const f32x4*>(A + ao + 4 * j);
+      y[j] = *reinterpret_cast<const f32x4*>(Bt + bo + 4 * j);
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x[s >> 2][s & 3], y[s >> 2][s & 3], acc, 0, 0, 0);
+    if (more) sstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: scaled tile -> LDS T[64 p1][64 = 8 rows x 8 cols of the (h2, w2) block]
+  constexpr int TLD = CB_BN + 1;
+  float* T = smem;
+  {
+    const int n = wn * 32 + (lane & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      T[row * TLD + n] = acc[r] / a.sqrt_c;  // positions outside H x W are exact zeros
+    }
+  }
+  __syncthreads();
+  // level 0: tiles (2by + i, 2bx + j); the two tiles of a tile row are adjacent (128 B)
+  for (int idx = tid; idx < CB_BM * 64; idx += 256) {
+    const int row = idx >> 6, o = idx & 63;
+    const int p1 = m0 + row;
+    const int ti = o >> 5, tj = (o >> 4) & 1, e = o & 15;
+    const int ty = 2 * by + ti, tx = 2 * bx + tj;
+    if (p1 < a.P && ty < a.l0.th && tx < a.l0.tw) {
+      const int n = (ti * 4 + (e >> 2)) * 8 + tj * 4 + (e & 3);
+      a.pyr[a.l0.off + ((long)b * a.P + p1) * a.l0.mapsz + ((long)ty * a.l0.tw + tx) * 16 + e] = T[row * TLD + n];
+    }
+  }
+  if (a.has_l1 && by < a.l1.th && bx < a.l1.tw) {
+    // level 1: the block pooled 2x2 -> one whole 4x4 tile (zeros beyond H1 x W1)
+    for (int idx = tid; idx < CB_BM * 16; idx += 256) {
+      const int row = idx >> 4, e = idx & 15;
+      const int p1 = m0 + row;
+      if (p1 >= a.P) continue;
+      const int yy = e >> 2, xx = e & 3;
+      float v = 0.f;
+      if (by * 4 + yy < a.l1.h && bx * 4 + xx < a.l1.w) {
+        const float* t = T + row * TLD + (2 * yy) * 8 + 2 * xx;
+        v = (((t[0] + t[1]) + t[8]) + t[9]) / 4.0f;  // avg_pool2d window order
+      }
+      a.pyr[a.l1.off + ((long)b * a.P + p1) * a.l1.mapsz + ((long)by * a.l1.tw + bx) * 16 + e] = v;
+    }
+  }
+}
+
+// Level l -> l+1 2x2 average pool (floor), tiled -> tiled, zeros in the padding.
+__global__ void pool2_tiled_kernel(const float* pyr, float* out_base, long n_maps, Level src,
+                                   Level dst) {
+  const long total = n_maps * dst.mapsz;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long q = i / dst.mapsz;
+    const int r = (int)(i - q * dst.mapsz);
+    const int tile = r >> 4, e = r & 15;
+    const int y = (tile / dst.tw) * 4 + (e >> 2), x = (tile % dst.tw) * 4 + (e & 3);
+    float v = 0.f;
+    if (y < dst.h && x < dst.w) {
+      const float* m = pyr + src.off + q * src.mapsz;
+      const float a0 = m[tiled_index(2 * y, 2 * x, src.tw)];
+      const float a1 = m[tiled_index(2 * y, 2 * x + 1, src.tw)];
+      const float a2 = m[tiled_index(2 * y + 1, 2 * x, src.tw)];
+      const float a3 = m[tiled_index(2 * y + 1, 2 * x + 1, src.tw)];
+      v = (((a0 + a1) + a2) + a3) / 4.0f;
+    }
+    out_base[dst.off + i] = v;
+  }
+}
+
+// Tiled -> row-major copy of one level (API accessor CorrBlock.corr_pyramid).
+__global__ void untile_kernel(const float* __restrict__ pyr, float* __restrict__ out, long n_maps, Level lv) {
+  const long total = n_maps * lv.h * lv.w;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int x = i % lv.w;
+    const long t = i / lv.w;
+    const int y = t % lv.h;
+    const long q = t / lv.h;
+    out[i] = pyr[lv.off + q * lv.mapsz + tiled_index(y, x, lv.tw)];
+  }
+}
+
+// ============================================================================
+// K1: radius-r lookup of every level (CorrBlock.__call__ core/corr.py:56-94)
+//
+// One wave per query pixel.  Phase 1: per level, the <= 4x4 tiles that cover
+// the (2r+2)^2 integer window around floor(coords/2^l) - r are read with one
+// 16-B load per lane (lane = tile row; tiles outside the window or the map are
+// skipped / zero) — all levels' loads in flight together — and staged as a
+// 16x16 LDS patch.  Phase 2: each lane evaluates taps of the (2r+1)^2 x L
+// output with the reference's arithmetic (offset added to the centroid, then
+// bilinear_sampler's 2x/(W-1)-1 and grid_sample's (g+1)*((W-1)/2)), so corner
+// indices and weights are the reference's; corners come from the LDS patch
+// (or from global memory when the float round trip moved a tap's floor off
+// it).  Output channel = lvl*(2r+1)^2 + ix*(2r+1) + iy, contiguous per pixel.
+// ============================================================================
+struct LookupArgs {
+  const float* pyr;
+  Level lv[LK_MAXL];
+  int B, H, W, L, r;
+  const float* coords;
+  int coords_layout;
+  float* out;
+  int out_ld, out_layout;
+  float* flow;
+  int flow_ld;
+};
+
+__device__ __forceinline__ void load_coords(const float* c, int layout, int b, int p, int P, float& x, float& y) {
+  if (layout == 0) {
+    x = c[2L * ((long)b * P + p)];
+    y = c[2L * ((long)b * P + p) + 1];
+  } else {
+    x = c[((long)b * 2) * P + p];
+    y = c[((long)b * 2 + 1) * P + p];
+  }
+}
+
+// q = a / b correctly rounded for normal operands, given rcp = RN(1/b): one
+// Newton step on the residual (Markstein); avoids the div_scale/div_fixup path.
+__device__ __forceinline__ float div_rn(float a, float b, float rcp) {
+  const float q = a * rcp;
+  const float r = fmaf(-q, b, a);
+  return fmaf(r, rcp, q);
+}
+
+template <int R, int LMAX>
+__global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
+  constexpr int RD = 2 * R + 1;
+  constexpr int WD = 2 * R + 2;  // integer window (<= 10 -> <= 4 tiles per axis)
+  static_assert(WD <= 13, "window must fit 4 tiles");
+  __shared__ __attribute__((aligned(16))) float patch[4][LMAX][16 * 16];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int P = a.H * a.W;
+  const long gp = (long)blockIdx.x * 4 + wv;  // global pixel index b*P + p
+  const bool valid = gp < (long)a.B * P;
+  const int b = valid ? (int)(gp / P) : 0;
+  const int p = valid ? (int)(gp - (long)b * P) : 0;
+  float x = 0.f, y = 0.f;
+  if (valid) load_coords(a.coords, a.coords_layout, b, p, P, x, y);
+
+  // lane -> (tile row ti, tile col tj, row-in-tile rr) of the 4x4-tile patch
+  const int ti = lane >> 4, tj = (lane >> 2) & 3, rr = lane & 3;
+  f32x4 v[LMAX];
+  int tyo[LMAX], txo[LMAX];
+#pragma unroll
+  for (int l = 0; l < LMAX; ++l) {
+    const float s = 1.0f / (float)(1 << l);  // coords / 2**l (exact power-of-two scaling)
+    const int x0 = (int)floorf(x * s) - R, y0 = (int)floorf(y * s) - R;
+    tyo[l] = y0 >> 2;  // arithmetic shift = floor division by 4 (negative too)
+    txo[l] = x0 >> 2;
+    const int nty = ((y0 + WD - 1) >> 2) - tyo[l] + 1;  // tiles the window needs (3 or 4)
+    const int ntx = ((x0 + WD - 1) >> 2) - txo[l] + 1;
+    const int ty = tyo[l] + ti, tx = txo[l] + tj;
+    const Level& lv = a.lv[l];
+    f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    if (l < a.L && valid && ti < nty && tj < ntx && (unsigned)ty < (unsigned)lv.th && (unsigned)tx < (unsigned)lv.tw)
+      z = *reinterpret_cast<const f32x4*>(a.pyr + lv.off + gp * lv.mapsz + ((long)ty * lv.tw + tx) * 16 + rr * 4);
+    v[l] = z;
+  }
+#pragma unroll
+  for (int l = 0; l < LMAX; ++l)
+    *reinterpret_cast<f32x4*>(&patch[wv][l][(ti * 4 + rr) * 16 + tj * 4]) = v[l];
+  __syncthreads();
+  if (!valid) return;
+
+  const int ntap = a.L * RD * RD;
+  for (int t = lane; t < ntap; t += 64) {
+    const int l = t / (RD * RD);
+    const int tt = t - l * RD * RD;
+    const int ix = tt / RD, iy = tt - ix * RD;
+    const float s = 1.0f / (float)(1 << l);
+    const float cx = x * s, cy = y * s;
+    const Level& lv = a.lv[l];
+    // patch origin and extent of the tiles phase 1 loaded for this level
+    const int x0 = (int)floorf(cx) - R, y0 = (int)floorf(cy) - R;
+    const int px0 = (x0 >> 2) * 4, py0 = (y0 >> 2) * 4;
+    const int pw = (((x0 + WD - 1) >> 2) - (x0 >> 2) + 1) * 4, ph = (((y0 + WD - 1) >> 2) - (y0 >> 2) + 1) * 4;
+    const float X = cx + (float)(ix - R);
+    const float Y = cy + (float)(iy - R);
+    const float wm1 = (float)(lv.w - 1), hm1 = (float)(lv.h - 1);
+    const float gx = div_rn(2.0f * X, wm1, 1.0f / wm1) - 1.0f;
+    const float gy = div_rn(2.0f * Y, hm1, 1.0f / hm1) - 1.0f;
+    const float ux = (gx + 1.0f) * (wm1 * 0.5f);
+    const float uy = (gy + 1.0f) * (hm1 * 0.5f);
+    float val;
+    if (!(isfinite(ux) && isfinite(uy))) {
+      val = __builtin_nanf("");
+    } else {
+      const float fx0 = floorf(ux), fy0 = floorf(uy);
+      const float tx = ux - fx0, ty = uy - fy0;
+      const int xi = (int)fx0, yi = (int)fy0;
+      const int wx = xi - px0, wy = yi - py0;
+      float vnw, vne, vsw, vse;
+      if (wx >= 0 && wx + 1 < pw && wy >= 0 && wy + 1 < ph) {
+        const float* w = &patch[wv][l][wy * 16 + wx];
+        vnw = w[0];
+        vne = w[1];
+        vsw = w[16];
+        vse = w[17];
+      } else {  // the float round trip moved this tap's floor off the staged patch
+        const float* m = a.pyr + lv.off + gp * lv.mapsz;
+        auto at = [&](int yy, int xx) {
+          return ((unsigned)yy < (unsigned)lv.h && (unsigned)xx < (unsigned)lv.w) ? m[tiled_index(yy, xx, lv.tw)]
+                                                                                  : 0.f;
+        };
+        vnw = at(yi, xi);
+        vne = at(yi, xi + 1);
+        vsw = at(yi + 1, xi);
+        vse = at(yi + 1, xi + 1);
+      }
+      const float e = 1.0f - tx, sS = 1.0f - ty;
+      val = vnw * (sS * e) + vne * (sS * tx) + vsw * (ty * e) + vse * (ty * tx);
+    }
+    if (a.out_layout == 0)
+      a.out[gp * a.out_ld + t] = val;
+    else
+      a.out[((long)b * ntap + t) * P + p] = val;
+  }
+  if (a.flow && lane < 2) {
+    const float g = lane == 0 ? (float)(p % a.W) : (float)(p / a.W);
+    a.flow[gp * a.flow_ld + lane] = (lane == 0 ? x : y) - g;
+  }
+}
+
+int grid_for(long n, int block = 256) {
+  long g = (n + block - 1) / block;
+  if (g > 65536) g = 65536;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+// level geometry; returns false if a level is empty
+bool pyramid_levels(int B, int H, int W, int L, Level* lv) {
+  long off = 0;
+  int h = H, w = W;
+  const long P = (long)H * W;
+  for (int l = 0; l < L; ++l) {
+    if (h < 1 || w < 1) return false;
+    lv[l].h = h;
+    lv[l].w = w;
+    lv[l].th = cdiv(h, 4);
+    lv[l].tw = cdiv(w, 4);
+    lv[l].mapsz = (long)lv[l].th * lv[l].tw * 16;
+    lv[l].off = off;
+    off += (long)B * P * lv[l].mapsz;
+    h /= 2;
+    w /= 2;
+  }
+  return true;
+}
+
+}  // namespace
+}  // namespace raft
+
+using namespace raft;
+
+extern "C" size_t raft_corr_pyramid_floats(int B, int H, int W, int L) {
+  if (B <= 0 || H <= 0 || W <= 0 || L <= 0 || L > LK_MAXL) return 0;
+  Level lv[LK_MAXL];
+  if (!pyramid_levels(B, H, W, L, lv)) return 0;
+  return (size_t)(lv[L - 1].off + (long)B * H * W * lv[L - 1].mapsz);
+}
+
+extern "C" int raft_corr_build(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C, int L,
+                               float sqrt_c, float* pyramid, raft_stream_t stream) {
+  RAFT_REQUIRE(fmap1 && fmap2 && pyramid, "raft_corr_build: null pointer");
+  RAFT_REQUIRE(B > 0 && H > 0 && W > 0 && C > 0 && L >= 1 && L <= LK_MAXL, "raft_corr_build: bad sizes");
+  RAFT_REQUIRE(C % 4 == 0, "raft_corr_build: C must be a multiple of 4 (got %d)", C);
+  RAFT_REQUIRE(ld % 4 == 0 && ld >= C, "raft_corr_build: ld must be >= C and a multiple of 4");
+  RAFT_REQUIRE((((uintptr_t)fmap1 | (uintptr_t)fmap2 | (uintptr_t)pyramid) & 15) == 0,
+               "raft_corr_build: fmaps and pyramid must be 16-byte aligned");
+  Level lv[LK_MAXL];
+  RAFT_REQUIRE(pyramid_levels(B, H, W, L, lv), "raft_corr_build: a pyramid level is empty (%dx%d, %d levels)", H, W, L);
+  const long P = (long)H * W;
+  CorrBuildArgs a;
+  a.f1 = fmap1;
+  a.f2 = fmap2;
+  a.ld = ld;
+  a.H = H;
+  a.W = W;
+  a.C = C;
+  a.P = (int)P;
+  a.sqrt_c = sqrt_c;
+  a.pyr = pyramid;
+  a.l0 = lv[0];
+  a.has_l1 = L > 1;
+  a.l1 = lv[L > 1 ? 1 : 0];
+  a.nbx = cdiv(W, 8);
+  hipStream_t s = as_stream(stream);
+  dim3 grid(cdiv((int)P, CB_BM), cdiv(H, 8) * a.nbx, B);
+  hipLaunchKernelGGL(corr_build_kernel, grid, dim3(256), 0, s, a);
+  int rc = check_launch("raft_corr_build");
+  if (rc) return rc;
+  for (int l = 2; l < L; ++l) {
+    const long n = (long)B * P * lv[l].mapsz;
+    hipLaunchKernelGGL(pool2_tiled_kernel, dim3(grid_for(n)), dim3(256), 0, s, pyramid, pyramid, (long)B * P, lv[l - 1],
+                       lv[l]);
+    rc = check_launch("raft_corr_build(pool)");
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+extern "C" int raft_corr_pyramid_level(const float* pyramid, int B, int H, int W, int L, int level, float* out,
+                                       raft_stream_t stream) {
+  RAFT_REQUIRE(pyramid && out && B > 0 && H > 0 && W > 0 && L >= 1 && L <= LK_MAXL && level >= 0 && level < L,
+               "raft_corr_pyramid_level: bad arguments");
+  Level lv[LK_MAXL];
+  RAFT_REQUIRE(pyramid_levels(B, H, W, L, lv), "raft_corr_pyramid_level: a pyramid level is empty");
+  const long n = (long)B * H * W * lv[level].h * lv[level].w;
+  hipLaunchKernelGGL(untile_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), pyramid, out,
+                     (long)B * H * W, lv[level]);
+  return check_launch("raft_corr_pyramid_level");
+}
+
+extern "C" int raft_corr_lookup(const float* pyramid, int B, int H, int W, int L, int radius, const float* coords,
+                                int coords_layout, float* out, int out_ld, int out_layout, float* flow_out,
+                                int flow_ld, raft_stream_t stream) {
+  RAFT_REQUIRE(pyramid && coords && out, "raft_corr_lookup: null pointer");
+  RAFT_REQUIRE(B > 0 && H > 0 && W > 0 && L >= 1 && L <= LK_MAXL, "raft_corr_lookup: bad sizes");
+  RAFT_REQUIRE(radius >= 1 && radius <= 4, "raft_corr_lookup: radius must be 1..4 (got %d)", radius);
+  RAFT_REQUIRE(coords_layout == 0 || coords_layout == 1, "raft_corr_lookup: bad coords_layout");
+  RAFT_REQUIRE(out_layout == 0 || out_layout == 1, "raft_corr_lookup: bad out_layout");
+  const int rd = 2 * radius + 1;
+  RAFT_REQUIRE(out_layout == 1 || out_ld >= L * rd * rd, "raft_corr_lookup: out_ld < L*(2r+1)^2");
+  RAFT_REQUIRE(!flow_out || flow_ld >= 2, "raft_corr_lookup: flow_ld < 2");
+  RAFT_REQUIRE(((uintptr_t)pyramid & 15) == 0, "raft_corr_lookup: pyramid must be 16-byte aligned");
+  LookupArgs a;
+  RAFT_REQUIRE(pyramid_levels(B, H, W, L, a.lv), "raft_corr_lookup: a pyramid level is empty");
+  for (int l = L; l < LK_MAXL; ++l) a.lv[l] = a.lv[L - 1];
+  a.pyr = pyramid;
+  a.B = B;
+  a.H = H;
+  a.W = W;
+  a.L = L;
+  a.r = radius;
+  a.coords = coords;
+  a.coords_layout = coords_layout;
+  a.out = out;
+  a.out_ld = out_ld;
+  a.out_layout = out_layout;
+  a.flow = flow_out;
+  a.flow_ld = flow_ld;
+  dim3 grid((unsigned)cdiv_l((long)B * H * W, 4));
+  hipStream_t s = as_stream(stream);
+  // the 4-level case (RAFT) gets a tight instantiation; other level counts use LMAX = 6
+#define RAFT_LOOKUP_CASE(RR)                                                           \
+  case RR:                                                                             \
+    if (L <= 4)                                                                        \
+      hipLaunchKernelGGL((corr_lookup_kernel<RR, 4>), grid, dim3(256), 0, s, a);       \
+    else                                                                               \
+      hipLaunchKernelGGL((corr_lookup_kernel<RR, LK_MAXL>), grid, dim3(256), 0, s, a); \
+    break;
+  switch (radius) {
+    RAFT_LOOKUP_CASE(1)
+    RAFT_LOOKUP_CASE(2)
+    RAFT_LOOKUP_CASE(3)
+    default:
+    RAFT_LOOKUP_CASE(4)
+  }
+#undef RAFT_LOOKUP_CASE
+  return check_launch("raft_corr_lookup");
+}

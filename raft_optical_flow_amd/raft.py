@@ -25,6 +25,10 @@ from .extractor import BasicEncoder, SmallEncoder
 from .update import BasicUpdateBlock, SmallUpdateBlock
 from .utils.utils import coords_grid
 
+# module attribute kept for API parity with core/raft.py:11-22 (callers monkeypatch it);
+# the HIP path itself never autocasts: it computes in fp32
+autocast = torch.amp.autocast
+
 
 class RAFT(nn.Module):
     def __init__(self, args):

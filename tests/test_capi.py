@@ -40,7 +40,7 @@ def test_abi_queries_without_gpu():
     assert lib.raft_hip_abi_version() == 1
     assert lib.raft_hip_arch() == b"gfx950"
     # size queries are pure host arithmetic
-    assert lib.raft_corr_pyramid_floats(1, 55, 128, 4) == 7040 * (55 * 128 + 27 * 64 + 13 * 32 + 6 * 16)
+    assert lib.raft_corr_pyramid_floats(1, 55, 128, 4) == 7040 * 16 * (14 * 32 + 7 * 16 + 4 * 8 + 2 * 4)
     n, k = ctypes.c_int(), ctypes.c_int()
     assert lib.raft_conv2d_packed_shape(0, 126, 3, 3, 256, ctypes.byref(n), ctypes.byref(k)) == 0
     assert (n.value, k.value) == (128, 9 * 256)

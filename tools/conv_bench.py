@@ -9,15 +9,18 @@ from raft_optical_flow_amd import _lib
 from raft_optical_flow_amd import kernels as K
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+ONLY = sys.argv[2].split(",") if len(sys.argv) > 2 else None
 H, W = 55, 128
 dev = "cuda"
 SHAPES = [  # name, cin, cout, kh, kw, pad
     ("convc1", 324, 256, 1, 1, (0, 0)), ("convc2", 256, 192, 3, 3, (1, 1)), ("convf2", 128, 64, 3, 3, (1, 1)),
     ("conv", 256, 126, 3, 3, (1, 1)), ("zr", 384, 256, 1, 5, (0, 2)), ("q", 384, 128, 1, 5, (0, 2)),
-    ("fh1", 128, 256, 3, 3, (1, 1)), ("fh1mask", 128, 512, 3, 3, (1, 1)), ("mask2", 256, 576, 1, 1, (0, 0)),
+    ("zr_split", 256, 256, 1, 5, (0, 2)), ("q_split", 256, 128, 1, 5, (0, 2)), ("fh1", 128, 256, 3, 3, (1, 1)), ("fh1mask", 128, 512, 3, 3, (1, 1)), ("mask2", 256, 576, 1, 1, (0, 0)),
 ]
 tot_t = 0
 for name, cin, cout, kh, kw, pad in SHAPES:
+    if ONLY and name not in ONLY:
+        continue
     x = torch.randn(B * H * W, cin, device=dev)
     w = torch.randn(cout, cin, kh, kw) * 0.05
     pc = K.pack_conv(w, torch.zeros(cout), 1, pad, device=dev)
