@@ -42,6 +42,7 @@ struct ConvArgs {
   int ctot;     // in0_c + in1_c
   int cpad;     // VEC: channels per tap in the packed weight (multiple of BK)
   int taps;     // kh * kw
+  unsigned w_bytes, in0_bytes, in1_bytes;  // buffer-descriptor ranges
 };
 
 __device__ __forceinline__ float sigmoidf_(float v) { return 1.0f / (1.0f + expf(-v)); }
@@ -88,66 +89,70 @@ __device__ __forceinline__ void epilogue(const raft_conv2d_params& p, long m, in
   }
 }
 
-// Per-thread staging state: two A rows (pixels) and the incremental K walk.
+// Per-thread staging state: two A rows (output pixels) of the tile.
 struct AWalk {
   int pb[2], py[2], px[2];
   bool pv[2];
-  int ky, kx, c;  // VEC: current tap and channel base of this thread's quad
+  // VEC mode: the rows' input pixel index for the current tap, and whether it
+  // is inside the image (named scalars, not arrays: no scratch)
+  unsigned pix0, pix1;
+  bool in0, in1;
+  int tap;
 };
 
-template <int MODE>
-__device__ __forceinline__ void load_a(const ConvArgs& a, const AWalk& w, int kc, int lq, const int* ktab,
-                                       f32x4 (&ra)[2]) {
-  const raft_conv2d_params& p = a.p;
-  if constexpr (MODE == RAFT_CONV_VEC) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      const int iy = w.py[i] + w.ky, ix = w.px[i] + w.kx;
-      if (w.pv[i] && (unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w) {
-        const long pix = ((long)w.pb[i] * p.in_h + iy) * p.in_w + ix;
-        if (w.c < p.in0_c)
-          v = *reinterpret_cast<const f32x4*>(p.in0 + pix * p.in0_ld + w.c);
-        else if (w.c - p.in0_c < p.in1_c)
-          v = *reinterpret_cast<const f32x4*>(p.in1 + pix * p.in1_ld + (w.c - p.in0_c));
-      }
-      ra[i] = v;
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      float e[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int code = ktab[kc * BK + lq * 4 + j];  // (ky << 20) | (kx << 10) | c, or -1 for padding
-        float v = 0.f;
-        if (w.pv[i] && code >= 0) {
-          const int ky = code >> 20, kx = (code >> 10) & 1023, c = code & 1023;
-          const int iy = w.py[i] + ky, ix = w.px[i] + kx;
-          if ((unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w) {
-            const long pix = ((long)w.pb[i] * p.in_h + iy) * p.in_w + ix;
-            v = (c < p.in0_c) ? p.in0[pix * p.in0_ld + c] : p.in1[pix * p.in1_ld + (c - p.in0_c)];
-          }
-        }
-        e[j] = v;
-      }
-      ra[i] = f32x4{e[0], e[1], e[2], e[3]};
-    }
-  }
+constexpr unsigned OFF_INVALID = 0x80000000u;  // > num_records of every buffer (host-checked)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
 
-template <int MODE>
-__device__ __forceinline__ void advance(const ConvArgs& a, AWalk& w) {
-  if constexpr (MODE == RAFT_CONV_VEC) {
-    w.c += BK;
-    if (w.c >= a.cpad) {
-      w.c -= a.cpad;
-      if (++w.kx == a.p.kw) {
-        w.kx = 0;
-        ++w.ky;
-      }
-    }
+__device__ __forceinline__ f32x4 buf_load4(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+  using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+
+// VEC: recompute the rows' pixel offsets when the K walk enters a new tap
+// (once per c_pad/32 K-steps; all tap/step bookkeeping is wave-uniform).
+__device__ __forceinline__ void vec_set_tap(const ConvArgs& a, AWalk& w, int tap) {
+  const raft_conv2d_params& p = a.p;
+  const int ky = tap / p.kw, kx = tap - ky * p.kw;
+  {
+    const int iy = w.py[0] + ky, ix = w.px[0] + kx;
+    w.in0 = w.pv[0] && (unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w;
+    w.pix0 = (unsigned)((w.pb[0] * p.in_h + iy) * p.in_w + ix);
   }
+  {
+    const int iy = w.py[1] + ky, ix = w.px[1] + kx;
+    w.in1 = w.pv[1] && (unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w;
+    w.pix1 = (unsigned)((w.pb[1] * p.in_h + iy) * p.in_w + ix);
+  }
+  w.tap = tap;
+}
+
+// GATHER mode (small / unaligned inputs): element-wise loads through the
+// k -> (ky, kx, c) LDS table, issued unconditionally from clamped addresses;
+// returns the validity bits (bit 4*i + j), applied when staging.
+__device__ __forceinline__ unsigned gather_a(const ConvArgs& a, const AWalk& w, int kc, int lq, const int* ktab,
+                                             f32x4 (&ra)[2]) {
+  const raft_conv2d_params& p = a.p;
+  unsigned mask = 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    float e[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int code = ktab[kc * BK + lq * 4 + j];  // (ky << 20) | (kx << 10) | c, or -1 for padding
+      const int ky = code >> 20, kx = (code >> 10) & 1023, c = code & 1023;
+      const int iy = w.py[i] + ky, ix = w.px[i] + kx;
+      const bool ok = w.pv[i] && code >= 0 && (unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w;
+      const long pix = ((long)w.pb[i] * p.in_h + iy) * p.in_w + ix;
+      const float* src = (c < p.in0_c) ? p.in0 + pix * p.in0_ld + c : p.in1 + pix * p.in1_ld + (c - p.in0_c);
+      e[j] = *(ok ? src : p.in0);
+      mask |= ok ? 1u << (4 * i + j) : 0u;
+    }
+    ra[i] = f32x4{e[0], e[1], e[2], e[3]};
+  }
+  return mask;
 }
 
 // KG = number of K-groups: the work-group holds KG x 4 waves; group g runs the
@@ -163,7 +168,7 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(ConvArgs a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int g = wave >> 2;          // K-group
+  const int g = __builtin_amdgcn_readfirstlane(wave >> 2);  // K-group (provably wave-uniform)
   const int wl = wave & 3;          // wave within the group
   const int wm = wl & 1, wn = wl >> 1;
   const int lt = tid & 255;         // thread within the group
@@ -197,31 +202,64 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(ConvArgs a) {
     w.py[i] = oy * p.stride_h - p.pad_h;
     w.px[i] = ox * p.stride_w - p.pad_w;
   }
-  w.ky = 0;
-  w.kx = 0;
-  w.c = lq * 4;
-  for (int i = 0; i < g; ++i) advance<MODE>(a, w);  // group g starts at K-step g
-  const float* wrow0 = p.weight + (long)(n0 + lr) * a.K + lq * 4;
-  const float* wrow1 = wrow0 + 32L * a.K;
-
+  w.tap = -1;
   const int nk = a.K / BK;
+  const int cpt = a.cpad / BK;  // K-steps per tap (VEC)
+  // buffer descriptors: wave-uniform (kernel arguments only)
+  const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(p.weight, a.w_bytes);
+  const __amdgpu_buffer_rsrc_t rs_0 = make_rsrc(p.in0, a.in0_bytes);
+  const __amdgpu_buffer_rsrc_t rs_1 = make_rsrc(p.in1_c ? p.in1 : p.in0, a.in1_bytes);
+  const unsigned wvoff0 = ((unsigned)(n0 + lr) * (unsigned)a.K + lq * 4) * 4u;
+  const unsigned wvoff1 = wvoff0 + 32u * (unsigned)a.K * 4u;
   const int cnt = g < nk ? (nk - g + KG - 1) / KG : 0;  // this group's K-steps
   const int nj = (nk + KG - 1) / KG;                     // phases (group 0's count)
   f32x4 ra0[2], rb0[2], ra1[2], rb1[2];  // two staging register sets (phases of even / odd parity)
+  unsigned am0 = 0, am1 = 0;             // their A validity masks
 
-  auto issue = [&](int j, f32x4(&ra)[2], f32x4(&rb)[2]) {
-    const int kc = g + KG * j;
-    load_a<MODE>(a, w, kc, lq, ktab, ra);
-#pragma unroll
-    for (int i = 0; i < KG; ++i) advance<MODE>(a, w);
-    rb[0] = *reinterpret_cast<const f32x4*>(wrow0 + kc * BK);
-    rb[1] = *reinterpret_cast<const f32x4*>(wrow1 + kc * BK);
+  // issue() is unconditional: phases beyond this group's count re-read the last
+  // K-step (clamped, never consumed) so every phase has the same load count
+  auto issue = [&](int j, f32x4(&ra)[2], f32x4(&rb)[2], unsigned& am) {
+    const int kc = min(g + KG * j, nk - 1);
+    if constexpr (MODE == RAFT_CONV_VEC) {
+      const int tap = kc / cpt;
+      if (tap != w.tap) vec_set_tap(a, w, tap);
+      const int cs = (kc - tap * cpt) * BK;  // first channel of this K-step (uniform)
+      const bool s0 = cs < p.in0_c;
+      const int cl = cs + lq * 4;          // this lane's channel
+      const bool lane_ok = s0 ? cl < p.in0_c : cl - p.in0_c < p.in1_c;
+      const unsigned soff = (unsigned)(s0 ? cs : cs - p.in0_c) * 4u;
+      // the segment's descriptor, rebuilt from readfirstlane'd (provably uniform)
+      // words so hipcc keeps it in SGPRs (no waterfall loop around the loads)
+      const unsigned long long base = s0 ? (unsigned long long)p.in0 : (unsigned long long)p.in1;
+      const unsigned blo = __builtin_amdgcn_readfirstlane((unsigned)base);
+      const unsigned bhi = __builtin_amdgcn_readfirstlane((unsigned)(base >> 32));
+      const unsigned nrec = __builtin_amdgcn_readfirstlane(s0 ? a.in0_bytes : a.in1_bytes);
+      const __amdgpu_buffer_rsrc_t rs =
+          make_rsrc(reinterpret_cast<const void*>(((unsigned long long)bhi << 32) | blo), nrec);
+      const unsigned ldb = (unsigned)(s0 ? p.in0_ld : p.in1_ld) * 4u;  // row pitch in bytes (uniform)
+      const unsigned v0 = (lane_ok && w.in0) ? w.pix0 * ldb + lq * 16u : OFF_INVALID;
+      const unsigned v1 = (lane_ok && w.in1) ? w.pix1 * ldb + lq * 16u : OFF_INVALID;
+      ra[0] = buf_load4(rs, v0, soff);
+      ra[1] = buf_load4(rs, v1, soff);
+      am = 0xFFu;
+    } else {
+      am = gather_a(a, w, kc, lq, ktab, ra);
+    }
+    const unsigned ws = (unsigned)kc * BK * 4u;
+    rb[0] = buf_load4(rs_w, wvoff0, ws);
+    rb[1] = buf_load4(rs_w, wvoff1, ws);
   };
-  auto stage = [&](int buf, const f32x4(&ra)[2], const f32x4(&rb)[2]) {
+  auto stage = [&](int buf, const f32x4(&ra)[2], const f32x4(&rb)[2], unsigned am) {
     float* A = gsm + buf * STAGE;
     float* B = A + BM * LDSK;
-    *reinterpret_cast<f32x4*>(A + lr * LDSK + lq * 4) = ra[0];
-    *reinterpret_cast<f32x4*>(A + (lr + 32) * LDSK + lq * 4) = ra[1];
+    f32x4 x0 = ra[0], x1 = ra[1];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      x0[e] = (am >> e) & 1 ? x0[e] : 0.f;
+      x1[e] = (am >> (4 + e)) & 1 ? x1[e] : 0.f;
+    }
+    *reinterpret_cast<f32x4*>(A + lr * LDSK + lq * 4) = x0;
+    *reinterpret_cast<f32x4*>(A + (lr + 32) * LDSK + lq * 4) = x1;
     *reinterpret_cast<f32x4*>(B + lr * LDSK + lq * 4) = rb[0];
     *reinterpret_cast<f32x4*>(B + (lr + 32) * LDSK + lq * 4) = rb[1];
   };
@@ -244,23 +282,24 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(ConvArgs a) {
   };
 
   // prologue: phases 0 and 1 in flight, phase 0 staged
-  if (cnt > 0) issue(0, ra0, rb0);
-  if (cnt > 1) issue(1, ra1, rb1);
-  if (cnt > 0) stage(0, ra0, rb0);
+  issue(0, ra0, rb0, am0);
+  issue(1, ra1, rb1, am1);
+  stage(0, ra0, rb0, am0);
   __syncthreads();
-  if (cnt > 2) issue(2, ra0, rb0);
+  issue(2, ra0, rb0, am0);
 
-  // steady state, unrolled by two so the register sets are static
+  // steady state, unrolled by two so the register sets are static; loads and
+  // LDS stores are branch-free, only the MFMA phases are predicated (uniformly)
   int j = 0;
   for (; j + 2 <= nj; j += 2) {
     if (j < cnt) compute(0);
-    if (j + 1 < cnt) stage(1, ra1, rb1);
+    stage(1, ra1, rb1, am1);
     __syncthreads();
-    if (j + 3 < cnt) issue(j + 3, ra1, rb1);
+    issue(j + 3, ra1, rb1, am1);
     if (j + 1 < cnt) compute(1);
-    if (j + 2 < cnt) stage(0, ra0, rb0);
+    stage(0, ra0, rb0, am0);
     __syncthreads();
-    if (j + 4 < cnt) issue(j + 4, ra0, rb0);
+    issue(j + 4, ra0, rb0, am0);
   }
   if (j < cnt) compute(0);  // odd phase count: the last phase sits in buffer 0
 
@@ -383,6 +422,16 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
   if (rc) return rc;
   a.K = k_pad;
   a.cpad = round_up(ctot, BK);
+  {
+    const double npix_in = (double)p.batch * p.in_h * p.in_w;
+    const double b0 = npix_in * p.in0_ld * 4.0, b1 = npix_in * (p.in1_c ? p.in1_ld : 0) * 4.0;
+    const double bw = (double)n_pad * k_pad * 4.0;
+    RAFT_REQUIRE(b0 < 2147483648.0 && b1 < 2147483648.0 && bw < 2147483648.0,
+                 "raft_conv2d: an operand exceeds 2 GiB (split the batch)");
+    a.in0_bytes = (unsigned)b0;
+    a.in1_bytes = (unsigned)b1;
+    a.w_bytes = (unsigned)bw;
+  }
   if (p.mode == RAFT_CONV_VEC) {
     RAFT_REQUIRE(p.in0_c % 4 == 0 && p.in1_c % 4 == 0, "raft_conv2d VEC: channel counts must be multiples of 4");
     RAFT_REQUIRE(p.in1_c == 0 || p.in0_c % BK == 0, "raft_conv2d VEC: seg0 channels must be a multiple of 32 with seg1");

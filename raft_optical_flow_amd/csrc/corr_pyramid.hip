@@ -70,23 +70,28 @@ __global__ __launch_bounds__(256) void corr_build_kernel(CorrBuildArgs a) {
     bv_[i] = h2 < a.H && w2 < a.W;
     brow[i] = a.f2 + ((long)b * a.P + (bv_[i] ? h2 * a.W + w2 : 0)) * a.ld + lq * 4;
   }
+  // loads are unconditional (clamped addresses) and zeroed at the LDS store, so
+  // the next K-step's loads stay in flight across the MFMAs (counted vmcnt)
   f32x4 ra[2], rb[2];
+  bool ok_a[2], ok_b[2];
   auto gload = [&](int kc) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
       const bool cin = kc * CB_BK + lq * 4 < a.C;  // C % 4 == 0; zero-fill the K tail
-      ra[i] = (av_[i] && cin) ? *reinterpret_cast<const f32x4*>(arow[i] + kc * CB_BK) : z;
-      rb[i] = (bv_[i] && cin) ? *reinterpret_cast<const f32x4*>(brow[i] + kc * CB_BK) : z;
+      ok_a[i] = av_[i] && cin;
+      ok_b[i] = bv_[i] && cin;
+      ra[i] = *reinterpret_cast<const f32x4*>(ok_a[i] ? arow[i] + kc * CB_BK : a.f1);
+      rb[i] = *reinterpret_cast<const f32x4*>(ok_b[i] ? brow[i] + kc * CB_BK : a.f2);
     }
   };
   auto sstore = [&](int buf) {
     float* A = smem + buf * STAGE;
     float* Bt = A + CB_BM * CB_LDSK;
-    *reinterpret_cast<f32x4*>(A + lr * CB_LDSK + lq * 4) = ra[0];
-    *reinterpret_cast<f32x4*>(A + (lr + 32) * CB_LDSK + lq * 4) = ra[1];
-    *reinterpret_cast<f32x4*>(Bt + lr * CB_LDSK + lq * 4) = rb[0];
-    *reinterpret_cast<f32x4*>(Bt + (lr + 32) * CB_LDSK + lq * 4) = rb[1];
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    *reinterpret_cast<f32x4*>(A + lr * CB_LDSK + lq * 4) = ok_a[0] ? ra[0] : z;
+    *reinterpret_cast<f32x4*>(A + (lr + 32) * CB_LDSK + lq * 4) = ok_a[1] ? ra[1] : z;
+    *reinterpret_cast<f32x4*>(Bt + lr * CB_LDSK + lq * 4) = ok_b[0] ? rb[0] : z;
+    *reinterpret_cast<f32x4*>(Bt + (lr + 32) * CB_LDSK + lq * 4) = ok_b[1] ? rb[1] : z;
   };
   const int nk = cdiv(a.C, CB_BK);
   gload(0);
@@ -251,6 +256,7 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
   // lane -> (tile row ti, tile col tj, row-in-tile rr) of the 4x4-tile patch
   const int ti = lane >> 4, tj = (lane >> 2) & 3, rr = lane & 3;
   f32x4 v[LMAX];
+  bool ok[LMAX];
   int tyo[LMAX], txo[LMAX];
 #pragma unroll
   for (int l = 0; l < LMAX; ++l) {
@@ -262,69 +268,76 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
     const int ntx = ((x0 + WD - 1) >> 2) - txo[l] + 1;
     const int ty = tyo[l] + ti, tx = txo[l] + tj;
     const Level& lv = a.lv[l];
-    f32x4 z = {0.f, 0.f, 0.f, 0.f};
-    if (l < a.L && valid && ti < nty && tj < ntx && (unsigned)ty < (unsigned)lv.th && (unsigned)tx < (unsigned)lv.tw)
-      z = *reinterpret_cast<const f32x4*>(a.pyr + lv.off + gp * lv.mapsz + ((long)ty * lv.tw + tx) * 16 + rr * 4);
-    v[l] = z;
+    // unconditional load from a clamped address: all levels' loads in flight at once
+    ok[l] = l < a.L && valid && ti < nty && tj < ntx && (unsigned)ty < (unsigned)lv.th && (unsigned)tx < (unsigned)lv.tw;
+    const float* src = a.pyr + lv.off + gp * lv.mapsz + ((long)ty * lv.tw + tx) * 16 + rr * 4;
+    v[l] = *reinterpret_cast<const f32x4*>(ok[l] ? src : a.pyr);
   }
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int l = 0; l < LMAX; ++l)
-    *reinterpret_cast<f32x4*>(&patch[wv][l][(ti * 4 + rr) * 16 + tj * 4]) = v[l];
+    *reinterpret_cast<f32x4*>(&patch[wv][l][(ti * 4 + rr) * 16 + tj * 4]) = ok[l] ? v[l] : zero;
   __syncthreads();
   if (!valid) return;
 
+  // levels unrolled so each level's geometry is a compile-time-indexed kernel
+  // argument (scalar loads), hoisted out of the per-tap work
   const int ntap = a.L * RD * RD;
-  for (int t = lane; t < ntap; t += 64) {
-    const int l = t / (RD * RD);
-    const int tt = t - l * RD * RD;
-    const int ix = tt / RD, iy = tt - ix * RD;
+#pragma unroll
+  for (int l = 0; l < LMAX; ++l) {
+    if (l >= a.L) break;
+    const Level lv = a.lv[l];
     const float s = 1.0f / (float)(1 << l);
     const float cx = x * s, cy = y * s;
-    const Level& lv = a.lv[l];
     // patch origin and extent of the tiles phase 1 loaded for this level
     const int x0 = (int)floorf(cx) - R, y0 = (int)floorf(cy) - R;
     const int px0 = (x0 >> 2) * 4, py0 = (y0 >> 2) * 4;
     const int pw = (((x0 + WD - 1) >> 2) - (x0 >> 2) + 1) * 4, ph = (((y0 + WD - 1) >> 2) - (y0 >> 2) + 1) * 4;
-    const float X = cx + (float)(ix - R);
-    const float Y = cy + (float)(iy - R);
     const float wm1 = (float)(lv.w - 1), hm1 = (float)(lv.h - 1);
-    const float gx = div_rn(2.0f * X, wm1, 1.0f / wm1) - 1.0f;
-    const float gy = div_rn(2.0f * Y, hm1, 1.0f / hm1) - 1.0f;
-    const float ux = (gx + 1.0f) * (wm1 * 0.5f);
-    const float uy = (gy + 1.0f) * (hm1 * 0.5f);
-    float val;
-    if (!(isfinite(ux) && isfinite(uy))) {
-      val = __builtin_nanf("");
-    } else {
-      const float fx0 = floorf(ux), fy0 = floorf(uy);
-      const float tx = ux - fx0, ty = uy - fy0;
-      const int xi = (int)fx0, yi = (int)fy0;
-      const int wx = xi - px0, wy = yi - py0;
-      float vnw, vne, vsw, vse;
-      if (wx >= 0 && wx + 1 < pw && wy >= 0 && wy + 1 < ph) {
-        const float* w = &patch[wv][l][wy * 16 + wx];
-        vnw = w[0];
-        vne = w[1];
-        vsw = w[16];
-        vse = w[17];
-      } else {  // the float round trip moved this tap's floor off the staged patch
-        const float* m = a.pyr + lv.off + gp * lv.mapsz;
-        auto at = [&](int yy, int xx) {
-          return ((unsigned)yy < (unsigned)lv.h && (unsigned)xx < (unsigned)lv.w) ? m[tiled_index(yy, xx, lv.tw)]
-                                                                                  : 0.f;
-        };
-        vnw = at(yi, xi);
-        vne = at(yi, xi + 1);
-        vsw = at(yi + 1, xi);
-        vse = at(yi + 1, xi + 1);
+    const float rw = 1.0f / wm1, rh = 1.0f / hm1;
+    for (int tt = lane; tt < RD * RD; tt += 64) {
+      const int ix = tt / RD, iy = tt - ix * RD;
+      const float X = cx + (float)(ix - R);
+      const float Y = cy + (float)(iy - R);
+      const float gx = div_rn(2.0f * X, wm1, rw) - 1.0f;
+      const float gy = div_rn(2.0f * Y, hm1, rh) - 1.0f;
+      const float ux = (gx + 1.0f) * (wm1 * 0.5f);
+      const float uy = (gy + 1.0f) * (hm1 * 0.5f);
+      float val;
+      if (!(isfinite(ux) && isfinite(uy))) {
+        val = __builtin_nanf("");
+      } else {
+        const float fx0 = floorf(ux), fy0 = floorf(uy);
+        const float tx = ux - fx0, ty = uy - fy0;
+        const int xi = (int)fx0, yi = (int)fy0;
+        const int wx = xi - px0, wy = yi - py0;
+        float vnw, vne, vsw, vse;
+        if (wx >= 0 && wx + 1 < pw && wy >= 0 && wy + 1 < ph) {
+          const float* w = &patch[wv][l][wy * 16 + wx];
+          vnw = w[0];
+          vne = w[1];
+          vsw = w[16];
+          vse = w[17];
+        } else {  // the float round trip moved this tap's floor off the staged patch
+          const float* m = a.pyr + lv.off + gp * lv.mapsz;
+          auto at = [&](int yy, int xx) {
+            return ((unsigned)yy < (unsigned)lv.h && (unsigned)xx < (unsigned)lv.w) ? m[tiled_index(yy, xx, lv.tw)]
+                                                                                    : 0.f;
+          };
+          vnw = at(yi, xi);
+          vne = at(yi, xi + 1);
+          vsw = at(yi + 1, xi);
+          vse = at(yi + 1, xi + 1);
+        }
+        const float e = 1.0f - tx, sS = 1.0f - ty;
+        val = vnw * (sS * e) + vne * (sS * tx) + vsw * (ty * e) + vse * (ty * tx);
       }
-      const float e = 1.0f - tx, sS = 1.0f - ty;
-      val = vnw * (sS * e) + vne * (sS * tx) + vsw * (ty * e) + vse * (ty * tx);
+      const int t = l * RD * RD + tt;
+      if (a.out_layout == 0)
+        a.out[gp * a.out_ld + t] = val;
+      else
+        a.out[((long)b * ntap + t) * P + p] = val;
     }
-    if (a.out_layout == 0)
-      a.out[gp * a.out_ld + t] = val;
-    else
-      a.out[((long)b * ntap + t) * P + p] = val;
   }
   if (a.flow && lane < 2) {
     const float g = lane == 0 ? (float)(p % a.W) : (float)(p / a.W);
