@@ -14,7 +14,10 @@ The line also carries
   roofline      the corr-lookup kernel (the metric's "corr-lookup GB/s vs HBM
                 peak"): algorithmic bytes P*2904 per pair-iteration / its
                 average launch time measured with HIP events on its stream;
-  update_gemm   the same accounting for the update-block convolutions (MFMA-bound);
+  update_gemm   the same accounting for the update-block convolutions (MFMA-bound;
+                peak per conv arithmetic: f32 MFMA 157.3 TF, f16x3 = f16 MFMA / 3);
+  fp32_exact    with the default f16x3 conv arithmetic: the same run with exact
+                f32 MFMA convs (value, ms_per_step), rank 0, N = 1;
   cpu_baseline  the numpy oracle (oracle/raft_oracle.py) on the host cores for one
                 pair of the same workload (rank 0, N = 1 only).
 """
@@ -34,6 +37,11 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TF = 157.3  # dense f32 MFMA (= f32 vector) peak
+F16_MFMA_PEAK_TF = 2500.0  # dense f16 MFMA peak
+# fp32-equivalent peak of the update convolutions per conv arithmetic
+CONV_PEAK_TF = {"fp32": FP32_MFMA_PEAK_TF, "f16x3": F16_MFMA_PEAK_TF / 3, "f16": F16_MFMA_PEAK_TF}
+DTYPE = {"fp32": "fp32", "f16x3": "fp32 (convs: f16x3 split MFMA, fp32 accumulate)",
+         "f16": "f16 convs, fp32 accumulate (mixed precision)"}
 
 
 def lookup_bytes_per_pixel(levels=4, r=4):
@@ -113,6 +121,8 @@ def main():
     ap.add_argument("--alternate-corr", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--precision", choices=["fp32", "f16x3", "f16"], default=None,
+                    help="conv arithmetic (default: the RAFT default, f16x3)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -131,6 +141,8 @@ def main():
     if rank == 0:
         model.load_state_dict(seeded_state_dict(model, 0))
     model.to(dev).eval()
+    model.conv_precision = args.precision
+    prec = model.resolved_precision()
     if world > 1:
         broadcast_state_dict(model, src=0)  # one RCCL broadcast over xGMI
 
@@ -144,29 +156,32 @@ def main():
     H, W = pool[0][0].shape[-2:]
     plan = model.plan(args.batch, H, W, args.iters, test_mode=True, device=dev)
 
-    def step(k):
-        plan.set_inputs(*pool[k % len(pool)])
-        if args.no_graph:
-            plan.run()
-        else:
-            plan.replay()
+    def timed(plan, barrier):
+        def step(k):
+            plan.set_inputs(*pool[k % len(pool)])
+            if args.no_graph:
+                plan.run()
+            else:
+                plan.replay()
 
-    if not args.no_graph:
-        plan.capture()
-    for k in range(args.warmup):
-        step(k)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(k)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+        if not args.no_graph:
+            plan.capture()
+        for k in range(args.warmup):
+            step(k)
+        torch.cuda.synchronize()
+        if barrier:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            step(k)
+        torch.cuda.synchronize()
+        if barrier:
+            dist.barrier()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    elapsed = timed(plan, world > 1)
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -201,10 +216,19 @@ def main():
     t_upd = time_kernel_events(lambda: [l(s) for l in one_iter], 50)
     fl = P * update_flops_per_pixel(pu, with_mask=False)
     upd_tf = fl / t_upd / 1e12
-    update_roof = {"kernel": "raft_conv2d (update block, one iteration)", "bound": "mfma",
-                   "achieved": round(upd_tf, 2), "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                   "frac": round(upd_tf / FP32_MFMA_PEAK_TF, 4), "iteration_us": round(t_upd * 1e6, 1),
+    peak = CONV_PEAK_TF[prec]
+    update_roof = {"kernel": f"raft_conv2d (update block, one iteration, {prec})", "bound": "mfma",
+                   "achieved": round(upd_tf, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+                   "frac": round(upd_tf / peak, 4), "iteration_us": round(t_upd * 1e6, 1),
                    "flops_per_iteration": fl}
+
+    exact = None
+    if prec != "fp32" and world == 1:
+        model.conv_precision = "fp32"
+        plan32 = model.plan(args.batch, H, W, args.iters, test_mode=True, device=dev)
+        e32 = timed(plan32, False)
+        exact = {"value": round(args.batch * args.steps / e32, 3), "ms_per_step": round(e32 / args.steps * 1e3, 3)}
+        model.conv_precision = args.precision
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -215,7 +239,7 @@ def main():
             "metric": "image-pairs/s at Sintel 436x1024, 32 iters; corr-lookup GB/s vs HBM peak",
             "value": round(value, 3), "unit": "image-pairs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": DTYPE[prec],
             "data": "synthetic (seeded uint8-valued frames, random-init seeded weights)",
             "config": {"workload": f"RAFT-full inference, {args.height}x{args.width} padded to {H}x{W}, "
                                    f"{args.batch} pair(s)/GPU/step, iters={args.iters}, "
@@ -224,6 +248,7 @@ def main():
                        "global_batch": world * args.batch, "parallelism": f"frame-pair sharding x{world}"},
             "roofline": roof,
             "update_gemm": update_roof,
+            "fp32_exact": exact,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RAFT_HIP_ABI_VERSION 1
+#define RAFT_HIP_ABI_VERSION 2
 
 /* Negative return codes (argument errors, raised before any launch). */
 #define RAFT_E_INVALID (-1)   /* bad size / null pointer / unsupported shape */
@@ -118,7 +118,7 @@ size_t raft_alt_corr_backward_workspace_floats(int B, int H1, int W1, int H2, in
 int raft_avgpool2_nhwc(const float* in, float* out, int B, int H, int W, int C, raft_stream_t stream);
 
 /* ---------------------------------------------------------------------------
- * Convolution as implicit GEMM on fp32 MFMA (v_mfma_f32_32x32x2_f32), NHWC.
+ * Convolution as implicit GEMM on MFMA, NHWC.
  * M = batch*out_h*out_w pixels, N = out channels, K = taps x input channels.
  * The input is a virtual concat of up to two NHWC row sources (seg 0, then
  * seg 1), which is how torch.cat([...], dim=1) of the reference is elided.
@@ -131,9 +131,26 @@ int raft_avgpool2_nhwc(const float* in, float* out, int B, int H, int W, int C, 
  *                          w[n_pad][k_pad], k = (ky*KW + kx)*(c0+c1) + c,
  *                          k_pad = roundup(KH*KW*(c0+c1), 32), zero padded;
  *   n_pad = roundup(N, 64).
+ *
+ * Arithmetic (params.precision):
+ *   RAFT_PREC_FP32   v_mfma_f32_32x32x2_f32 on the fp32 packed weight.
+ *   RAFT_PREC_F16X3  fp32-accurate split: every operand x = hi + lo/2048 with
+ *                    hi = f16(x), lo = f16((x - hi) * 2048); products
+ *                    hi*hi + (hi*lo + lo*hi)/2048 on v_mfma_f32_32x32x16_f16
+ *                    with fp32 accumulation (the lo*lo term, 2^-22 relative,
+ *                    is dropped).  Weight: the split form of the packed
+ *                    weight (raft_conv2d_split_weight), same byte size.
+ *   RAFT_PREC_F16    one f16 product (hi*hi), fp32 accumulation: the mixed-
+ *                    precision mode (reference: autocast, core/raft.py:156);
+ *                    uses the same split weight.
+ * N <= 4 convolutions always take the fp32 packed weight (VALU kernel).
  * --------------------------------------------------------------------------- */
 #define RAFT_CONV_VEC 0
 #define RAFT_CONV_GATHER 1
+
+#define RAFT_PREC_FP32 0
+#define RAFT_PREC_F16X3 1
+#define RAFT_PREC_F16 2
 
 /* epilogues: v = acc + bias[n] */
 #define RAFT_EPI_LINEAR 0         /* out = alpha * v                                          */
@@ -163,11 +180,16 @@ typedef struct raft_conv2d_params {
   const float* add0; int add0_ld;           /* optional addend rows: v = acc + bias[n] + add0[m,n]
                                                (a precomputed partial sum, e.g. the GRU's
                                                iteration-invariant context term) */
+  int precision;                            /* RAFT_PREC_* (weight format follows it) */
 } raft_conv2d_params;
 
 /* Packed weight geometry for a conv (n_pad, k_pad in floats per row). */
 int raft_conv2d_packed_shape(int mode, int n, int kh, int kw, int cin, int* n_pad, int* k_pad);
 int raft_conv2d(const raft_conv2d_params* p, raft_stream_t stream);
+/* fp32 packed weight [n_pad][k_pad] -> split form for RAFT_PREC_F16X3 / F16:
+ * per row and 32-wide K-step, 32 f16 hi then 32 f16 lo (lo scaled by 2048);
+ * out holds n_pad*k_pad*4 bytes, like the input. */
+int raft_conv2d_split_weight(const float* w, void* out, int n_pad, int k_pad, raft_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * InstanceNorm2d (affine=False, eps): statistics per (image, channel) over

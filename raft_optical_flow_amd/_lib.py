@@ -23,6 +23,13 @@ P = c_void_p  # device pointers are passed as integers / void*
 RAFT_CONV_VEC = 0
 RAFT_CONV_GATHER = 1
 
+PREC_FP32 = 0    # v_mfma_f32_32x32x2_f32
+PREC_F16X3 = 1   # fp32-accurate hi/lo f16 split on v_mfma_f32_32x32x16_f16
+PREC_F16 = 2     # single f16 product (mixed precision)
+PRECISIONS = {"fp32": PREC_FP32, "f16x3": PREC_F16X3, "f16": PREC_F16}
+
+ABI_VERSION = 2
+
 EPI_LINEAR = 0
 EPI_RELU = 1
 EPI_RESID_RELU = 2
@@ -50,6 +57,7 @@ class ConvParams(ctypes.Structure):
         ("aux1", P), ("aux1_ld", c_int),
         ("out1", P), ("out1_ld", c_int),
         ("add0", P), ("add0_ld", c_int),
+        ("precision", c_int),
     ]
 
 
@@ -72,6 +80,7 @@ _PROTOS = {
     "raft_conv2d_packed_shape": (c_int, [c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_int),
                                          ctypes.POINTER(c_int)]),
     "raft_conv2d": (c_int, [ctypes.POINTER(ConvParams), P]),
+    "raft_conv2d_split_weight": (c_int, [P, P, c_int, c_int, P]),
     "raft_instnorm_workspace_floats": (c_size_t, [c_int, c_int, c_int]),
     "raft_instnorm_stats": (c_int, [P, c_int, c_int, c_int, c_int, c_float, P, P, P]),
     "raft_instnorm_apply": (c_int, [P, c_int, P, P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, P]),
@@ -111,7 +120,7 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.raft_hip_abi_version() != 1:
+        if lib.raft_hip_abi_version() != ABI_VERSION:
             raise RaftHipError("libraft_hip.so ABI version mismatch")
         _lib = lib
         return lib

@@ -1,4 +1,4 @@
-// Implicit-GEMM convolution on fp32 MFMA (v_mfma_f32_32x32x2_f32) for gfx950.
+// Implicit-GEMM convolution on MFMA for gfx950.
 //
 // Replaces every nn.Conv2d of the RAFT update block (core/update.py:6-325) and
 // encoders (core/extractor.py:6-267), with the surrounding elementwise work of
@@ -7,19 +7,30 @@
 //
 // Layout: NHWC rows.  GEMM view: M = output pixels, N = output channels,
 // K = (tap, channel).  Work-group tile 64(M) x 64(N), K-step 32; four waves in
-// a 2x2 arrangement each own a 32x32 accumulator (16 f32 AGPR/VGPR per lane).
-// Within a K-step the 32 k's are split 16/16 over the two lane halves that
-// the MFMA's A/B operand maps assign to k = 0 / 1, so each lane reads its 16
-// operand floats with four ds_read_b128 from a row-major [row][32+4] LDS tile
-// (the +4 pad makes any 16 consecutive rows hit distinct 16-B bank slots).
+// a 2x2 arrangement each own a 32x32 accumulator.  LDS rows are 32+4 dwords
+// (the pad keeps 32 consecutive rows' 16-B reads on distinct bank slots).
+//
+// Arithmetic (template PREC, include/raft_hip.h):
+//  * FP32: v_mfma_f32_32x32x2_f32; the 32 k of a K-step are split 16/16 over
+//    the two lane halves that the operand maps assign to k = 0 / 1, so each
+//    lane reads its 16 operand floats with four ds_read_b128.
+//  * F16X3: the staging threads split every fp32 activation into f16 hi and
+//    2048-scaled f16 lo (the weight arrives pre-split); an LDS row holds the
+//    K-step's 32 hi then 32 lo halves (same 128 B).  Per K-step a wave issues
+//    2 hi*hi MFMAs into acc and 4 cross MFMAs (hi*lo, lo*hi) into accx on
+//    v_mfma_f32_32x32x16_f16 (16x the f32 rate): 6 x 32 cycles instead of
+//    16 x 64.  Result acc + accx/2048: ~22-bit operands, fp32 accumulation.
+//  * F16: hi*hi only (the mixed-precision mode).
 //
 // Pipeline: two register staging sets and two LDS buffers.  The global loads
 // of K-step k+2 are issued right after the barrier that publishes step k+1,
-// so every load has two MFMA phases (2 x 16 MFMAs = 2 x 1024 cycles per wave)
-// to land before its ds_write; one barrier per K-step.  The (tap, channel)
-// walk is incremental (no integer division in the loop).  GATHER mode (inputs
-// with < 4 or unaligned channels: the 3-channel stem, the 2-channel flow)
-// decodes k -> (ky, kx, c) through a per-workgroup LDS table.
+// one barrier per K-step.  VEC staging uses raw buffer loads: per-tap row byte
+// offsets (recomputed only when the K walk changes tap), the K-step's channel
+// offset as the wave-uniform soffset, and out-of-image rows pointed past the
+// buffer end so the hardware returns zeros (no branches, no 64-bit address
+// arithmetic in the loop).  GATHER mode (inputs with < 4 or unaligned
+// channels: the 3-channel stem, the 2-channel flow) decodes k -> (ky, kx, c)
+// through a per-workgroup LDS table.
 //
 // N <= 4 outputs (the flow head's 256 -> 2 conv) use conv_smalln_kernel: one
 // wave per output pixel, channels across lanes, wave reduction per output.
@@ -44,6 +55,22 @@ struct ConvArgs {
   int taps;     // kh * kw
   unsigned w_bytes, in0_bytes, in1_bytes;  // buffer-descriptor ranges
 };
+
+using h4 = __attribute__((ext_vector_type(4))) _Float16;
+using h8 = __attribute__((ext_vector_type(8))) _Float16;
+
+constexpr float SPLIT_SCALE = 2048.f;  // lo is stored scaled by 2^11 (kept out of f16 subnormals)
+
+// x = hi + lo / 2048 to ~22 bits: hi = f16(x); x - hi is exact in fp32, its
+// 2^11-scaled value rounds to f16 lo.
+__device__ __forceinline__ void split4(const f32x4 x, h4& hi, h4& lo) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const _Float16 h = (_Float16)x[e];
+    hi[e] = h;
+    lo[e] = (_Float16)((x[e] - (float)h) * SPLIT_SCALE);
+  }
+}
 
 __device__ __forceinline__ float sigmoidf_(float v) { return 1.0f / (1.0f + expf(-v)); }
 
@@ -160,7 +187,7 @@ __device__ __forceinline__ unsigned gather_a(const ConvArgs& a, const AWalk& w, 
 // double buffer, so each SIMD carries KG waves of the tile that interleave
 // (one group's MFMAs cover the other's LDS reads, barrier skew and staging).
 // The groups' accumulators are summed through LDS before the epilogue.
-template <int MODE, int KG>
+template <int MODE, int KG, int PREC>
 __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(ConvArgs a) {
   __shared__ __attribute__((aligned(16))) float
       smem[KG * 2 * STAGE + (MODE == RAFT_CONV_GATHER ? MAX_GATHER_K : 0)];
@@ -258,27 +285,74 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(ConvArgs a) {
       x0[e] = (am >> e) & 1 ? x0[e] : 0.f;
       x1[e] = (am >> (4 + e)) & 1 ? x1[e] : 0.f;
     }
-    *reinterpret_cast<f32x4*>(A + lr * LDSK + lq * 4) = x0;
-    *reinterpret_cast<f32x4*>(A + (lr + 32) * LDSK + lq * 4) = x1;
+    if constexpr (PREC == RAFT_PREC_FP32) {
+      *reinterpret_cast<f32x4*>(A + lr * LDSK + lq * 4) = x0;
+      *reinterpret_cast<f32x4*>(A + (lr + 32) * LDSK + lq * 4) = x1;
+    } else {
+      // row: 32 hi halves (bytes 0..63) then 32 lo halves (64..127)
+      h4 h0, l0, h1, l1;
+      split4(x0, h0, l0);
+      split4(x1, h1, l1);
+      _Float16* a0 = reinterpret_cast<_Float16*>(A + lr * LDSK) + lq * 4;
+      _Float16* a1 = reinterpret_cast<_Float16*>(A + (lr + 32) * LDSK) + lq * 4;
+      *reinterpret_cast<h4*>(a0) = h0;
+      *reinterpret_cast<h4*>(a1) = h1;
+      if constexpr (PREC == RAFT_PREC_F16X3) {
+        *reinterpret_cast<h4*>(a0 + 32) = l0;
+        *reinterpret_cast<h4*>(a1 + 32) = l1;
+      }
+    }
+    // the weight block arrives in the LDS row format of its precision
     *reinterpret_cast<f32x4*>(B + lr * LDSK + lq * 4) = rb[0];
     *reinterpret_cast<f32x4*>(B + (lr + 32) * LDSK + lq * 4) = rb[1];
   };
 
   f32x16 acc = {};
+  f32x16 accx = {};  // F16X3 cross terms (x 2048)
   const int arow = (wm * 32 + (lane & 31)) * LDSK + (lane >> 5) * 16;
   const int brow = (wn * 32 + (lane & 31)) * LDSK + (lane >> 5) * 16;
   auto compute = [&](int buf) {
     const float* A = gsm + buf * STAGE;
     const float* B = A + BM * LDSK;
-    f32x4 av[4], bv[4];
+    if constexpr (PREC == RAFT_PREC_FP32) {
+      f32x4 av[4], bv[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      av[j] = *reinterpret_cast<const f32x4*>(A + arow + 4 * j);
-      bv[j] = *reinterpret_cast<const f32x4*>(B + brow + 4 * j);
+      for (int j = 0; j < 4; ++j) {
+        av[j] = *reinterpret_cast<const f32x4*>(A + arow + 4 * j);
+        bv[j] = *reinterpret_cast<const f32x4*>(B + brow + 4 * j);
+      }
+#pragma unroll
+      for (int s = 0; s < 16; ++s)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s >> 2][s & 3], bv[s >> 2][s & 3], acc, 0, 0, 0);
+    } else {
+      // lane half h takes k in [16h, 16h+16): MFMA q gets k = 16h + 8q + j,
+      // i.e. halves 8q.. of the lane's 16 (bytes 32h + 16q; lo at +64)
+      const _Float16* Ar = reinterpret_cast<const _Float16*>(A + arow - (lane >> 5) * 8);
+      const _Float16* Br = reinterpret_cast<const _Float16*>(B + brow - (lane >> 5) * 8);
+      h8 ah[2], bh[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        ah[q] = *reinterpret_cast<const h8*>(Ar + 8 * q);
+        bh[q] = *reinterpret_cast<const h8*>(Br + 8 * q);
+      }
+      if constexpr (PREC == RAFT_PREC_F16X3) {
+        h8 al[2], bl[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          al[q] = *reinterpret_cast<const h8*>(Ar + 32 + 8 * q);
+          bl[q] = *reinterpret_cast<const h8*>(Br + 32 + 8 * q);
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[q], bh[q], acc, 0, 0, 0);
+          accx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[q], bl[q], accx, 0, 0, 0);
+          accx = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[q], bh[q], accx, 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[q], bh[q], acc, 0, 0, 0);
+      }
     }
-#pragma unroll
-    for (int s = 0; s < 16; ++s)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s >> 2][s & 3], bv[s >> 2][s & 3], acc, 0, 0, 0);
   };
 
   // prologue: phases 0 and 1 in flight, phase 0 staged
@@ -302,6 +376,10 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(ConvArgs a) {
     issue(j + 4, ra0, rb0, am0);
   }
   if (j < cnt) compute(0);  // odd phase count: the last phase sits in buffer 0
+  if constexpr (PREC == RAFT_PREC_F16X3) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] += accx[r] * (1.0f / SPLIT_SCALE);
+  }
 
   if constexpr (KG > 1) {
     // sum the K-groups' accumulators through LDS: red[r][wave-in-group][lane]
@@ -384,6 +462,50 @@ __global__ __launch_bounds__(256) void conv_smalln_kernel(ConvArgs a) {
 }  // namespace raft
 
 using namespace raft;
+
+namespace {
+template <int MODE, int PREC>
+void launch_gemm_p(const ConvArgs& a, dim3 grid, bool two, hipStream_t s) {
+  if (two)
+    hipLaunchKernelGGL((conv_gemm_kernel<MODE, 2, PREC>), grid, dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_gemm_kernel<MODE, 1, PREC>), grid, dim3(256), 0, s, a);
+}
+template <int MODE>
+void launch_gemm_m(const ConvArgs& a, dim3 grid, bool two, hipStream_t s) {
+  switch (a.p.precision) {
+    case RAFT_PREC_F16X3: launch_gemm_p<MODE, RAFT_PREC_F16X3>(a, grid, two, s); break;
+    case RAFT_PREC_F16: launch_gemm_p<MODE, RAFT_PREC_F16>(a, grid, two, s); break;
+    default: launch_gemm_p<MODE, RAFT_PREC_FP32>(a, grid, two, s); break;
+  }
+}
+void launch_gemm(const ConvArgs& a, dim3 grid, bool two, hipStream_t s) {
+  if (a.p.mode == RAFT_CONV_VEC)
+    launch_gemm_m<RAFT_CONV_VEC>(a, grid, two, s);
+  else
+    launch_gemm_m<RAFT_CONV_GATHER>(a, grid, two, s);
+}
+
+// fp32 packed weight -> per (row, K-step): 32 f16 hi then 32 f16 lo (x 2048)
+__global__ void split_weight_kernel(const float* __restrict__ w, _Float16* __restrict__ out, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const float x = w[i];
+  const _Float16 h = (_Float16)x;
+  const long blk = i >> 5, k = i & 31;
+  out[blk * 64 + k] = h;
+  out[blk * 64 + 32 + k] = (_Float16)((x - (float)h) * SPLIT_SCALE);
+}
+}  // namespace
+
+extern "C" int raft_conv2d_split_weight(const float* w, void* out, int n_pad, int k_pad, raft_stream_t stream) {
+  RAFT_REQUIRE(w && out && n_pad > 0 && k_pad > 0 && k_pad % BK == 0, "raft_conv2d_split_weight: bad args");
+  RAFT_REQUIRE((const void*)w != out, "raft_conv2d_split_weight: in-place split is not supported");
+  const long total = (long)n_pad * k_pad;
+  hipLaunchKernelGGL(split_weight_kernel, dim3((unsigned)cdiv_l(total, 256)), dim3(256), 0, as_stream(stream), w,
+                     reinterpret_cast<_Float16*>(out), total);
+  return check_launch("raft_conv2d_split_weight");
+}
 
 extern "C" int raft_conv2d_packed_shape(int mode, int n, int kh, int kw, int cin, int* n_pad, int* k_pad) {
   RAFT_REQUIRE(n > 0 && kh > 0 && kw > 0 && cin > 0 && n_pad && k_pad, "raft_conv2d_packed_shape: bad args");
@@ -472,19 +594,11 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
       hipLaunchKernelGGL(conv_smalln_kernel<4>, grid, dim3(256), 0, s, a);
     return check_launch("raft_conv2d(small n)");
   }
+  RAFT_REQUIRE(p.precision == RAFT_PREC_FP32 || p.precision == RAFT_PREC_F16X3 || p.precision == RAFT_PREC_F16,
+               "raft_conv2d: unknown precision %d", p.precision);
   dim3 grid(cdiv(a.M, BM), n_pad / BN);
   // few tiles (fewer than ~4 per CU): two K-groups per tile give every SIMD two waves
   const bool two = (long)grid.x * grid.y < 1024 && a.K / BK >= 4;
-  if (p.mode == RAFT_CONV_VEC) {
-    if (two)
-      hipLaunchKernelGGL((conv_gemm_kernel<RAFT_CONV_VEC, 2>), grid, dim3(512), 0, s, a);
-    else
-      hipLaunchKernelGGL((conv_gemm_kernel<RAFT_CONV_VEC, 1>), grid, dim3(256), 0, s, a);
-  } else {
-    if (two)
-      hipLaunchKernelGGL((conv_gemm_kernel<RAFT_CONV_GATHER, 2>), grid, dim3(512), 0, s, a);
-    else
-      hipLaunchKernelGGL((conv_gemm_kernel<RAFT_CONV_GATHER, 1>), grid, dim3(256), 0, s, a);
-  }
+  launch_gemm(a, grid, two, s);
   return check_launch("raft_conv2d");
 }

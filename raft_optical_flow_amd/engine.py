@@ -32,7 +32,7 @@ import torch
 
 from . import _lib
 from . import kernels as K
-from .kernels import Launch, PackedConv, Rows, conv_launch, conv_params, pack_conv, fold_bn
+from .kernels import Launch, PackedConv, Rows, conv_launch, conv_params, pack_conv, fold_bn, set_precision
 
 # ----------------------------------------------------------------------------
 # Weight packing
@@ -134,7 +134,7 @@ class PackedUpdate:
 
 
 class PackedRaft:
-    def __init__(self, model, device):
+    def __init__(self, model, device, precision=_lib.PREC_FP32):
         self.small = bool(model.args.small)
         self.hdim, self.cdim = model.hidden_dim, model.context_dim
         self.radius = model.args.corr_radius
@@ -143,6 +143,8 @@ class PackedRaft:
         self.cnet = PackedEncoder(model.cnet, device)
         self.update = PackedUpdate(model.update_block, self.small, device)
         self.fdim = self.fnet.head.n
+        self.precision = precision
+        set_precision(self, precision)
 
 
 # ----------------------------------------------------------------------------

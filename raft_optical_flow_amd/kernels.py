@@ -64,7 +64,7 @@ class Rows:
 
 
 # ----------------------------------------------------------------------------
-# Convolution (implicit GEMM, fp32 MFMA)
+# Convolution (implicit GEMM on MFMA)
 # ----------------------------------------------------------------------------
 
 
@@ -80,6 +80,44 @@ class PackedConv:
     pad: tuple
     mode: int
     cin_real: int = 0         # input channels of the original weight (FLOP accounting)
+    precision: int = _lib.PREC_FP32
+    split: torch.Tensor | None = None   # hi/lo f16 form of `weight` (F16X3 / F16), made on first use
+
+    def launch_precision(self) -> int:
+        # N <= 4 convs run on the VALU kernel, which reads the fp32 weight
+        return self.precision if self.n > 4 else _lib.PREC_FP32
+
+    def launch_weight(self) -> torch.Tensor:
+        if self.launch_precision() == _lib.PREC_FP32:
+            return self.weight
+        if self.split is None:
+            w = self.weight
+            self.split = torch.empty_like(w)
+            _lib.call("raft_conv2d_split_weight", w.data_ptr(), self.split.data_ptr(), w.shape[0], w.shape[1],
+                      stream_handle())
+        return self.split
+
+
+def set_precision(obj, precision: int, _seen=None):
+    """Set the conv arithmetic of every PackedConv reachable from obj (attributes, lists, dicts)."""
+    _seen = set() if _seen is None else _seen
+    if id(obj) in _seen:
+        return
+    _seen.add(id(obj))
+    if isinstance(obj, PackedConv):
+        if obj.precision != precision:
+            obj.precision = precision
+        return
+    if isinstance(obj, (list, tuple)):
+        items = obj
+    elif isinstance(obj, dict):
+        items = obj.values()
+    elif hasattr(obj, "__dict__") and not isinstance(obj, torch.Tensor):
+        items = vars(obj).values()
+    else:
+        return
+    for v in items:
+        set_precision(v, precision, _seen)
 
 
 def pack_conv(weight: torch.Tensor, bias: torch.Tensor | None, stride=1, padding=0,
@@ -159,7 +197,8 @@ def conv_params(pc: PackedConv, src0: Rows, batch: int, in_h: int, in_w: int, ou
     p.batch, p.in_h, p.in_w, p.out_h, p.out_w = batch, in_h, in_w, out_h, out_w
     p.kh, p.kw, p.stride_h, p.stride_w, p.pad_h, p.pad_w = pc.kh, pc.kw, sh, sw, ph, pw
     p.mode = pc.mode
-    p.weight = pc.weight.data_ptr()
+    p.weight = pc.launch_weight().data_ptr()
+    p.precision = pc.launch_precision()
     p.bias = pc.bias.data_ptr() if pc.bias is not None else None
     p.n = pc.n
     p.out, p.out_ld = out.ptr, out.ld

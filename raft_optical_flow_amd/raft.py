@@ -26,8 +26,12 @@ from .update import BasicUpdateBlock, SmallUpdateBlock
 from .utils.utils import coords_grid
 
 # module attribute kept for API parity with core/raft.py:11-22 (callers monkeypatch it);
-# the HIP path itself never autocasts: it computes in fp32
+# the HIP path never autocasts: its arithmetic is RAFT.conv_precision
 autocast = torch.amp.autocast
+
+# default conv arithmetic of an fp32 model (include/raft_hip.h, RAFT_PREC_*):
+# "f16x3" = fp32-accurate split-f16 MFMA, "fp32" = f32 MFMA
+DEFAULT_PRECISION = "f16x3"
 
 
 class RAFT(nn.Module):
@@ -60,6 +64,9 @@ class RAFT(nn.Module):
             self.update_block = BasicUpdateBlock(self.args, hidden_dim=hdim)
         # execution state (not part of state_dict)
         self.hip_graph = bool(getattr(args, "hip_graph", False))
+        # conv arithmetic: "fp32" | "f16x3" | "f16"; args.mixed_precision (the
+        # reference's fp16 autocast, core/raft.py:156) selects "f16"
+        self.conv_precision = getattr(args, "conv_precision", None)
         self._packed = None
         self._packed_key = None
         self._plans = {}
@@ -93,11 +100,20 @@ class RAFT(nn.Module):
         return tuple((p.data_ptr(), p._version) for p in self.parameters()) + tuple(
             (b.data_ptr(), b._version) for b in self.buffers())
 
+    def resolved_precision(self) -> str:
+        from . import _lib
+        prec = self.conv_precision or ("f16" if self.args.mixed_precision else DEFAULT_PRECISION)
+        if prec not in _lib.PRECISIONS:
+            raise ValueError(f"conv_precision must be one of {sorted(_lib.PRECISIONS)}, got {prec!r}")
+        return prec
+
     def packed(self, device):
-        key = (self._weights_key(), str(device))
+        from . import _lib
+        prec = self.resolved_precision()
+        key = (self._weights_key(), str(device), prec)
         if self._packed is None or self._packed_key != key:
             with torch.no_grad():
-                self._packed = PackedRaft(self, device)
+                self._packed = PackedRaft(self, device, _lib.PRECISIONS[prec])
             self._packed_key = key
             self._plans = {}
         return self._packed

@@ -1,7 +1,7 @@
 """GPU parity: the HIP path (through the C-ABI) against the golden vectors of the
 reference and against the numpy oracle.  Tolerances (max-abs, fp32):
   lookup / pyramid   1e-5   (values O(1..10))
-  conv GEMM          1e-4 x max|ref| scale
+  conv GEMM          1e-4 x max|ref| scale (fp32, f16x3); 5e-3 (f16, one half-precision product)
   update block       1e-4
   end-to-end flow    1e-3   (north_star bound on the final flow field)
 """
@@ -39,10 +39,11 @@ def _gpu():
     _lib.load()
 
 
-def make_model(small, seed=0, alternate=False):
+def make_model(small, seed=0, alternate=False, precision=None):
     from raft_optical_flow_amd import RAFT
     from raft_optical_flow_amd.init import seeded_state_dict
     m = RAFT(argparse.Namespace(small=small, mixed_precision=False, alternate_corr=alternate))
+    m.conv_precision = precision
     sd = seeded_state_dict(m, seed)
     m.load_state_dict(sd)
     return m.to(DEV).eval(), {k: v.numpy() for k, v in sd.items()}
@@ -170,8 +171,12 @@ CONV_CASES = [
 ]
 
 
+CONV_TOL = {"fp32": 1e-4, "f16x3": 1e-4, "f16": 5e-3}
+
+
+@pytest.mark.parametrize("prec", ["fp32", "f16x3", "f16"])
 @pytest.mark.parametrize("cin,cout,kh,kw,stride,pad,H,W,B", CONV_CASES)
-def test_conv2d_vs_torch_fp64(cin, cout, kh, kw, stride, pad, H, W, B):
+def test_conv2d_vs_torch_fp64(cin, cout, kh, kw, stride, pad, H, W, B, prec):
     from raft_optical_flow_amd import kernels as K
     from raft_optical_flow_amd import _lib
     g = torch.Generator().manual_seed(cin * 1000 + cout)
@@ -180,16 +185,34 @@ def test_conv2d_vs_torch_fp64(cin, cout, kh, kw, stride, pad, H, W, B):
     b = torch.randn(cout, generator=g)
     ref = F.conv2d(x.double(), w.double(), b.double(), stride, pad)
     pc = K.pack_conv(w, b, stride, pad, device=DEV)
+    pc.precision = _lib.PRECISIONS[prec]
     src = K.Rows(K.nchw_to_rows(x.to(DEV)))
     ho, wo = ref.shape[-2:]
     out = K.Rows(torch.empty(B * ho * wo, cout, device=DEV))
     K.conv2d_rows(pc, src, B, H, W, out, epilogue=_lib.EPI_LINEAR)
     y = K.rows_to_nchw(out, B, ho, wo)
     err = maxabs(y, ref)
-    assert err < 1e-4 * max(1.0, float(ref.abs().max())), err
+    assert err < CONV_TOL[prec] * max(1.0, float(ref.abs().max())), err
 
 
-def test_conv2d_two_segments_and_gru_epilogues():
+def test_conv2d_split_weight_layout():
+    """raft_conv2d_split_weight: per 32-wide K-step, 32 f16 hi then 32 f16 lo (x2048)."""
+    from raft_optical_flow_amd import _lib
+    g = torch.Generator().manual_seed(11)
+    w = (torch.randn(64, 96, generator=g) * 0.05).to(DEV)
+    out = torch.empty_like(w)
+    _lib.call("raft_conv2d_split_weight", w.data_ptr(), out.data_ptr(), 64, 96, 0)
+    torch.cuda.synchronize()
+    h = out.view(torch.float16).view(64, 3, 2, 32)
+    hi = w.view(64, 3, 32).half()
+    lo = ((w.view(64, 3, 32) - hi.float()) * 2048).half()
+    assert torch.equal(h[:, :, 0], hi) and torch.equal(h[:, :, 1], lo)
+    rec = h[:, :, 0].double() + h[:, :, 1].double() / 2048
+    assert float((rec - w.view(64, 3, 32).double()).abs().max()) < 2.0 ** -22 * 0.25
+
+
+@pytest.mark.parametrize("prec", ["fp32", "f16x3"])
+def test_conv2d_two_segments_and_gru_epilogues(prec):
     """Virtual concat [RH | x] + the GRU z/r and q epilogues vs a torch restatement."""
     from raft_optical_flow_amd import kernels as K
     from raft_optical_flow_amd import _lib
@@ -211,6 +234,7 @@ def test_conv2d_two_segments_and_gru_epilogues():
     RH = torch.empty(B * H * W, hd, device=DEV)
     pzr = K.pack_conv(torch.cat([wz, wr]), torch.cat([bz, br]), 1, (0, 2), device=DEV)
     pq = K.pack_conv(wq, bq, 1, (0, 2), seg_real=[hd, xd], device=DEV)
+    pzr.precision = pq.precision = _lib.PRECISIONS[prec]
     hrows = K.Rows(HX, 0, hd)
     K.conv2d_rows(pzr, K.Rows(HX), B, H, W, K.Rows(Z), epilogue=_lib.EPI_GRU_ZR, split=hd, aux0=hrows,
                   out1=K.Rows(RH))
@@ -267,10 +291,11 @@ E2E = [("raft_full_smooth_b2_128x192_i12", False, False),
        ("raft_small_smooth_b1_128x192_i12", True, False)]
 
 
+@pytest.mark.parametrize("prec", ["fp32", "f16x3"])
 @pytest.mark.parametrize("name,small,alt", E2E)
-def test_raft_e2e_golden(name, small, alt):
+def test_raft_e2e_golden(name, small, alt, prec):
     g = load_golden(name + ".npz")
-    m, _ = make_model(small, int(g["seed"]), alternate=alt)
+    m, _ = make_model(small, int(g["seed"]), alternate=alt, precision=prec)
     with torch.no_grad():
         low, up = m(t(g["image1"]), t(g["image2"]), iters=int(g["iters"]), test_mode=True)
     assert maxabs(low, g["flow_low"]) < 1e-3
@@ -304,16 +329,35 @@ def test_raft_flow_init_warm_start():
     assert maxabs(low, rlow) < 1e-3 and maxabs(up, rup) < 1e-3
 
 
-def test_raft_full_size_golden():
+@pytest.mark.parametrize("prec", ["fp32", "f16x3"])
+def test_raft_full_size_golden(prec):
     """Config 2 shape: B=1, 436x1024 padded to 440x1024, iters=32."""
     from raft_optical_flow_amd.init import seeded_images
     g = load_golden("raft_full_rand_b1_440x1024_i32.npz")
-    m, _ = make_model(False, int(g["seed"]))
+    m, _ = make_model(False, int(g["seed"]), precision=prec)
     i1, i2 = seeded_images(1, 440, 1024, seed=int(g["img_seed"]))
     with torch.no_grad():
         low, up = m(i1.to(DEV), i2.to(DEV), iters=32, test_mode=True)
-    assert maxabs(low, g["flow_low"]) < 1e-3
-    assert maxabs(up[:, :, ::8], g["flow_up_rows8"]) < 1e-3
+    err = (maxabs(low, g["flow_low"]), maxabs(up[:, :, ::8], g["flow_up_rows8"]))
+    print(f"full-size {prec}: flow_low {err[0]:.3g} flow_up {err[1]:.3g}")
+    assert err[0] < 1e-3 and err[1] < 1e-3
+
+
+def test_raft_mixed_precision_band():
+    """args.mixed_precision -> one f16 product per MAC (the reference autocasts to fp16,
+    core/raft.py:156): its own band against the fp32 reference flow."""
+    from raft_optical_flow_amd import RAFT
+    from raft_optical_flow_amd.init import seeded_state_dict
+    g = load_golden("raft_full_rand_b1_128x192_i32.npz")
+    m = RAFT(argparse.Namespace(small=False, mixed_precision=True, alternate_corr=False))
+    m.load_state_dict(seeded_state_dict(m, int(g["seed"])))
+    m.to(DEV).eval()
+    assert m.resolved_precision() == "f16"
+    with torch.no_grad():
+        low, up = m(t(g["image1"]), t(g["image2"]), iters=int(g["iters"]), test_mode=True)
+    d = (up.cpu().double() - torch.from_numpy(g["flow_up"]).double()).abs()
+    print(f"f16 band: max {float(d.max()):.3g} mean {float(d.mean()):.3g}")
+    assert float(d.max()) < 0.5 and float(d.mean()) < 0.05
 
 
 def test_raft_small_demo_frames_golden():

@@ -1,4 +1,6 @@
-"""Time each update-block convolution shape of RAFT-full at B x 55 x 128 in isolation."""
+"""Time each update-block convolution shape of RAFT-full at B x 55 x 128 in isolation.
+
+    python tools/conv_bench.py B [name,name...]      (PREC=fp32|f16x3|f16, default f16x3)"""
 import sys
 import time
 
@@ -10,6 +12,7 @@ from raft_optical_flow_amd import kernels as K
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1
 ONLY = sys.argv[2].split(",") if len(sys.argv) > 2 else None
+PREC = __import__("os").environ.get("PREC", "f16x3")
 H, W = 55, 128
 dev = "cuda"
 SHAPES = [  # name, cin, cout, kh, kw, pad
@@ -24,6 +27,7 @@ for name, cin, cout, kh, kw, pad in SHAPES:
     x = torch.randn(B * H * W, cin, device=dev)
     w = torch.randn(cout, cin, kh, kw) * 0.05
     pc = K.pack_conv(w, torch.zeros(cout), 1, pad, device=dev)
+    pc.precision = _lib.PRECISIONS[PREC]
     out = torch.empty(B * H * W, cout, device=dev)
     prm = K.conv_params(pc, K.Rows(x), B, H, W, K.Rows(out), epilogue=_lib.EPI_RELU)
     L = [K.conv_launch(prm)]
@@ -42,4 +46,4 @@ for name, cin, cout, kh, kw, pad in SHAPES:
     fl = 2.0 * B * H * W * cout * cin * kh * kw
     tot_t += us
     print(f"{name:8s} M={B*H*W:6d} N={cout:4d} K={cin*kh*kw:5d}  {us:8.1f} us  {fl/us/1e6:7.1f} TF/s")
-print(f"total {tot_t:.1f} us")
+print(f"total {tot_t:.1f} us ({PREC})")

@@ -3,8 +3,10 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 TAG=${1:-dev}
-timeout -k 10 500 python -m pytest tests/test_gpu_parity.py -q -m gpu -x > gpurun_out/gpu_$TAG.log 2>&1
-echo "tests rc=$?"; tail -3 gpurun_out/gpu_$TAG.log
+timeout -k 10 500 python -m pytest tests/test_gpu_parity.py -q -m gpu -x -s > gpurun_out/gpu_$TAG.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -15 gpurun_out/gpu_$TAG.log
+# a crash / abort / timeout ends the GPU work of this call (plain test failures do not)
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 400 python bench.py --steps 20 --warmup 3 ${BENCH_ARGS} > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo bench failed; tail -20 gpurun_out/bench_$TAG.err; exit 1; }
 cat gpurun_out/bench_$TAG.json
 if [ -n "$PROFILE" ]; then
