@@ -40,6 +40,16 @@ __host__ __device__ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 __host__ __device__ inline int round_up(int a, int b) { return cdiv(a, b) * b; }
 __host__ __device__ inline long cdiv_l(long a, long b) { return (a + b - 1) / b; }
 
+// XCD-aware tile order.  The dispatcher deals work-groups round-robin over the
+// 8 XCDs (work-group L -> XCD L % 8), each with its own L2; hand XCD c a
+// contiguous run of the logical tile order so tiles that share operand rows
+// (and neighbouring pixels under a conv's taps) hit the same L2.
+__device__ inline int xcd_tile(int L, int T) {
+  const int c = L & 7, slot = L >> 3;
+  const int per = T >> 3, rem = T & 7;
+  return c * per + (c < rem ? c : rem) + slot;
+}
+
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 

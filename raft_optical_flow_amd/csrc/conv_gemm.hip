@@ -44,7 +44,10 @@ constexpr int BN = 64;
 constexpr int BK = 32;
 constexpr int LDSK = BK + 4;
 constexpr int STAGE = (BM + BN) * LDSK;       // floats per LDS buffer
-constexpr int MAX_GATHER_K = 1024;            // k_pad limit of GATHER mode (LDS table)
+constexpr int MAX_GATHER_K = 1024;
+#ifndef GEMM_NS
+#define GEMM_NS 2                                 // staging register sets (K-steps in flight)
+#endif            // k_pad limit of GATHER mode (LDS table)
 
 struct ConvArgs {
   raft_conv2d_params p;
@@ -53,6 +56,7 @@ struct ConvArgs {
   int ctot;     // in0_c + in1_c
   int cpad;     // VEC: channels per tap in the packed weight (multiple of BK)
   int taps;     // kh * kw
+  int gn;       // N-tiles
   unsigned w_bytes, in0_bytes, in1_bytes;  // buffer-descriptor ranges
 };
 
@@ -120,10 +124,10 @@ __device__ __forceinline__ void epilogue(const raft_conv2d_params& p, long m, in
 struct AWalk {
   int pb[2], py[2], px[2];
   bool pv[2];
-  // VEC mode: the rows' input pixel index for the current tap, and whether it
-  // is inside the image (named scalars, not arrays: no scratch)
-  unsigned pix0, pix1;
-  bool in0, in1;
+  // VEC mode, current tap: the rows' input-pixel byte offsets in segment 0 / 1
+  // (OFF_INVALID outside the image: the buffer load returns 0).  Named
+  // scalars, not arrays: a runtime-selected array element goes to scratch.
+  unsigned o0s0, o1s0, o0s1, o1s1;
   int tap;
 };
 
@@ -134,24 +138,27 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, unsig
 }
 
 __device__ __forceinline__ f32x4 buf_load4(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
-  using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 
 // VEC: recompute the rows' pixel offsets when the K walk enters a new tap
 // (once per c_pad/32 K-steps; all tap/step bookkeeping is wave-uniform).
-__device__ __forceinline__ void vec_set_tap(const ConvArgs& a, AWalk& w, int tap) {
-  const raft_conv2d_params& p = a.p;
+__device__ __forceinline__ void vec_set_tap(const raft_conv2d_params& p, unsigned ld0b, unsigned ld1b, AWalk& w,
+                                            int tap) {
   const int ky = tap / p.kw, kx = tap - ky * p.kw;
   {
     const int iy = w.py[0] + ky, ix = w.px[0] + kx;
-    w.in0 = w.pv[0] && (unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w;
-    w.pix0 = (unsigned)((w.pb[0] * p.in_h + iy) * p.in_w + ix);
+    const bool in = w.pv[0] && (unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w;
+    const unsigned pix = (unsigned)((w.pb[0] * p.in_h + iy) * p.in_w + ix);
+    w.o0s0 = in ? pix * ld0b : OFF_INVALID;
+    w.o0s1 = in ? pix * ld1b : OFF_INVALID;
   }
   {
     const int iy = w.py[1] + ky, ix = w.px[1] + kx;
-    w.in1 = w.pv[1] && (unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w;
-    w.pix1 = (unsigned)((w.pb[1] * p.in_h + iy) * p.in_w + ix);
+    const bool in = w.pv[1] && (unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w;
+    const unsigned pix = (unsigned)((w.pb[1] * p.in_h + iy) * p.in_w + ix);
+    w.o1s0 = in ? pix * ld0b : OFF_INVALID;
+    w.o1s1 = in ? pix * ld1b : OFF_INVALID;
   }
   w.tap = tap;
 }
@@ -187,8 +194,9 @@ __device__ __forceinline__ unsigned gather_a(const ConvArgs& a, const AWalk& w, 
 // double buffer, so each SIMD carries KG waves of the tile that interleave
 // (one group's MFMAs cover the other's LDS reads, barrier skew and staging).
 // The groups' accumulators are summed through LDS before the epilogue.
-template <int MODE, int KG, int PREC>
+template <int MODE, int KG, int PREC, int NS>
 __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(ConvArgs a) {
+  static_assert(NS % 2 == 0, "NS must be even (LDS buffer parity follows the unrolled phase index)");
   __shared__ __attribute__((aligned(16))) float
       smem[KG * 2 * STAGE + (MODE == RAFT_CONV_GATHER ? MAX_GATHER_K : 0)];
   const raft_conv2d_params& p = a.p;
@@ -199,8 +207,11 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(ConvArgs a) {
   const int wl = wave & 3;          // wave within the group
   const int wm = wl & 1, wn = wl >> 1;
   const int lt = tid & 255;         // thread within the group
-  const int m0 = blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
+  // 1-D grid of gm x gn tiles in XCD order, N fastest (an M-tile's N-tiles share its A rows)
+  const int q = xcd_tile(blockIdx.x, gridDim.x);
+  const int gn = a.gn;
+  const int m0 = (q / gn) * BM;
+  const int n0 = (q - (q / gn) * gn) * BN;
   int* ktab = reinterpret_cast<int*>(smem + KG * 2 * STAGE);
   float* gsm = smem + g * 2 * STAGE;  // this group's two LDS buffers
 
@@ -231,50 +242,64 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(ConvArgs a) {
   }
   w.tap = -1;
   const int nk = a.K / BK;
-  const int cpt = a.cpad / BK;  // K-steps per tap (VEC)
-  // buffer descriptors: wave-uniform (kernel arguments only)
+  // wave-uniform operands, read once from the kernel arguments (readfirstlane'd
+  // so the per-step selects stay scalar: no kernarg reloads, no waterfalls)
+  const unsigned rfl_in0c = __builtin_amdgcn_readfirstlane(p.in0_c);
+  const unsigned rfl_in1c = __builtin_amdgcn_readfirstlane(p.in1_c);
+  const unsigned ld0b = __builtin_amdgcn_readfirstlane(p.in0_ld) * 4u;
+  const unsigned ld1b = __builtin_amdgcn_readfirstlane(p.in1_c ? p.in1_ld : p.in0_ld) * 4u;
+  const unsigned long long b0 = (unsigned long long)p.in0;
+  const unsigned long long b1 = p.in1_c ? (unsigned long long)p.in1 : b0;
+  const unsigned b0lo = __builtin_amdgcn_readfirstlane((unsigned)b0), b0hi = __builtin_amdgcn_readfirstlane((unsigned)(b0 >> 32));
+  const unsigned b1lo = __builtin_amdgcn_readfirstlane((unsigned)b1), b1hi = __builtin_amdgcn_readfirstlane((unsigned)(b1 >> 32));
+  const unsigned nrec0 = __builtin_amdgcn_readfirstlane(a.in0_bytes);
+  const unsigned nrec1 = __builtin_amdgcn_readfirstlane(p.in1_c ? a.in1_bytes : a.in0_bytes);
+  const int cpad = __builtin_amdgcn_readfirstlane(a.cpad);
   const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(p.weight, a.w_bytes);
-  const __amdgpu_buffer_rsrc_t rs_0 = make_rsrc(p.in0, a.in0_bytes);
-  const __amdgpu_buffer_rsrc_t rs_1 = make_rsrc(p.in1_c ? p.in1 : p.in0, a.in1_bytes);
   const unsigned wvoff0 = ((unsigned)(n0 + lr) * (unsigned)a.K + lq * 4) * 4u;
   const unsigned wvoff1 = wvoff0 + 32u * (unsigned)a.K * 4u;
   const int cnt = g < nk ? (nk - g + KG - 1) / KG : 0;  // this group's K-steps
   const int nj = (nk + KG - 1) / KG;                     // phases (group 0's count)
-  f32x4 ra0[2], rb0[2], ra1[2], rb1[2];  // two staging register sets (phases of even / odd parity)
-  unsigned am0 = 0, am1 = 0;             // their A validity masks
+  f32x4 ra[NS][2], rb[NS][2];  // NS staging register sets: K-steps t+1 .. t+NS-1 in flight during phase t
+  unsigned am[NS];             // their A validity masks
 
-  // issue() is unconditional: phases beyond this group's count re-read the last
-  // K-step (clamped, never consumed) so every phase has the same load count
-  auto issue = [&](int j, f32x4(&ra)[2], f32x4(&rb)[2], unsigned& am) {
-    const int kc = min(g + KG * j, nk - 1);
+  // the K walk of issue(): this group's next K-step as (tap, first channel cs)
+  // and weight byte offset, advanced incrementally (issue() runs in step order)
+  int wtap = (g * BK) / cpad, wcs = g * BK - wtap * cpad;
+  unsigned wsoff = (unsigned)g * BK * 4u;
+  int kstep = g;
+
+  // issue() is unconditional: steps beyond this group's count load harmless
+  // data (zeros past the buffer ends, never consumed) so every phase has the
+  // same load count and hipcc's counted vmcnt stays exact
+  auto issue = [&](f32x4(&ra)[2], f32x4(&rb)[2], unsigned& am) {
     if constexpr (MODE == RAFT_CONV_VEC) {
-      const int tap = kc / cpt;
-      if (tap != w.tap) vec_set_tap(a, w, tap);
-      const int cs = (kc - tap * cpt) * BK;  // first channel of this K-step (uniform)
-      const bool s0 = cs < p.in0_c;
-      const int cl = cs + lq * 4;          // this lane's channel
-      const bool lane_ok = s0 ? cl < p.in0_c : cl - p.in0_c < p.in1_c;
-      const unsigned soff = (unsigned)(s0 ? cs : cs - p.in0_c) * 4u;
-      // the segment's descriptor, rebuilt from readfirstlane'd (provably uniform)
-      // words so hipcc keeps it in SGPRs (no waterfall loop around the loads)
-      const unsigned long long base = s0 ? (unsigned long long)p.in0 : (unsigned long long)p.in1;
-      const unsigned blo = __builtin_amdgcn_readfirstlane((unsigned)base);
-      const unsigned bhi = __builtin_amdgcn_readfirstlane((unsigned)(base >> 32));
-      const unsigned nrec = __builtin_amdgcn_readfirstlane(s0 ? a.in0_bytes : a.in1_bytes);
+      if (wtap != w.tap) vec_set_tap(p, ld0b, ld1b, w, wtap);
+      const bool s0 = (unsigned)wcs < rfl_in0c;  // uniform: the K-step lies in segment 0
+      const unsigned cl = (unsigned)(wcs + lq * 4);
+      const bool lane_ok = s0 ? cl < rfl_in0c : cl - rfl_in0c < rfl_in1c;
+      const unsigned soff = (unsigned)(s0 ? wcs : wcs - (int)rfl_in0c) * 4u;
+      const unsigned blo = s0 ? b0lo : b1lo, bhi = s0 ? b0hi : b1hi, nrec = s0 ? nrec0 : nrec1;
       const __amdgpu_buffer_rsrc_t rs =
           make_rsrc(reinterpret_cast<const void*>(((unsigned long long)bhi << 32) | blo), nrec);
-      const unsigned ldb = (unsigned)(s0 ? p.in0_ld : p.in1_ld) * 4u;  // row pitch in bytes (uniform)
-      const unsigned v0 = (lane_ok && w.in0) ? w.pix0 * ldb + lq * 16u : OFF_INVALID;
-      const unsigned v1 = (lane_ok && w.in1) ? w.pix1 * ldb + lq * 16u : OFF_INVALID;
+      const unsigned r0 = s0 ? w.o0s0 : w.o0s1, r1 = s0 ? w.o1s0 : w.o1s1;
+      const unsigned v0 = (lane_ok && r0 != OFF_INVALID) ? r0 + lq * 16u : OFF_INVALID;
+      const unsigned v1 = (lane_ok && r1 != OFF_INVALID) ? r1 + lq * 16u : OFF_INVALID;
       ra[0] = buf_load4(rs, v0, soff);
       ra[1] = buf_load4(rs, v1, soff);
       am = 0xFFu;
+      wcs += KG * BK;
+      while (wcs >= cpad) {
+        wcs -= cpad;
+        ++wtap;
+      }
     } else {
-      am = gather_a(a, w, kc, lq, ktab, ra);
+      am = gather_a(a, w, min(kstep, nk - 1), lq, ktab, ra);
     }
-    const unsigned ws = (unsigned)kc * BK * 4u;
-    rb[0] = buf_load4(rs_w, wvoff0, ws);
-    rb[1] = buf_load4(rs_w, wvoff1, ws);
+    rb[0] = buf_load4(rs_w, wvoff0, wsoff);
+    rb[1] = buf_load4(rs_w, wvoff1, wsoff);
+    wsoff += KG * BK * 4u;
+    kstep += KG;
   };
   auto stage = [&](int buf, const f32x4(&ra)[2], const f32x4(&rb)[2], unsigned am) {
     float* A = gsm + buf * STAGE;
@@ -355,27 +380,40 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(ConvArgs a) {
     }
   };
 
-  // prologue: phases 0 and 1 in flight, phase 0 staged
-  issue(0, ra0, rb0, am0);
-  issue(1, ra1, rb1, am1);
-  stage(0, ra0, rb0, am0);
+  // prologue: K-steps 0 .. NS-1 in flight, step 0 staged, its set refilled with step NS
+#pragma unroll
+  for (int u = 0; u < NS; ++u) issue(ra[u], rb[u], am[u]);
+  stage(0, ra[0], rb[0], am[0]);
   __syncthreads();
-  issue(2, ra0, rb0, am0);
+  issue(ra[0], rb[0], am[0]);
 
-  // steady state, unrolled by two so the register sets are static; loads and
-  // LDS stores are branch-free, only the MFMA phases are predicated (uniformly)
-  int j = 0;
-  for (; j + 2 <= nj; j += 2) {
-    if (j < cnt) compute(0);
-    stage(1, ra1, rb1, am1);
-    __syncthreads();
-    issue(j + 3, ra1, rb1, am1);
-    if (j + 1 < cnt) compute(1);
-    stage(0, ra0, rb0, am0);
-    __syncthreads();
-    issue(j + 4, ra0, rb0, am0);
+  // phase t: MFMAs on LDS buffer t&1 (step t); stage step t+1 (set (t+1)%NS) into
+  // the other buffer; one barrier; refill the freed set with step t+1+NS.  The
+  // body is unrolled NS times so every register set index is static, and the
+  // main loop is branch-free around the loads (only the MFMAs are predicated,
+  // on a wave-uniform count), so hipcc's counted vmcnt keeps NS-1 K-steps in
+  // flight.  The < NS tail phases issue nothing more.
+  const int nfull = nj - nj % NS;
+  for (int j = 0; j < nfull; j += NS) {
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      if (j + u < cnt) compute(u & 1);
+      stage((u + 1) & 1, ra[(u + 1) % NS], rb[(u + 1) % NS], am[(u + 1) % NS]);
+      __syncthreads();
+      issue(ra[(u + 1) % NS], rb[(u + 1) % NS], am[(u + 1) % NS]);
+    }
   }
-  if (j < cnt) compute(0);  // odd phase count: the last phase sits in buffer 0
+#pragma unroll
+  for (int u = 0; u < NS - 1; ++u) {
+    const int t = nfull + u;
+    if (t < nj) {
+      if (t < cnt) compute(u & 1);
+      if (t + 1 < nj) {
+        stage((u + 1) & 1, ra[(u + 1) % NS], rb[(u + 1) % NS], am[(u + 1) % NS]);
+        __syncthreads();
+      }
+    }
+  }
   if constexpr (PREC == RAFT_PREC_F16X3) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] += accx[r] * (1.0f / SPLIT_SCALE);
@@ -467,9 +505,9 @@ namespace {
 template <int MODE, int PREC>
 void launch_gemm_p(const ConvArgs& a, dim3 grid, bool two, hipStream_t s) {
   if (two)
-    hipLaunchKernelGGL((conv_gemm_kernel<MODE, 2, PREC>), grid, dim3(512), 0, s, a);
+    hipLaunchKernelGGL((conv_gemm_kernel<MODE, 2, PREC, GEMM_NS>), grid, dim3(512), 0, s, a);
   else
-    hipLaunchKernelGGL((conv_gemm_kernel<MODE, 1, PREC>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv_gemm_kernel<MODE, 1, PREC, GEMM_NS>), grid, dim3(256), 0, s, a);
 }
 template <int MODE>
 void launch_gemm_m(const ConvArgs& a, dim3 grid, bool two, hipStream_t s) {
@@ -596,9 +634,12 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
   }
   RAFT_REQUIRE(p.precision == RAFT_PREC_FP32 || p.precision == RAFT_PREC_F16X3 || p.precision == RAFT_PREC_F16,
                "raft_conv2d: unknown precision %d", p.precision);
-  dim3 grid(cdiv(a.M, BM), n_pad / BN);
+  a.gn = n_pad / BN;
+  const long tiles = (long)cdiv(a.M, BM) * a.gn;
+  RAFT_REQUIRE(tiles < (1L << 31), "raft_conv2d: too many tiles");
+  dim3 grid((unsigned)tiles);
   // few tiles (fewer than ~4 per CU): two K-groups per tile give every SIMD two waves
-  const bool two = (long)grid.x * grid.y < 1024 && a.K / BK >= 4;
+  const bool two = tiles < 1024 && a.K / BK >= 4;
   launch_gemm(a, grid, two, s);
   return check_launch("raft_conv2d");
 }
