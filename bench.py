@@ -66,15 +66,22 @@ def update_flops_per_pixel(pu, with_mask):
 
 
 def time_kernel_events(fn, reps):
-    """Average duration of fn() (one launch) with HIP events on the current stream."""
+    """Average GPU duration of fn() (kernel launches on the current stream): the reps
+    launches are captured in one hipGraph and timed with HIP events around its replay
+    on the launch stream, so host launch overhead is not part of the figure."""
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
     s = torch.cuda.current_stream()
     start = torch.cuda.Event(enable_timing=True)
     end = torch.cuda.Event(enable_timing=True)
-    fn()
-    torch.cuda.synchronize()
     start.record(s)
-    for _ in range(reps):
-        fn()
+    g.replay()
     end.record(s)
     end.synchronize()
     return start.elapsed_time(end) / reps * 1e-3  # seconds
@@ -191,11 +198,10 @@ def main():
 
     # ---- per-kernel live timing (HIP events on the launch stream) -------------------
     from raft_optical_flow_amd import kernels as K
-    s = K.stream_handle()
     lk = [l for l in plan.launches[plan.loop_start:plan.loop_end] if getattr(l, "name", None) in
           ("raft_corr_lookup", "raft_alt_corr_lookup_nhwc")]
     reps = 200
-    t_lookup = time_kernel_events(lambda: [l(s) for l in lk[:1 if not args.alternate_corr else 4]], reps)
+    t_lookup = time_kernel_events(lambda: [l(K.stream_handle()) for l in lk[:1 if not args.alternate_corr else 4]], reps)
     h8, w8 = H // 8, W // 8
     P = args.batch * h8 * w8
     bytes_per_launch = P * lookup_bytes_per_pixel()
@@ -213,7 +219,7 @@ def main():
     # one non-final iteration's conv GEMMs (no mask head)
     one_iter = upd[:n_iter_convs - 0]
     pu = plan.pk.update
-    t_upd = time_kernel_events(lambda: [l(s) for l in one_iter], 50)
+    t_upd = time_kernel_events(lambda: [l(K.stream_handle()) for l in one_iter], 50)
     fl = P * update_flops_per_pixel(pu, with_mask=False)
     upd_tf = fl / t_upd / 1e12
     peak = CONV_PEAK_TF[prec]

@@ -156,10 +156,10 @@ int raft_avgpool2_nhwc(const float* in, float* out, int B, int H, int W, int C, 
 #define RAFT_EPI_LINEAR 0         /* out = alpha * v                                          */
 #define RAFT_EPI_RELU 1           /* out = relu(v)                                            */
 #define RAFT_EPI_RESID_RELU 2     /* out = relu(aux0[m,n] + relu(v))    (ResidualBlock tail) */
-#define RAFT_EPI_GRU_ZR 3         /* n <  split: out[m,n] = sigmoid(v)               (z)      */
+#define RAFT_EPI_GRU_ZR 3         /* n <  split: out[m,n] = sigmoid(v) (z); split % 32 == 0      */
                                   /* n >= split: out1[m,n-split] = sigmoid(v)*aux0[m,n-split] (r*h) */
 #define RAFT_EPI_GRU_Q 4          /* q = tanh(v); out[m,n] = (1-aux1[m,n])*aux0[m,n] + aux1[m,n]*q */
-#define RAFT_EPI_TANH_RELU 5      /* n < split: out[m,n] = tanh(v); else out1[m,n-split] = relu(v) */
+#define RAFT_EPI_TANH_RELU 5      /* n < split: out[m,n] = tanh(v); else out1[m,n-split] = relu(v); split % 32 == 0 */
 #define RAFT_EPI_ADD_TO_OUT 6     /* out[m,n] = out[m,n] + v   (coords1 += delta_flow)         */
 
 typedef struct raft_conv2d_params {

@@ -120,6 +120,92 @@ __device__ __forceinline__ void epilogue(const raft_conv2d_params& p, long m, in
   }
 }
 
+// Epilogue of one 32x32 MFMA tile: lane owns column n and the 16 rows
+// mb + (r&3) + 8*(r>>2).  All operand loads of the 16 rows (add0, aux0/aux1,
+// the ADD_TO_OUT destination) are issued together from clamped addresses
+// before any store, and only the stores are predicated: on gfx9 stores share
+// vmcnt with loads, so a row-by-row load/store interleave would wait for every
+// earlier store to complete (one full write latency per row).
+__device__ __forceinline__ long row_of(int mb, int r) { return mb + (r & 3) + 8 * (r >> 2); }
+
+__device__ __forceinline__ void load_rows(const float* base, int ld, int M, int mb, int col, float (&t)[16]) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) t[r] = base[min(row_of(mb, r), (long)M - 1) * ld + col];
+}
+
+// branch-free activations (no per-row control flow between the stores)
+__device__ __forceinline__ float sigmoid_bf(float x) { return __frcp_rn(1.0f + __expf(-x)); }
+__device__ __forceinline__ float tanh_bf(float x) { return 1.0f - 2.0f * __frcp_rn(__expf(2.0f * x) + 1.0f); }
+
+__device__ __forceinline__ void tile_epilogue(const raft_conv2d_params& p, int M, int mb, int n, const f32x16& acc) {
+  const bool ncol = n < p.n;
+  const int nc = ncol ? n : p.n - 1;  // clamped column for loads
+  float v[16];
+  const float bias = p.bias ? p.bias[nc] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = acc[r] + bias;
+  if (p.add0) {
+    float t[16];
+    load_rows(p.add0, p.add0_ld, M, mb, nc, t);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] += t[r];
+  }
+  // 1) operand loads, 2) values, 3) stores: destination dst[row * ld + col]
+  float* dst = p.out;
+  int ld = p.out_ld, col = n;
+  const int epi = p.epilogue;
+  if (epi == RAFT_EPI_LINEAR) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] *= p.alpha;
+  } else if (epi == RAFT_EPI_RELU) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = fmaxf(v[r], 0.f);
+  } else if (epi == RAFT_EPI_RESID_RELU) {
+    float t[16];
+    load_rows(p.aux0, p.aux0_ld, M, mb, nc, t);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = fmaxf(t[r] + fmaxf(v[r], 0.f), 0.f);
+  } else if (epi == RAFT_EPI_GRU_ZR) {
+    if (nc < p.split) {  // a wave's 32 columns lie on one side of split (split % 32 == 0, host-checked)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = sigmoid_bf(v[r]);
+    } else {
+      col = nc - p.split;
+      float t[16];
+      load_rows(p.aux0, p.aux0_ld, M, mb, col, t);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = sigmoid_bf(v[r]) * t[r];
+      dst = p.out1;
+      ld = p.out1_ld;
+    }
+  } else if (epi == RAFT_EPI_GRU_Q) {
+    float h[16], z[16];
+    load_rows(p.aux0, p.aux0_ld, M, mb, nc, h);
+    load_rows(p.aux1, p.aux1_ld, M, mb, nc, z);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = (1.0f - z[r]) * h[r] + z[r] * tanh_bf(v[r]);
+  } else if (epi == RAFT_EPI_TANH_RELU) {
+    if (nc < p.split) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = tanh_bf(v[r]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = fmaxf(v[r], 0.f);
+      dst = p.out1;
+      ld = p.out1_ld;
+      col = n - p.split;
+    }
+  } else if (epi == RAFT_EPI_ADD_TO_OUT) {
+    float t[16];
+    load_rows(p.out, p.out_ld, M, mb, nc, t);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] += t[r];
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    if (ncol && row_of(mb, r) < M) dst[row_of(mb, r) * ld + col] = v[r];
+}
+
 // Per-thread staging state: two A rows (output pixels) of the tile.
 struct AWalk {
   int pb[2], py[2], px[2];
@@ -285,8 +371,14 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(ConvArgs a) {
       const unsigned r0 = s0 ? w.o0s0 : w.o0s1, r1 = s0 ? w.o1s0 : w.o1s1;
       const unsigned v0 = (lane_ok && r0 != OFF_INVALID) ? r0 + lq * 16u : OFF_INVALID;
       const unsigned v1 = (lane_ok && r1 != OFF_INVALID) ? r1 + lq * 16u : OFF_INVALID;
+#ifdef ABL_NOLOAD  // timing ablation (dev builds only): no A/B global loads
+      ra[0] = f32x4{(float)v0, 1.f, 2.f, 3.f};
+      ra[1] = f32x4{(float)v1, 1.f, 2.f, (float)soff};
+      (void)rs;
+#else
       ra[0] = buf_load4(rs, v0, soff);
       ra[1] = buf_load4(rs, v1, soff);
+#endif
       am = 0xFFu;
       wcs += KG * BK;
       while (wcs >= cpad) {
@@ -296,8 +388,13 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(ConvArgs a) {
     } else {
       am = gather_a(a, w, min(kstep, nk - 1), lq, ktab, ra);
     }
+#ifdef ABL_NOLOAD
+    rb[0] = f32x4{(float)wsoff, 1.f, 2.f, 3.f};
+    rb[1] = f32x4{(float)wsoff, 1.f, 2.f, 4.f};
+#else
     rb[0] = buf_load4(rs_w, wvoff0, wsoff);
     rb[1] = buf_load4(rs_w, wvoff1, wsoff);
+#endif
     wsoff += KG * BK * 4u;
     kstep += KG;
   };
@@ -397,9 +494,13 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(ConvArgs a) {
   for (int j = 0; j < nfull; j += NS) {
 #pragma unroll
     for (int u = 0; u < NS; ++u) {
+#ifndef ABL_NOCOMPUTE
       if (j + u < cnt) compute(u & 1);
+#endif
       stage((u + 1) & 1, ra[(u + 1) % NS], rb[(u + 1) % NS], am[(u + 1) % NS]);
+#ifndef ABL_NOBARRIER
       __syncthreads();
+#endif
       issue(ra[(u + 1) % NS], rb[(u + 1) % NS], am[(u + 1) % NS]);
     }
   }
@@ -439,14 +540,7 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(ConvArgs a) {
   }
 
   // ---- epilogue: lane owns column n, rows (r&3) + 8*(r>>2) + 4*(lane>>5)
-  const int n = n0 + wn * 32 + (lane & 31);
-  if (n >= p.n) return;
-  const float bias = p.bias ? p.bias[n] : 0.f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (m < a.M) epilogue(p, m, n, acc[r] + bias);
-  }
+  tile_epilogue(p, a.M, m0 + wm * 32 + 4 * (lane >> 5), n0 + wn * 32 + (lane & 31), acc);
 }
 
 // Small-N convolution (N <= 4, VEC inputs): one wave per output pixel.
@@ -608,13 +702,15 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
       RAFT_REQUIRE(p.aux0, "raft_conv2d: RESID_RELU needs aux0");
       break;
     case RAFT_EPI_GRU_ZR:
-      RAFT_REQUIRE(p.aux0 && p.out1 && p.split > 0 && p.split < p.n, "raft_conv2d: GRU_ZR needs aux0, out1, split");
+      RAFT_REQUIRE(p.aux0 && p.out1 && p.split > 0 && p.split < p.n && p.split % 32 == 0,
+                   "raft_conv2d: GRU_ZR needs aux0, out1 and split (a multiple of 32)");
       break;
     case RAFT_EPI_GRU_Q:
       RAFT_REQUIRE(p.aux0 && p.aux1, "raft_conv2d: GRU_Q needs aux0 (h) and aux1 (z)");
       break;
     case RAFT_EPI_TANH_RELU:
-      RAFT_REQUIRE(p.out1 && p.split > 0 && p.split < p.n, "raft_conv2d: TANH_RELU needs out1 and split");
+      RAFT_REQUIRE(p.out1 && p.split > 0 && p.split < p.n && p.split % 32 == 0,
+                   "raft_conv2d: TANH_RELU needs out1 and split (a multiple of 32)");
       break;
     case RAFT_EPI_LINEAR:
     case RAFT_EPI_RELU:

@@ -31,15 +31,21 @@ for name, cin, cout, kh, kw, pad in SHAPES:
     out = torch.empty(B * H * W, cout, device=dev)
     prm = K.conv_params(pc, K.Rows(x), B, H, W, K.Rows(out), epilogue=_lib.EPI_RELU)
     L = [K.conv_launch(prm)]
-    s = K.stream_handle()
     for _ in range(3):
-        L[0](s)
+        L[0](K.stream_handle())
+    torch.cuda.synchronize()
+    # capture the repetitions in a hipGraph: the replay has no host launch overhead
+    reps = 50
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        s = K.stream_handle()
+        for _ in range(reps):
+            L[0](s)
+    g.replay()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    reps = 50
     e0.record()
-    for _ in range(reps):
-        L[0](s)
+    g.replay()
     e1.record()
     e1.synchronize()
     us = e0.elapsed_time(e1) / reps * 1e3
