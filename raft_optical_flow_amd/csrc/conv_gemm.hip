@@ -45,8 +45,11 @@ constexpr int BK = 32;
 constexpr int LDSK = BK + 4;
 constexpr int STAGE = (BM + BN) * LDSK;       // floats per LDS buffer
 constexpr int MAX_GATHER_K = 1024;
+#ifndef CONV_SCHED
+#define CONV_SCHED 1                              // sched_group_barrier interleave of a phase
+#endif
 #ifndef GEMM_NS
-#define GEMM_NS 2                                 // staging register sets (K-steps in flight)
+#define GEMM_NS 2                                 // staging register sets (NS-1 K-steps in flight + one refilling)
 #endif            // k_pad limit of GATHER mode (LDS table)
 
 struct ConvArgs {
@@ -208,13 +211,8 @@ __device__ __forceinline__ void tile_epilogue(const raft_conv2d_params& p, int M
 
 // Per-thread staging state: two A rows (output pixels) of the tile.
 struct AWalk {
-  int pb[2], py[2], px[2];
+  int pb[2], py[2], px[2];  // pb: the row's image base pixel (b * in_h * in_w)
   bool pv[2];
-  // VEC mode, current tap: the rows' input-pixel byte offsets in segment 0 / 1
-  // (OFF_INVALID outside the image: the buffer load returns 0).  Named
-  // scalars, not arrays: a runtime-selected array element goes to scratch.
-  unsigned o0s0, o1s0, o0s1, o1s1;
-  int tap;
 };
 
 constexpr unsigned OFF_INVALID = 0x80000000u;  // > num_records of every buffer (host-checked)
@@ -225,28 +223,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, unsig
 
 __device__ __forceinline__ f32x4 buf_load4(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
-}
-
-// VEC: recompute the rows' pixel offsets when the K walk enters a new tap
-// (once per c_pad/32 K-steps; all tap/step bookkeeping is wave-uniform).
-__device__ __forceinline__ void vec_set_tap(const raft_conv2d_params& p, unsigned ld0b, unsigned ld1b, AWalk& w,
-                                            int tap) {
-  const int ky = tap / p.kw, kx = tap - ky * p.kw;
-  {
-    const int iy = w.py[0] + ky, ix = w.px[0] + kx;
-    const bool in = w.pv[0] && (unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w;
-    const unsigned pix = (unsigned)((w.pb[0] * p.in_h + iy) * p.in_w + ix);
-    w.o0s0 = in ? pix * ld0b : OFF_INVALID;
-    w.o0s1 = in ? pix * ld1b : OFF_INVALID;
-  }
-  {
-    const int iy = w.py[1] + ky, ix = w.px[1] + kx;
-    const bool in = w.pv[1] && (unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w;
-    const unsigned pix = (unsigned)((w.pb[1] * p.in_h + iy) * p.in_w + ix);
-    w.o1s0 = in ? pix * ld0b : OFF_INVALID;
-    w.o1s1 = in ? pix * ld1b : OFF_INVALID;
-  }
-  w.tap = tap;
 }
 
 // GATHER mode (small / unaligned inputs): element-wise loads through the
@@ -265,7 +241,7 @@ __device__ __forceinline__ unsigned gather_a(const ConvArgs& a, const AWalk& w, 
       const int ky = code >> 20, kx = (code >> 10) & 1023, c = code & 1023;
       const int iy = w.py[i] + ky, ix = w.px[i] + kx;
       const bool ok = w.pv[i] && code >= 0 && (unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w;
-      const long pix = ((long)w.pb[i] * p.in_h + iy) * p.in_w + ix;
+      const long pix = (long)w.pb[i] + (long)iy * p.in_w + ix;
       const float* src = (c < p.in0_c) ? p.in0 + pix * p.in0_ld + c : p.in1 + pix * p.in1_ld + (c - p.in0_c);
       e[j] = *(ok ? src : p.in0);
       mask |= ok ? 1u << (4 * i + j) : 0u;
@@ -280,9 +256,22 @@ __device__ __forceinline__ unsigned gather_a(const ConvArgs& a, const AWalk& w, 
 // double buffer, so each SIMD carries KG waves of the tile that interleave
 // (one group's MFMAs cover the other's LDS reads, barrier skew and staging).
 // The groups' accumulators are summed through LDS before the epilogue.
+#ifdef STAMPS  // dev-only phase timing (tools/conv_bench.py STAMPS=1 with a -DSTAMPS variant)
+__device__ unsigned long long g_stamp[4 * 16384];
+__device__ __forceinline__ unsigned long long stamp_now() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#endif
+
 template <int MODE, int KG, int PREC, int NS>
-__global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(ConvArgs a) {
-  static_assert(NS % 2 == 0, "NS must be even (LDS buffer parity follows the unrolled phase index)");
+__global__ __launch_bounds__(256 * KG, 4) void conv_gemm_kernel(ConvArgs a) {  // 4 waves per SIMD: <= 128 VGPRs
+  static_assert(NS >= 2, "at least two staging register sets");
+  constexpr int U = NS % 2 ? 2 * NS : NS;  // phase unroll: static LDS-buffer parity and register-set index
+  constexpr int D = NS - 1;                // K-steps in flight ahead of the one being staged
   __shared__ __attribute__((aligned(16))) float
       smem[KG * 2 * STAGE + (MODE == RAFT_CONV_GATHER ? MAX_GATHER_K : 0)];
   const raft_conv2d_params& p = a.p;
@@ -322,11 +311,10 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(ConvArgs a) {
     const int ox = mm % p.out_w;
     const int t = mm / p.out_w;
     const int oy = t % p.out_h;
-    w.pb[i] = t / p.out_h;
+    w.pb[i] = (t / p.out_h) * p.in_h * p.in_w;
     w.py[i] = oy * p.stride_h - p.pad_h;
     w.px[i] = ox * p.stride_w - p.pad_w;
   }
-  w.tap = -1;
   const int nk = a.K / BK;
   // wave-uniform operands, read once from the kernel arguments (readfirstlane'd
   // so the per-step selects stay scalar: no kernarg reloads, no waterfalls)
@@ -346,54 +334,76 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(ConvArgs a) {
   const unsigned wvoff1 = wvoff0 + 32u * (unsigned)a.K * 4u;
   const int cnt = g < nk ? (nk - g + KG - 1) / KG : 0;  // this group's K-steps
   const int nj = (nk + KG - 1) / KG;                     // phases (group 0's count)
-  f32x4 ra[NS][2], rb[NS][2];  // NS staging register sets: K-steps t+1 .. t+NS-1 in flight during phase t
+  f32x4 ra[NS][2], rb[NS][2];  // staging register sets: during phase t, steps t+1 .. t+D in flight, set t%NS refilling
   unsigned am[NS];             // their A validity masks
 
-  // the K walk of issue(): this group's next K-step as (tap, first channel cs)
-  // and weight byte offset, advanced incrementally (issue() runs in step order)
-  int wtap = (g * BK) / cpad, wcs = g * BK - wtap * cpad;
+  // the K walk of issue(): this group's next K-step as (tap (ky, kx), first
+  // channel cs) and weight byte offset, advanced incrementally in SGPRs
+  // (issue() runs in step order); no branches, so a whole phase is one
+  // scheduling region
+  const int kw = __builtin_amdgcn_readfirstlane(p.kw);
+  const unsigned in_h = __builtin_amdgcn_readfirstlane(p.in_h), in_w = __builtin_amdgcn_readfirstlane(p.in_w);
+  int wcs = g * BK, wky = 0, wkx = 0;
+  auto advance_tap = [&]() {
+    const bool wrap = wcs >= cpad;
+    wcs = wrap ? wcs - cpad : wcs;
+    const int kx1 = wkx + (wrap ? 1 : 0);
+    const bool row = kx1 == kw;
+    wkx = row ? 0 : kx1;
+    wky = row ? wky + 1 : wky;
+  };
+  advance_tap();
+  advance_tap();
   unsigned wsoff = (unsigned)g * BK * 4u;
   int kstep = g;
 
-  // issue() is unconditional: steps beyond this group's count load harmless
-  // data (zeros past the buffer ends, never consumed) so every phase has the
-  // same load count and hipcc's counted vmcnt stays exact
+  // issue() is unconditional: steps beyond this group's count load zeros
+  // (offsets past the buffer ends), so every phase has the same load count
+  // (hipcc's counted vmcnt stays exact) and the MFMA phases need no predicate
   auto issue = [&](f32x4(&ra)[2], f32x4(&rb)[2], unsigned& am) {
     if constexpr (MODE == RAFT_CONV_VEC) {
-      if (wtap != w.tap) vec_set_tap(p, ld0b, ld1b, w, wtap);
       const bool s0 = (unsigned)wcs < rfl_in0c;  // uniform: the K-step lies in segment 0
       const unsigned cl = (unsigned)(wcs + lq * 4);
-      const bool lane_ok = s0 ? cl < rfl_in0c : cl - rfl_in0c < rfl_in1c;
+      // channel limit of the K-step's segment (segment 1 starts at in0_c): one compare
+      const unsigned lim = (kstep < nk) ? (s0 ? rfl_in0c : rfl_in0c + rfl_in1c) : 0u;
+      const bool lane_ok = cl < lim;
       const unsigned soff = (unsigned)(s0 ? wcs : wcs - (int)rfl_in0c) * 4u;
       const unsigned blo = s0 ? b0lo : b1lo, bhi = s0 ? b0hi : b1hi, nrec = s0 ? nrec0 : nrec1;
+      const unsigned ldb = s0 ? ld0b : ld1b;
       const __amdgpu_buffer_rsrc_t rs =
           make_rsrc(reinterpret_cast<const void*>(((unsigned long long)bhi << 32) | blo), nrec);
-      const unsigned r0 = s0 ? w.o0s0 : w.o0s1, r1 = s0 ? w.o1s0 : w.o1s1;
-      const unsigned v0 = (lane_ok && r0 != OFF_INVALID) ? r0 + lq * 16u : OFF_INVALID;
-      const unsigned v1 = (lane_ok && r1 != OFF_INVALID) ? r1 + lq * 16u : OFF_INVALID;
+      // row byte offsets for this tap, 24-bit multiplies (pixels < 2^24, host-checked)
+      unsigned voff[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int iy = w.py[i] + wky, ix = w.px[i] + wkx;
+        const bool ok = lane_ok & w.pv[i] & ((unsigned)iy < in_h) & ((unsigned)ix < in_w);
+        const unsigned pix = (unsigned)w.pb[i] + __umul24((unsigned)iy, in_w) + (unsigned)ix;
+        voff[i] = ok ? __umul24(pix, ldb) + lq * 16u : OFF_INVALID;
+      }
 #ifdef ABL_NOLOAD  // timing ablation (dev builds only): no A/B global loads
-      ra[0] = f32x4{(float)v0, 1.f, 2.f, 3.f};
-      ra[1] = f32x4{(float)v1, 1.f, 2.f, (float)soff};
+      ra[0] = f32x4{(float)voff[0], 1.f, 2.f, 3.f};
+      ra[1] = f32x4{(float)voff[1], 1.f, 2.f, (float)soff};
       (void)rs;
 #else
-      ra[0] = buf_load4(rs, v0, soff);
-      ra[1] = buf_load4(rs, v1, soff);
+      ra[0] = buf_load4(rs, voff[0], soff);
+      ra[1] = buf_load4(rs, voff[1], soff);
 #endif
       am = 0xFFu;
       wcs += KG * BK;
-      while (wcs >= cpad) {
-        wcs -= cpad;
-        ++wtap;
-      }
+      advance_tap();
+      advance_tap();
     } else {
-      am = gather_a(a, w, min(kstep, nk - 1), lq, ktab, ra);
+      am = kstep < nk ? gather_a(a, w, kstep, lq, ktab, ra) : 0u;
     }
 #ifdef ABL_NOLOAD
     rb[0] = f32x4{(float)wsoff, 1.f, 2.f, 3.f};
     rb[1] = f32x4{(float)wsoff, 1.f, 2.f, 4.f};
 #else
-    rb[0] = buf_load4(rs_w, wvoff0, wsoff);
-    rb[1] = buf_load4(rs_w, wvoff1, wsoff);
+    // past the last K-step the soffset points beyond the weight buffer: zeros
+    const unsigned ws = kstep < nk ? wsoff : OFF_INVALID;
+    rb[0] = buf_load4(rs_w, wvoff0, ws);
+    rb[1] = buf_load4(rs_w, wvoff1, ws);
 #endif
     wsoff += KG * BK * 4u;
     kstep += KG;
@@ -477,38 +487,96 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(ConvArgs a) {
     }
   };
 
-  // prologue: K-steps 0 .. NS-1 in flight, step 0 staged, its set refilled with step NS
+  // one phase's schedule (LLVM sched groups): the LDS reads of the MFMA operands
+  // first, then each MFMA followed by a share of the next stage's conversion
+  // VALU and one of the global loads of step t+NS, then the LDS writes, so
+  // the MFMA pipe is fed while the split runs and the loads queue at the
+  // texture unit in the MFMA shadow (not all at once after the barrier)
+  auto interleave = [&]() {
+#if CONV_SCHED
+    constexpr int NMF = PREC == RAFT_PREC_FP32 ? 16 : PREC == RAFT_PREC_F16X3 ? 6 : 2;
+    constexpr int NRD = PREC == RAFT_PREC_F16 ? 4 : 8;
+    constexpr int NVA = PREC == RAFT_PREC_FP32 ? 1 : PREC == RAFT_PREC_F16X3 ? 6 : 10;
+    // operand reads in two halves (the second half after a third of the
+    // MFMAs) keep fewer fragment registers live
+    __builtin_amdgcn_sched_group_barrier(0x100, NRD / 2, 0);
+#pragma unroll
+    for (int i = 0; i < NMF; ++i) {
+      if (i == (NMF + 2) / 3) __builtin_amdgcn_sched_group_barrier(0x100, NRD - NRD / 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x2, NVA, 0);
+      if (i < 4) __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);  // the next step's global loads
+    }
+    __builtin_amdgcn_sched_group_barrier(0x200, 4, 0);
+#endif
+  };
+
+#ifdef ABL_EMPTY
+  if (a.M > 0) return;
+#endif
+#ifdef ABL_NOLOOP
+  if (a.M > 0) {
+    tile_epilogue(p, a.M, m0 + wm * 32 + 4 * (lane >> 5), n0 + wn * 32 + (lane & 31), acc);
+    return;
+  }
+#endif
+  // prologue: K-steps 0 .. NS-1 issued into sets 0 .. NS-1, step 0 staged
 #pragma unroll
   for (int u = 0; u < NS; ++u) issue(ra[u], rb[u], am[u]);
   stage(0, ra[0], rb[0], am[0]);
   __syncthreads();
-  issue(ra[0], rb[0], am[0]);
 
-  // phase t: MFMAs on LDS buffer t&1 (step t); stage step t+1 (set (t+1)%NS) into
-  // the other buffer; one barrier; refill the freed set with step t+1+NS.  The
-  // body is unrolled NS times so every register set index is static, and the
-  // main loop is branch-free around the loads (only the MFMAs are predicated,
-  // on a wave-uniform count), so hipcc's counted vmcnt keeps NS-1 K-steps in
-  // flight.  The < NS tail phases issue nothing more.
-  const int nfull = nj - nj % NS;
-  for (int j = 0; j < nfull; j += NS) {
+  // phase t: refill set t%NS (its step t was staged in phase t-1) with step
+  // t+NS; MFMAs on LDS buffer t&1 (step t); stage step t+1 from set (t+1)%NS
+  // into the other buffer; one barrier.  The refill has no dependence on the
+  // rest of the phase, so the sched groups spread its loads between the
+  // MFMAs.  The body is unrolled U times (static set index and buffer parity)
+  // and is branch-free; hipcc's counted vmcnt keeps D steps in flight.  The
+  // < U tail phases issue only the steps still needed.
+  const int nfull = nj - nj % U;
+#ifdef STAMPS
+  unsigned long long st_work = 0, st_bar = 0, st_iss = 0, st0 = stamp_now();
+  const unsigned long long st_begin = st0;
+#endif
+  for (int j = 0; j < nfull; j += U) {
 #pragma unroll
-    for (int u = 0; u < NS; ++u) {
+    for (int u = 0; u < U; ++u) {
+      issue(ra[u % NS], rb[u % NS], am[u % NS]);
 #ifndef ABL_NOCOMPUTE
-      if (j + u < cnt) compute(u & 1);
+      compute(u & 1);
 #endif
       stage((u + 1) & 1, ra[(u + 1) % NS], rb[(u + 1) % NS], am[(u + 1) % NS]);
+      interleave();
+#ifdef STAMPS
+      const unsigned long long st1 = stamp_now();
+      st_work += st1 - st0;
+#endif
 #ifndef ABL_NOBARRIER
       __syncthreads();
 #endif
-      issue(ra[(u + 1) % NS], rb[(u + 1) % NS], am[(u + 1) % NS]);
+#ifdef STAMPS
+      st0 = stamp_now();
+      st_bar += st0 - st1;
+#endif
     }
   }
+#ifdef STAMPS
+  {
+    const unsigned wid = blockIdx.x * (KG * 4) + wave;
+    if (lane == 0 && wid < 16384) {
+      g_stamp[wid * 4 + 0] = st_work;
+      g_stamp[wid * 4 + 1] = st_bar;
+      g_stamp[wid * 4 + 2] = st_iss;
+      g_stamp[wid * 4 + 3] = st0 - st_begin;
+    }
+  }
+#endif
 #pragma unroll
-  for (int u = 0; u < NS - 1; ++u) {
+  for (int u = 0; u < U - 1; ++u) {
     const int t = nfull + u;
     if (t < nj) {
-      if (t < cnt) compute(u & 1);
+      if (t + NS < nj) issue(ra[u % NS], rb[u % NS], am[u % NS]);  // steps still to come
+      compute(u & 1);
       if (t + 1 < nj) {
         stage((u + 1) & 1, ra[(u + 1) % NS], rb[(u + 1) % NS], am[(u + 1) % NS]);
         __syncthreads();
@@ -596,12 +664,12 @@ __global__ __launch_bounds__(256) void conv_smalln_kernel(ConvArgs a) {
 using namespace raft;
 
 namespace {
-template <int MODE, int PREC>
+template <int MODE, int PREC, int NSETS = MODE == RAFT_CONV_VEC ? GEMM_NS : 2>
 void launch_gemm_p(const ConvArgs& a, dim3 grid, bool two, hipStream_t s) {
   if (two)
-    hipLaunchKernelGGL((conv_gemm_kernel<MODE, 2, PREC, GEMM_NS>), grid, dim3(512), 0, s, a);
+    hipLaunchKernelGGL((conv_gemm_kernel<MODE, 2, PREC, NSETS>), grid, dim3(512), 0, s, a);
   else
-    hipLaunchKernelGGL((conv_gemm_kernel<MODE, 1, PREC, GEMM_NS>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv_gemm_kernel<MODE, 1, PREC, NSETS>), grid, dim3(256), 0, s, a);
 }
 template <int MODE>
 void launch_gemm_m(const ConvArgs& a, dim3 grid, bool two, hipStream_t s) {
@@ -629,6 +697,12 @@ __global__ void split_weight_kernel(const float* __restrict__ w, _Float16* __res
   out[blk * 64 + 32 + k] = (_Float16)((x - (float)h) * SPLIT_SCALE);
 }
 }  // namespace
+
+#ifdef STAMPS
+extern "C" int raft_debug_stamps(unsigned long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamp), sizeof(unsigned long long) * (size_t)n);
+}
+#endif
 
 extern "C" int raft_conv2d_split_weight(const float* w, void* out, int n_pad, int k_pad, raft_stream_t stream) {
   RAFT_REQUIRE(w && out && n_pad > 0 && k_pad > 0 && k_pad % BK == 0, "raft_conv2d_split_weight: bad args");
@@ -692,6 +766,8 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
     RAFT_REQUIRE(p.in0_ld % 4 == 0 && (p.in1_c == 0 || p.in1_ld % 4 == 0), "raft_conv2d VEC: ld must be a multiple of 4");
     RAFT_REQUIRE(((uintptr_t)p.in0 & 15) == 0 && ((uintptr_t)p.in1 & 15) == 0,
                  "raft_conv2d VEC: inputs must be 16-byte aligned");
+    RAFT_REQUIRE((long)p.batch * p.in_h * p.in_w < (1L << 24) && p.in0_ld < (1 << 20) && p.in1_ld < (1 << 20),
+                 "raft_conv2d VEC: more than 2^24 input pixels (split the batch)");
   } else {
     RAFT_REQUIRE(k_pad <= MAX_GATHER_K && ctot < 1024 && p.kw < 1024,
                  "raft_conv2d GATHER: kh*kw*cin must be <= %d (got %d)", MAX_GATHER_K, p.kh * p.kw * ctot);

@@ -49,6 +49,17 @@ for name, cin, cout, kh, kw, pad in SHAPES:
     e1.record()
     e1.synchronize()
     us = e0.elapsed_time(e1) / reps * 1e3
+    if __import__("os").environ.get("STAMPS"):
+        import ctypes
+        import numpy as np
+        lib = _lib.load()
+        buf = np.zeros(4 * 16384, dtype=np.uint64)
+        lib.raft_debug_stamps(ctypes.c_void_p(buf.ctypes.data), buf.size)
+        st = buf.reshape(-1, 4).astype(np.float64)
+        st = st[st[:, 3] > 0]
+        mean = st.mean(0)
+        print(f"   stamps over {len(st)} waves (cycles per wave): work {mean[0]:.0f} barrier {mean[1]:.0f} "
+              f"issue {mean[2]:.0f} loop {mean[3]:.0f}; max loop {st[:, 3].max():.0f}")
     fl = 2.0 * B * H * W * cout * cin * kh * kw
     tot_t += us
     print(f"{name:8s} M={B*H*W:6d} N={cout:4d} K={cin*kh*kw:5d}  {us:8.1f} us  {fl/us/1e6:7.1f} TF/s")
