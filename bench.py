@@ -128,6 +128,7 @@ def main():
     ap.add_argument("--alternate-corr", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-fp32-exact", action="store_true", help="skip the exact-f32 comparison run")
     ap.add_argument("--precision", choices=["fp32", "f16x3", "f16"], default=None,
                     help="conv arithmetic (default: the RAFT default, f16x3)")
     args = ap.parse_args()
@@ -229,7 +230,7 @@ def main():
                    "flops_per_iteration": fl}
 
     exact = None
-    if prec != "fp32" and world == 1:
+    if prec != "fp32" and world == 1 and not args.no_fp32_exact:
         model.conv_precision = "fp32"
         plan32 = model.plan(args.batch, H, W, args.iters, test_mode=True, device=dev)
         e32 = timed(plan32, False)

@@ -11,6 +11,6 @@ timeout -k 10 400 python bench.py --steps 20 --warmup 3 ${BENCH_ARGS} > gpurun_o
 cat gpurun_out/bench_$TAG.json
 if [ -n "$PROFILE" ]; then
   export TMPDIR=/tmp
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/prof_$TAG.log 2>&1
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-fp32-exact ${BENCH_ARGS} > gpurun_out/prof_$TAG.log 2>&1
   echo "prof rc=$?"
 fi
