@@ -217,6 +217,9 @@ struct LookupArgs {
   int out_ld, out_layout;
   float* flow;
   int flow_ld;
+  // per level: W-1, H-1 and their reciprocals, rounded on the host exactly as
+  // the device's correctly rounded 1.0f / x would
+  float wm1[LK_MAXL], hm1[LK_MAXL], rw[LK_MAXL], rh[LK_MAXL];
 };
 
 __device__ __forceinline__ void load_coords(const float* c, int layout, int b, int p, int P, float& x, float& y) {
@@ -237,111 +240,192 @@ __device__ __forceinline__ float div_rn(float a, float b, float rcp) {
   return fmaf(r, rcp, q);
 }
 
+// One-axis sampling entry of offset d at level l.  The window's x and y
+// sample positions are separable — tap (ix, iy) samples x-entry ix and
+// y-entry iy — so the reference's per-tap coordinate arithmetic runs on
+// 2(2r+1) entries per level instead of (2r+1)^2 taps.
+//   w: i - patch origin when i and i + 1 lie on the staged patch; OFF_PATCH
+//      when the float round trip moved the floor off it; NAN_POS when the
+//      position is not finite (a 1-px level: W - 1 = 0)
+constexpr int OFF_PATCH = -1000000;
+constexpr int NAN_POS = -2000000;
+constexpr int PSTR = 16 * 16 + 16;  // level stride of the LDS patch: +16 floats staggers the levels' banks
+
+template <int R>
+__device__ __forceinline__ void axis_entry(float c, int d, float m1, float rcp, int& w, float& t, int& i) {
+  constexpr int WD = 2 * R + 2;
+  const int v0 = (int)floorf(c) - R;
+  const int o = (v0 >> 2) * 4;                               // patch origin on this axis
+  const int ext = (((v0 + WD - 1) >> 2) - (v0 >> 2) + 1) * 4;  // patch extent (12 or 16)
+  const float X = c + (float)(d - R);
+  const float g = div_rn(2.0f * X, m1, rcp) - 1.0f;
+  const float u = (g + 1.0f) * (m1 * 0.5f);
+  const bool fin = isfinite(u);
+  const float f0 = fin ? floorf(u) : 0.f;
+  t = u - f0;
+  i = (int)f0;
+  const int ww = i - o;
+  w = !fin ? NAN_POS : (ww >= 0 && ww + 1 < ext) ? ww : OFF_PATCH;
+}
+
 template <int R, int LMAX>
 __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
   constexpr int RD = 2 * R + 1;
   constexpr int WD = 2 * R + 2;  // integer window (<= 10 -> <= 4 tiles per axis)
   static_assert(WD <= 13, "window must fit 4 tiles");
-  __shared__ __attribute__((aligned(16))) float patch[4][LMAX][16 * 16];
+  static_assert(LMAX * RD <= 64, "one lane per (level, x offset)");
+  __shared__ __attribute__((aligned(16))) float patch[4][LMAX * PSTR];
+  __shared__ __attribute__((aligned(8))) int2 ytab[4][LMAX * RD];  // (w, t bits) of the y-entries
+  __shared__ int yint[4][LMAX * RD];                               // their floors (off-patch path)
   const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int P = a.H * a.W;
-  const long gp = (long)blockIdx.x * 4 + wv;  // global pixel index b*P + p
-  const bool valid = gp < (long)a.B * P;
-  const int b = valid ? (int)(gp / P) : 0;
-  const int p = valid ? (int)(gp - (long)b * P) : 0;
+  // global pixel index b*P + p: wave-uniform, so the index math stays scalar (B*P < 2^31, host-checked)
+  const int gp = (int)blockIdx.x * 4 + wv;
+  const bool valid = gp < a.B * P;
+  const int gpc = valid ? gp : 0;
+  const int b = gpc / P;
+  const int p = gpc - b * P;
   float x = 0.f, y = 0.f;
-  if (valid) load_coords(a.coords, a.coords_layout, b, p, P, x, y);
+  load_coords(a.coords, a.coords_layout, b, p, P, x, y);
 
-  // lane -> (tile row ti, tile col tj, row-in-tile rr) of the 4x4-tile patch
+  // phase 1: per level, the <= 4x4 tiles covering the (2r+2)^2 integer window,
+  // one 16-B load per lane (lane = tile row ti, tile col tj, row-in-tile rr),
+  // all levels in flight together; the pixel's map base is wave-uniform
   const int ti = lane >> 4, tj = (lane >> 2) & 3, rr = lane & 3;
   f32x4 v[LMAX];
   bool ok[LMAX];
-  int tyo[LMAX], txo[LMAX];
 #pragma unroll
   for (int l = 0; l < LMAX; ++l) {
     const float s = 1.0f / (float)(1 << l);  // coords / 2**l (exact power-of-two scaling)
     const int x0 = (int)floorf(x * s) - R, y0 = (int)floorf(y * s) - R;
-    tyo[l] = y0 >> 2;  // arithmetic shift = floor division by 4 (negative too)
-    txo[l] = x0 >> 2;
-    const int nty = ((y0 + WD - 1) >> 2) - tyo[l] + 1;  // tiles the window needs (3 or 4)
-    const int ntx = ((x0 + WD - 1) >> 2) - txo[l] + 1;
-    const int ty = tyo[l] + ti, tx = txo[l] + tj;
+    const int tyo = y0 >> 2, txo = x0 >> 2;  // arithmetic shift = floor division by 4 (negative too)
+    const int nty = ((y0 + WD - 1) >> 2) - tyo + 1;  // tiles the window needs (3 or 4)
+    const int ntx = ((x0 + WD - 1) >> 2) - txo + 1;
+    const int ty = tyo + ti, tx = txo + tj;
     const Level& lv = a.lv[l];
-    // unconditional load from a clamped address: all levels' loads in flight at once
     ok[l] = l < a.L && valid && ti < nty && tj < ntx && (unsigned)ty < (unsigned)lv.th && (unsigned)tx < (unsigned)lv.tw;
-    const float* src = a.pyr + lv.off + gp * lv.mapsz + ((long)ty * lv.tw + tx) * 16 + rr * 4;
-    v[l] = *reinterpret_cast<const f32x4*>(ok[l] ? src : a.pyr);
+    const float* mapb = a.pyr + lv.off + (long)gpc * lv.mapsz;
+    const int off = ok[l] ? (ty * lv.tw + tx) * 16 + rr * 4 : 0;  // unconditional load, zeroed below
+#ifdef LK_ABL_NOLOAD  // timing ablation (dev builds only): no tile loads
+    v[l] = f32x4{(float)off, (float)(long)mapb, 0.f, 0.f};
+#else
+    v[l] = *reinterpret_cast<const f32x4*>(mapb + off);
+#endif
+  }
+
+  // phase 2 (while the loads fly): lane (l, d) = (lane / RD, lane % RD)
+  // evaluates x-entry d (kept: this lane's column in phase 3) and y-entry d
+  // (shared through LDS) of level l, with the reference's arithmetic — offset
+  // added to the centroid, bilinear_sampler's 2x/(W-1)-1, grid_sample's
+  // (g+1)*((W-1)/2) — so corner indices and weights are the reference's
+  const int nlane = a.L * RD;
+  const bool col = lane < nlane;
+  const int l = col ? lane / RD : 0;
+  const int ix = lane - l * RD;
+  int xw = NAN_POS, xi = 0;
+  float xt = 0.f;
+  {
+    float wm1 = a.wm1[0], hm1 = a.hm1[0], rw = a.rw[0], rh = a.rh[0], s = 1.0f;
+#pragma unroll
+    for (int k = 1; k < LMAX; ++k) {
+      const bool sel = l == k;
+      wm1 = sel ? a.wm1[k] : wm1;
+      hm1 = sel ? a.hm1[k] : hm1;
+      rw = sel ? a.rw[k] : rw;
+      rh = sel ? a.rh[k] : rh;
+      s = sel ? 1.0f / (float)(1 << k) : s;
+    }
+    axis_entry<R>(x * s, ix, wm1, rw, xw, xt, xi);
+    int yw, yi;
+    float yt;
+    axis_entry<R>(y * s, ix, hm1, rh, yw, yt, yi);
+    if (col) {
+      ytab[wv][lane] = int2{yw, __float_as_int(yt)};
+      yint[wv][lane] = yi;
+    }
   }
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int l = 0; l < LMAX; ++l)
-    *reinterpret_cast<f32x4*>(&patch[wv][l][(ti * 4 + rr) * 16 + tj * 4]) = ok[l] ? v[l] : zero;
+  for (int k = 0; k < LMAX; ++k)
+    *reinterpret_cast<f32x4*>(&patch[wv][k * PSTR + (ti * 4 + rr) * 16 + tj * 4]) = ok[k] ? v[k] : zero;
   __syncthreads();
   if (!valid) return;
 
-  // levels unrolled so each level's geometry is a compile-time-indexed kernel
-  // argument (scalar loads), hoisted out of the per-tap work
+  // phase 3: lane (l, ix) walks its column iy = 0 .. 2r of output channels
+  // l*RD^2 + ix*RD + iy; the y-entries are LDS broadcasts, the patch reads of
+  // one level hit consecutive banks (levels staggered by PSTR)
   const int ntap = a.L * RD * RD;
+  const int cbase = l * RD * RD + ix * RD;
+  float val[RD];
+  if (col) {
+    const float* pl = &patch[wv][l * PSTR];
+    const float ex = 1.0f - xt;
+    unsigned deferred = 0;
 #pragma unroll
-  for (int l = 0; l < LMAX; ++l) {
-    if (l >= a.L) break;
-    const Level lv = a.lv[l];
-    const float s = 1.0f / (float)(1 << l);
-    const float cx = x * s, cy = y * s;
-    // patch origin and extent of the tiles phase 1 loaded for this level
-    const int x0 = (int)floorf(cx) - R, y0 = (int)floorf(cy) - R;
-    const int px0 = (x0 >> 2) * 4, py0 = (y0 >> 2) * 4;
-    const int pw = (((x0 + WD - 1) >> 2) - (x0 >> 2) + 1) * 4, ph = (((y0 + WD - 1) >> 2) - (y0 >> 2) + 1) * 4;
-    const float wm1 = (float)(lv.w - 1), hm1 = (float)(lv.h - 1);
-    const float rw = 1.0f / wm1, rh = 1.0f / hm1;
-    for (int tt = lane; tt < RD * RD; tt += 64) {
-      const int ix = tt / RD, iy = tt - ix * RD;
-      const float X = cx + (float)(ix - R);
-      const float Y = cy + (float)(iy - R);
-      const float gx = div_rn(2.0f * X, wm1, rw) - 1.0f;
-      const float gy = div_rn(2.0f * Y, hm1, rh) - 1.0f;
-      const float ux = (gx + 1.0f) * (wm1 * 0.5f);
-      const float uy = (gy + 1.0f) * (hm1 * 0.5f);
-      float val;
-      if (!(isfinite(ux) && isfinite(uy))) {
-        val = __builtin_nanf("");
-      } else {
-        const float fx0 = floorf(ux), fy0 = floorf(uy);
-        const float tx = ux - fx0, ty = uy - fy0;
-        const int xi = (int)fx0, yi = (int)fy0;
-        const int wx = xi - px0, wy = yi - py0;
-        float vnw, vne, vsw, vse;
-        if (wx >= 0 && wx + 1 < pw && wy >= 0 && wy + 1 < ph) {
-          const float* w = &patch[wv][l][wy * 16 + wx];
-          vnw = w[0];
-          vne = w[1];
-          vsw = w[16];
-          vse = w[17];
-        } else {  // the float round trip moved this tap's floor off the staged patch
-          const float* m = a.pyr + lv.off + gp * lv.mapsz;
-          auto at = [&](int yy, int xx) {
-            return ((unsigned)yy < (unsigned)lv.h && (unsigned)xx < (unsigned)lv.w) ? m[tiled_index(yy, xx, lv.tw)]
-                                                                                    : 0.f;
-          };
-          vnw = at(yi, xi);
-          vne = at(yi, xi + 1);
-          vsw = at(yi + 1, xi);
-          vse = at(yi + 1, xi + 1);
-        }
-        const float e = 1.0f - tx, sS = 1.0f - ty;
-        val = vnw * (sS * e) + vne * (sS * tx) + vsw * (ty * e) + vse * (ty * tx);
-      }
-      const int t = l * RD * RD + tt;
-      if (a.out_layout == 0)
-        a.out[gp * a.out_ld + t] = val;
-      else
-        a.out[((long)b * ntap + t) * P + p] = val;
+    for (int iy = 0; iy < RD; ++iy) {
+      const int2 ye = ytab[wv][l * RD + iy];
+      const int yw = ye.x;
+      const float ty = __int_as_float(ye.y);
+      const bool on = (xw | yw) >= 0;
+      const bool nan = xw == NAN_POS || yw == NAN_POS;
+      const float* w = pl + (on ? yw * 16 + xw : 0);
+      const float sS = 1.0f - ty;
+      const float v = w[0] * (sS * ex) + w[1] * (sS * xt) + w[16] * (ty * ex) + w[17] * (ty * xt);
+      val[iy] = nan ? __builtin_nanf("") : v;
+      deferred |= (!on && !nan) ? 1u << iy : 0u;
     }
+    if (__builtin_expect(deferred != 0, 0)) {
+      // taps whose floor the float round trip moved off the staged patch: the
+      // four corners from global memory (zeros outside the map)
+      const Level& lv = a.lv[l];
+      const float* m = a.pyr + lv.off + (long)gp * lv.mapsz;
+      auto at = [&](int yy, int xx) {
+        return ((unsigned)yy < (unsigned)lv.h && (unsigned)xx < (unsigned)lv.w) ? m[tiled_index(yy, xx, lv.tw)] : 0.f;
+      };
+#pragma unroll
+      for (int iy = 0; iy < RD; ++iy) {
+        if (!((deferred >> iy) & 1u)) continue;
+        const int yi = yint[wv][l * RD + iy];
+        const float ty = __int_as_float(ytab[wv][l * RD + iy].y);
+        const float sS = 1.0f - ty;
+        val[iy] = at(yi, xi) * (sS * ex) + at(yi, xi + 1) * (sS * xt) + at(yi + 1, xi) * (ty * ex) +
+                  at(yi + 1, xi + 1) * (ty * xt);
+      }
+    }
+  }
+#ifdef LK_ABL_NOSTORE  // timing ablation (dev builds only): no output stores
+  if (val[0] != -12345.f) return;
+#endif
+  const bool vec_out = a.out_layout == 0 && (a.out_ld & 3) == 0 && (ntap & 3) == 0 && ((uintptr_t)a.out & 15) == 0;
+  if (vec_out) {
+    // NHWC row: transpose the columns through this wave's (consumed) patch
+    // and write the row with 16-B stores (a one-dword-per-lane strided store
+    // tail costs more than the gather itself)
+    float* st = &patch[wv][0];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (col) {
+#pragma unroll
+      for (int iy = 0; iy < RD; ++iy) st[cbase + iy] = val[iy];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float* orow = a.out + (long)gp * a.out_ld;
+    for (int j = 4 * lane; j < ntap; j += 256)
+      *reinterpret_cast<f32x4*>(orow + j) = *reinterpret_cast<const f32x4*>(st + j);
+  } else if (col) {
+    float* orow = a.out_layout == 0 ? a.out + (long)gp * a.out_ld + cbase
+                                    : a.out + ((long)b * ntap + cbase) * P + p;
+    const long ostep = a.out_layout == 0 ? 1 : P;
+#pragma unroll
+    for (int iy = 0; iy < RD; ++iy) orow[iy * ostep] = val[iy];
   }
   if (a.flow && lane < 2) {
     const float g = lane == 0 ? (float)(p % a.W) : (float)(p / a.W);
-    a.flow[gp * a.flow_ld + lane] = (lane == 0 ? x : y) - g;
+    a.flow[(long)gp * a.flow_ld + lane] = (lane == 0 ? x : y) - g;
   }
 }
 
@@ -448,9 +532,17 @@ extern "C" int raft_corr_lookup(const float* pyramid, int B, int H, int W, int L
   RAFT_REQUIRE(out_layout == 1 || out_ld >= L * rd * rd, "raft_corr_lookup: out_ld < L*(2r+1)^2");
   RAFT_REQUIRE(!flow_out || flow_ld >= 2, "raft_corr_lookup: flow_ld < 2");
   RAFT_REQUIRE(((uintptr_t)pyramid & 15) == 0, "raft_corr_lookup: pyramid must be 16-byte aligned");
+  RAFT_REQUIRE((long)B * H * W < (1L << 30), "raft_corr_lookup: more than 2^30 query pixels (split the batch)");
   LookupArgs a;
   RAFT_REQUIRE(pyramid_levels(B, H, W, L, a.lv), "raft_corr_lookup: a pyramid level is empty");
   for (int l = L; l < LK_MAXL; ++l) a.lv[l] = a.lv[L - 1];
+  for (int l = 0; l < LK_MAXL; ++l) {
+    a.wm1[l] = (float)(a.lv[l].w - 1);
+    a.hm1[l] = (float)(a.lv[l].h - 1);
+    volatile float one = 1.0f;  // host IEEE division, as the reference's 1 / (W - 1) path on the device
+    a.rw[l] = one / a.wm1[l];
+    a.rh[l] = one / a.hm1[l];
+  }
   a.pyr = pyramid;
   a.B = B;
   a.H = H;

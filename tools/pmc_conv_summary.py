@@ -1,4 +1,5 @@
-"""Median per-dispatch PMC values of the conv GEMM kernel from tools/pmc_conv.sh passes."""
+"""Median per-dispatch PMC values of one kernel (default: the conv GEMM) from tools/pmc_conv.sh or
+tools/pmc_sq.sh passes:  pmc_conv_summary.py <dir> [kernel-substring]"""
 import csv
 import glob
 import os
@@ -6,10 +7,11 @@ import statistics
 import sys
 
 base = sys.argv[1]
+ksub = sys.argv[2] if len(sys.argv) > 2 else "conv_gemm"
 vals = {}
 for f in sorted(glob.glob(os.path.join(base, "p*", "run_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
-        if "conv_gemm" not in r["Kernel_Name"]:
+        if ksub not in r["Kernel_Name"]:
             continue
         vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
 med = {k: statistics.median(v) for k, v in vals.items()}

@@ -1,0 +1,17 @@
+#!/bin/bash
+# SQ issue/stall PMC passes (one counter group per pass, kernel-trace only) on any
+# kernel of a command:  tools/pmc_sq.sh <tag> <kernel-substring> <command...>
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+TAG=$1; KSUB=$2; shift 2
+OUT=gpurun_out/pmcsq_$TAG
+mkdir -p $OUT
+i=0
+for C in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE SQ_WAVES" \
+         "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU" \
+         "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES"; do
+  i=$((i+1))
+  timeout -k 10 120 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/p$i -o run -- "$@" > $OUT/p$i.log 2>&1 || { echo "pmc pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
+done
+python tools/pmc_conv_summary.py $OUT "$KSUB"
