@@ -249,7 +249,6 @@ __device__ __forceinline__ float div_rn(float a, float b, float rcp) {
 //      position is not finite (a 1-px level: W - 1 = 0)
 constexpr int OFF_PATCH = -1000000;
 constexpr int NAN_POS = -2000000;
-constexpr int PSTR = 16 * 16 + 16;  // level stride of the LDS patch: +16 floats staggers the levels' banks
 
 template <int R>
 __device__ __forceinline__ void axis_entry(float c, int d, float m1, float rcp, int& w, float& t, int& i) {
@@ -268,19 +267,31 @@ __device__ __forceinline__ void axis_entry(float c, int d, float m1, float rcp, 
   w = !fin ? NAN_POS : (ww >= 0 && ww + 1 < ext) ? ww : OFF_PATCH;
 }
 
+// LDS patch of one wave: element (row r, column c) of level l at
+// ((r*4 + c/4)*LMAX + l)*4 + c%4 — levels interleaved at 16-B granularity, so
+// a tile row of one level is one ds_write_b128, and with LMAX = 4 the bank of
+// (r, c, l) is 16(c/4) + 4l + c%4: one bank per (column, level) whatever the
+// rows, so phase 3 (every level's lanes reading its own row) is conflict-free
+template <int LMAX>
+__device__ __forceinline__ int pidx(int r, int c, int l) {
+  return ((r * 4 + (c >> 2)) * LMAX + l) * 4 + (c & 3);
+}
+
 template <int R, int LMAX>
 __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
+#pragma clang fp contract(off)  // the reference's bilinear is separate multiplies and adds
   constexpr int RD = 2 * R + 1;
   constexpr int WD = 2 * R + 2;  // integer window (<= 10 -> <= 4 tiles per axis)
+  constexpr int RS = 16 * LMAX;  // patch row stride (floats)
   static_assert(WD <= 13, "window must fit 4 tiles");
   static_assert(LMAX * RD <= 64, "one lane per (level, x offset)");
-  __shared__ __attribute__((aligned(16))) float patch[4][LMAX * PSTR];
-  __shared__ __attribute__((aligned(8))) int2 ytab[4][LMAX * RD];  // (w, t bits) of the y-entries
-  __shared__ int yint[4][LMAX * RD];                               // their floors (off-patch path)
+  static_assert(RS + 16 <= 255, "ds_read2 offsets");
+  __shared__ __attribute__((aligned(16))) float patch[4][16 * RS];
+  __shared__ __attribute__((aligned(16))) int4 ytab[4][LMAX * RD];  // y-entries: (w, t, 1 - t, floor)
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int P = a.H * a.W;
-  // global pixel index b*P + p: wave-uniform, so the index math stays scalar (B*P < 2^31, host-checked)
+  // global pixel index b*P + p: wave-uniform, so the index math stays scalar (B*P < 2^30, host-checked)
   const int gp = (int)blockIdx.x * 4 + wv;
   const bool valid = gp < a.B * P;
   const int gpc = valid ? gp : 0;
@@ -291,20 +302,23 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
 
   // phase 1: per level, the <= 4x4 tiles covering the (2r+2)^2 integer window,
   // one 16-B load per lane (lane = tile row ti, tile col tj, row-in-tile rr),
-  // all levels in flight together; the pixel's map base is wave-uniform
+  // all levels in flight together.  The window geometry is wave-uniform
+  // (scalar); the pixel's map base too.
   const int ti = lane >> 4, tj = (lane >> 2) & 3, rr = lane & 3;
   f32x4 v[LMAX];
   bool ok[LMAX];
 #pragma unroll
   for (int l = 0; l < LMAX; ++l) {
     const float s = 1.0f / (float)(1 << l);  // coords / 2**l (exact power-of-two scaling)
-    const int x0 = (int)floorf(x * s) - R, y0 = (int)floorf(y * s) - R;
+    const int x0 = __builtin_amdgcn_readfirstlane((int)floorf(x * s)) - R;
+    const int y0 = __builtin_amdgcn_readfirstlane((int)floorf(y * s)) - R;
     const int tyo = y0 >> 2, txo = x0 >> 2;  // arithmetic shift = floor division by 4 (negative too)
     const int nty = ((y0 + WD - 1) >> 2) - tyo + 1;  // tiles the window needs (3 or 4)
     const int ntx = ((x0 + WD - 1) >> 2) - txo + 1;
     const int ty = tyo + ti, tx = txo + tj;
     const Level& lv = a.lv[l];
-    ok[l] = l < a.L && valid && ti < nty && tj < ntx && (unsigned)ty < (unsigned)lv.th && (unsigned)tx < (unsigned)lv.tw;
+    ok[l] = (l < a.L) & valid & (ti < nty) & (tj < ntx) & ((unsigned)ty < (unsigned)lv.th) &
+            ((unsigned)tx < (unsigned)lv.tw);
     const float* mapb = a.pyr + lv.off + (long)gpc * lv.mapsz;
     const int off = ok[l] ? (ty * lv.tw + tx) * 16 + rr * 4 : 0;  // unconditional load, zeroed below
 #ifdef LK_ABL_NOLOAD  // timing ablation (dev builds only): no tile loads
@@ -323,8 +337,8 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
   const bool col = lane < nlane;
   const int l = col ? lane / RD : 0;
   const int ix = lane - l * RD;
-  int xw = NAN_POS, xi = 0;
-  float xt = 0.f;
+  int xw, xi, yw;
+  float xt;
   {
     float wm1 = a.wm1[0], hm1 = a.hm1[0], rw = a.rw[0], rh = a.rh[0], s = 1.0f;
 #pragma unroll
@@ -337,45 +351,54 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
       s = sel ? 1.0f / (float)(1 << k) : s;
     }
     axis_entry<R>(x * s, ix, wm1, rw, xw, xt, xi);
-    int yw, yi;
+    int yi;
     float yt;
     axis_entry<R>(y * s, ix, hm1, rh, yw, yt, yi);
-    if (col) {
-      ytab[wv][lane] = int2{yw, __float_as_int(yt)};
-      yint[wv][lane] = yi;
-    }
+    if (col) ytab[wv][lane] = int4{yw, __float_as_int(yt), __float_as_int(1.0f - yt), yi};
   }
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int k = 0; k < LMAX; ++k)
-    *reinterpret_cast<f32x4*>(&patch[wv][k * PSTR + (ti * 4 + rr) * 16 + tj * 4]) = ok[k] ? v[k] : zero;
+    *reinterpret_cast<f32x4*>(&patch[wv][pidx<LMAX>(ti * 4 + rr, tj * 4, k)]) = ok[k] ? v[k] : zero;
   __syncthreads();
   if (!valid) return;
 
   // phase 3: lane (l, ix) walks its column iy = 0 .. 2r of output channels
-  // l*RD^2 + ix*RD + iy; the y-entries are LDS broadcasts, the patch reads of
-  // one level hit consecutive banks (levels staggered by PSTR)
+  // l*RD^2 + ix*RD + iy; the y-entries are LDS broadcasts
   const int ntap = a.L * RD * RD;
   const int cbase = l * RD * RD + ix * RD;
+  const float ex = 1.0f - xt;
   float val[RD];
-  if (col) {
-    const float* pl = &patch[wv][l * PSTR];
-    const float ex = 1.0f - xt;
+  // the common case: every entry of the wave is finite and on the patch
+  if (__all(!col || (xw >= 0 && yw >= 0))) {
+    if (col) {
+      const float* p0 = &patch[wv][pidx<LMAX>(0, xw, l)];
+      const float* p1 = &patch[wv][pidx<LMAX>(0, xw + 1, l)];
+#pragma unroll
+      for (int iy = 0; iy < RD; ++iy) {
+        const int4 ye = ytab[wv][l * RD + iy];
+        const int ro = ye.x * RS;
+        const float ty = __int_as_float(ye.y), sS = __int_as_float(ye.z);
+        val[iy] = p0[ro] * (sS * ex) + p1[ro] * (sS * xt) + p0[ro + RS] * (ty * ex) + p1[ro + RS] * (ty * xt);
+      }
+    }
+  } else if (col) {
     unsigned deferred = 0;
 #pragma unroll
     for (int iy = 0; iy < RD; ++iy) {
-      const int2 ye = ytab[wv][l * RD + iy];
-      const int yw = ye.x;
-      const float ty = __int_as_float(ye.y);
-      const bool on = (xw | yw) >= 0;
-      const bool nan = xw == NAN_POS || yw == NAN_POS;
-      const float* w = pl + (on ? yw * 16 + xw : 0);
-      const float sS = 1.0f - ty;
-      const float v = w[0] * (sS * ex) + w[1] * (sS * xt) + w[16] * (ty * ex) + w[17] * (ty * xt);
+      const int4 ye = ytab[wv][l * RD + iy];
+      const int yw2 = ye.x;
+      const float ty = __int_as_float(ye.y), sS = __int_as_float(ye.z);
+      const bool on = (xw | yw2) >= 0;
+      const bool nan = xw == NAN_POS || yw2 == NAN_POS;
+      const int r0 = on ? yw2 : 0, c0 = on ? xw : 0;
+      const float* pl = &patch[wv][0];
+      const float v = pl[pidx<LMAX>(r0, c0, l)] * (sS * ex) + pl[pidx<LMAX>(r0, c0 + 1, l)] * (sS * xt) +
+                      pl[pidx<LMAX>(r0 + 1, c0, l)] * (ty * ex) + pl[pidx<LMAX>(r0 + 1, c0 + 1, l)] * (ty * xt);
       val[iy] = nan ? __builtin_nanf("") : v;
       deferred |= (!on && !nan) ? 1u << iy : 0u;
     }
-    if (__builtin_expect(deferred != 0, 0)) {
+    if (deferred != 0) {
       // taps whose floor the float round trip moved off the staged patch: the
       // four corners from global memory (zeros outside the map)
       const Level& lv = a.lv[l];
@@ -386,9 +409,9 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
 #pragma unroll
       for (int iy = 0; iy < RD; ++iy) {
         if (!((deferred >> iy) & 1u)) continue;
-        const int yi = yint[wv][l * RD + iy];
-        const float ty = __int_as_float(ytab[wv][l * RD + iy].y);
-        const float sS = 1.0f - ty;
+        const int4 ye = ytab[wv][l * RD + iy];
+        const int yi = ye.w;
+        const float ty = __int_as_float(ye.y), sS = __int_as_float(ye.z);
         val[iy] = at(yi, xi) * (sS * ex) + at(yi, xi + 1) * (sS * xt) + at(yi + 1, xi) * (ty * ex) +
                   at(yi + 1, xi + 1) * (ty * xt);
       }
