@@ -1,0 +1,181 @@
+// Shared pieces of the conv GEMM kernels (conv_gemm.hip, conv_halo.hip):
+// operand types, the fp32 split, buffer descriptors and the fused epilogues.
+#pragma once
+
+#include "common.hpp"
+
+namespace raft {
+namespace {
+
+using h4 = __attribute__((ext_vector_type(4))) _Float16;
+using h8 = __attribute__((ext_vector_type(8))) _Float16;
+
+constexpr float SPLIT_SCALE = 2048.f;  // lo is stored scaled by 2^11 (kept out of f16 subnormals)
+
+// x = hi + lo / 2048 to ~22 bits: hi = f16(x); x - hi is exact in fp32, its
+// 2^11-scaled value rounds to f16 lo.
+__device__ __forceinline__ void split4(const f32x4 x, h4& hi, h4& lo) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const _Float16 h = (_Float16)x[e];
+    hi[e] = h;
+    lo[e] = (_Float16)((x[e] - (float)h) * SPLIT_SCALE);
+  }
+}
+
+__device__ __forceinline__ float sigmoidf_(float v) { return 1.0f / (1.0f + expf(-v)); }
+
+__device__ __forceinline__ void epilogue(const raft_conv2d_params& p, long m, int n, float v) {
+  if (p.add0) v += p.add0[m * p.add0_ld + n];
+  float* o = p.out + m * p.out_ld + n;
+  switch (p.epilogue) {
+    case RAFT_EPI_LINEAR:
+      *o = p.alpha * v;
+      break;
+    case RAFT_EPI_RELU:
+      *o = fmaxf(v, 0.f);
+      break;
+    case RAFT_EPI_RESID_RELU:
+      *o = fmaxf(p.aux0[m * p.aux0_ld + n] + fmaxf(v, 0.f), 0.f);
+      break;
+    case RAFT_EPI_GRU_ZR:
+      if (n < p.split) {
+        *o = sigmoidf_(v);
+      } else {
+        const int c = n - p.split;
+        p.out1[m * p.out1_ld + c] = sigmoidf_(v) * p.aux0[m * p.aux0_ld + c];
+      }
+      break;
+    case RAFT_EPI_GRU_Q: {
+      const float q = tanhf(v);
+      const float z = p.aux1[m * p.aux1_ld + n];
+      const float h = p.aux0[m * p.aux0_ld + n];
+      *o = (1.0f - z) * h + z * q;
+      break;
+    }
+    case RAFT_EPI_TANH_RELU:
+      if (n < p.split)
+        *o = tanhf(v);
+      else
+        p.out1[m * p.out1_ld + (n - p.split)] = fmaxf(v, 0.f);
+      break;
+    case RAFT_EPI_ADD_TO_OUT:
+      *o = *o + v;
+      break;
+    default:
+      break;
+  }
+}
+
+// Epilogue of one 32x32 MFMA tile: lane owns column n and the 16 rows
+// mb + (r&3) + 8*(r>>2).  All operand loads of the 16 rows (add0, aux0/aux1,
+// the ADD_TO_OUT destination) are issued together from clamped addresses
+// before any store, and only the stores are predicated: on gfx9 stores share
+// vmcnt with loads, so a row-by-row load/store interleave would wait for every
+// earlier store to complete (one full write latency per row).
+__device__ __forceinline__ long row_of(int mb, int r) { return mb + (r & 3) + 8 * (r >> 2); }
+
+// rows[r] = the output pixel (GEMM row) of accumulator register r, or -1 past
+// the edge (its loads read row 0, its store is dropped).  Element indices are
+// 32-bit (rows * ld < 2^30, host-checked), so each address is one VGPR offset
+// from the scalar base.
+__device__ __forceinline__ unsigned eidx(int row, int ld, int col) {
+  return (unsigned)(row < 0 ? 0 : row) * (unsigned)ld + (unsigned)col;
+}
+__device__ __forceinline__ void load_rows(const float* base, int ld, const int (&rows)[16], int col, float (&t)[16]) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) t[r] = base[eidx(rows[r], ld, col)];
+}
+
+// branch-free activations (no per-row control flow between the stores)
+__device__ __forceinline__ float sigmoid_bf(float x) { return __frcp_rn(1.0f + __expf(-x)); }
+__device__ __forceinline__ float tanh_bf(float x) { return 1.0f - 2.0f * __frcp_rn(__expf(2.0f * x) + 1.0f); }
+
+__device__ __forceinline__ void tile_epilogue(const raft_conv2d_params& p, const int (&rows)[16], int n,
+                                              const f32x16& acc) {
+  const bool ncol = n < p.n;
+  const int nc = ncol ? n : p.n - 1;  // clamped column for loads
+  float v[16];
+  const float bias = p.bias ? p.bias[nc] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = acc[r] + bias;
+  if (p.add0) {
+    float t[16];
+    load_rows(p.add0, p.add0_ld, rows, nc, t);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] += t[r];
+  }
+  // 1) operand loads, 2) values, 3) stores: destination dst[row * ld + col]
+  float* dst = p.out;
+  int ld = p.out_ld, col = n;
+  const int epi = p.epilogue;
+  if (epi == RAFT_EPI_LINEAR) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] *= p.alpha;
+  } else if (epi == RAFT_EPI_RELU) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = fmaxf(v[r], 0.f);
+  } else if (epi == RAFT_EPI_RESID_RELU) {
+    float t[16];
+    load_rows(p.aux0, p.aux0_ld, rows, nc, t);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = fmaxf(t[r] + fmaxf(v[r], 0.f), 0.f);
+  } else if (epi == RAFT_EPI_GRU_ZR) {
+    if (nc < p.split) {  // a wave's 32 columns lie on one side of split (split % 32 == 0, host-checked)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = sigmoid_bf(v[r]);
+    } else {
+      col = nc - p.split;
+      float t[16];
+      load_rows(p.aux0, p.aux0_ld, rows, col, t);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = sigmoid_bf(v[r]) * t[r];
+      dst = p.out1;
+      ld = p.out1_ld;
+    }
+  } else if (epi == RAFT_EPI_GRU_Q) {
+    float h[16], z[16];
+    load_rows(p.aux0, p.aux0_ld, rows, nc, h);
+    load_rows(p.aux1, p.aux1_ld, rows, nc, z);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = (1.0f - z[r]) * h[r] + z[r] * tanh_bf(v[r]);
+  } else if (epi == RAFT_EPI_TANH_RELU) {
+    if (nc < p.split) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = tanh_bf(v[r]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = fmaxf(v[r], 0.f);
+      dst = p.out1;
+      ld = p.out1_ld;
+      col = n - p.split;
+    }
+  } else if (epi == RAFT_EPI_ADD_TO_OUT) {
+    float t[16];
+    load_rows(p.out, p.out_ld, rows, nc, t);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] += t[r];
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    if (ncol && rows[r] >= 0) dst[eidx(rows[r], ld, col)] = v[r];
+}
+
+constexpr unsigned OFF_INVALID = 0x80000000u;  // > num_records of every buffer (host-checked)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ f32x4 buf_load4(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+
+}  // namespace
+
+// conv_halo.hip: the halo-tiled LDS-DMA kernel for stride-1 "same" convs;
+// returns 1 (nothing launched) when the conv is not one it covers
+int conv_halo_launch(const raft_conv2d_params& p, int k_pad, int n_pad, unsigned w_bytes, unsigned in0_bytes,
+                     unsigned in1_bytes, hipStream_t s);
+
+}  // namespace raft

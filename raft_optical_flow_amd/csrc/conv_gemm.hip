@@ -34,7 +34,7 @@
 //
 // N <= 4 outputs (the flow head's 256 -> 2 conv) use conv_smalln_kernel: one
 // wave per output pixel, channels across lanes, wave reduction per output.
-#include "common.hpp"
+#include "conv_common.hpp"
 
 namespace raft {
 namespace {
@@ -63,167 +63,11 @@ struct ConvArgs {
   unsigned w_bytes, in0_bytes, in1_bytes;  // buffer-descriptor ranges
 };
 
-using h4 = __attribute__((ext_vector_type(4))) _Float16;
-using h8 = __attribute__((ext_vector_type(8))) _Float16;
-
-constexpr float SPLIT_SCALE = 2048.f;  // lo is stored scaled by 2^11 (kept out of f16 subnormals)
-
-// x = hi + lo / 2048 to ~22 bits: hi = f16(x); x - hi is exact in fp32, its
-// 2^11-scaled value rounds to f16 lo.
-__device__ __forceinline__ void split4(const f32x4 x, h4& hi, h4& lo) {
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const _Float16 h = (_Float16)x[e];
-    hi[e] = h;
-    lo[e] = (_Float16)((x[e] - (float)h) * SPLIT_SCALE);
-  }
-}
-
-__device__ __forceinline__ float sigmoidf_(float v) { return 1.0f / (1.0f + expf(-v)); }
-
-__device__ __forceinline__ void epilogue(const raft_conv2d_params& p, long m, int n, float v) {
-  if (p.add0) v += p.add0[m * p.add0_ld + n];
-  float* o = p.out + m * p.out_ld + n;
-  switch (p.epilogue) {
-    case RAFT_EPI_LINEAR:
-      *o = p.alpha * v;
-      break;
-    case RAFT_EPI_RELU:
-      *o = fmaxf(v, 0.f);
-      break;
-    case RAFT_EPI_RESID_RELU:
-      *o = fmaxf(p.aux0[m * p.aux0_ld + n] + fmaxf(v, 0.f), 0.f);
-      break;
-    case RAFT_EPI_GRU_ZR:
-      if (n < p.split) {
-        *o = sigmoidf_(v);
-      } else {
-        const int c = n - p.split;
-        p.out1[m * p.out1_ld + c] = sigmoidf_(v) * p.aux0[m * p.aux0_ld + c];
-      }
-      break;
-    case RAFT_EPI_GRU_Q: {
-      const float q = tanhf(v);
-      const float z = p.aux1[m * p.aux1_ld + n];
-      const float h = p.aux0[m * p.aux0_ld + n];
-      *o = (1.0f - z) * h + z * q;
-      break;
-    }
-    case RAFT_EPI_TANH_RELU:
-      if (n < p.split)
-        *o = tanhf(v);
-      else
-        p.out1[m * p.out1_ld + (n - p.split)] = fmaxf(v, 0.f);
-      break;
-    case RAFT_EPI_ADD_TO_OUT:
-      *o = *o + v;
-      break;
-    default:
-      break;
-  }
-}
-
-// Epilogue of one 32x32 MFMA tile: lane owns column n and the 16 rows
-// mb + (r&3) + 8*(r>>2).  All operand loads of the 16 rows (add0, aux0/aux1,
-// the ADD_TO_OUT destination) are issued together from clamped addresses
-// before any store, and only the stores are predicated: on gfx9 stores share
-// vmcnt with loads, so a row-by-row load/store interleave would wait for every
-// earlier store to complete (one full write latency per row).
-__device__ __forceinline__ long row_of(int mb, int r) { return mb + (r & 3) + 8 * (r >> 2); }
-
-__device__ __forceinline__ void load_rows(const float* base, int ld, int M, int mb, int col, float (&t)[16]) {
-#pragma unroll
-  for (int r = 0; r < 16; ++r) t[r] = base[min(row_of(mb, r), (long)M - 1) * ld + col];
-}
-
-// branch-free activations (no per-row control flow between the stores)
-__device__ __forceinline__ float sigmoid_bf(float x) { return __frcp_rn(1.0f + __expf(-x)); }
-__device__ __forceinline__ float tanh_bf(float x) { return 1.0f - 2.0f * __frcp_rn(__expf(2.0f * x) + 1.0f); }
-
-__device__ __forceinline__ void tile_epilogue(const raft_conv2d_params& p, int M, int mb, int n, const f32x16& acc) {
-  const bool ncol = n < p.n;
-  const int nc = ncol ? n : p.n - 1;  // clamped column for loads
-  float v[16];
-  const float bias = p.bias ? p.bias[nc] : 0.f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = acc[r] + bias;
-  if (p.add0) {
-    float t[16];
-    load_rows(p.add0, p.add0_ld, M, mb, nc, t);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] += t[r];
-  }
-  // 1) operand loads, 2) values, 3) stores: destination dst[row * ld + col]
-  float* dst = p.out;
-  int ld = p.out_ld, col = n;
-  const int epi = p.epilogue;
-  if (epi == RAFT_EPI_LINEAR) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] *= p.alpha;
-  } else if (epi == RAFT_EPI_RELU) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = fmaxf(v[r], 0.f);
-  } else if (epi == RAFT_EPI_RESID_RELU) {
-    float t[16];
-    load_rows(p.aux0, p.aux0_ld, M, mb, nc, t);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = fmaxf(t[r] + fmaxf(v[r], 0.f), 0.f);
-  } else if (epi == RAFT_EPI_GRU_ZR) {
-    if (nc < p.split) {  // a wave's 32 columns lie on one side of split (split % 32 == 0, host-checked)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = sigmoid_bf(v[r]);
-    } else {
-      col = nc - p.split;
-      float t[16];
-      load_rows(p.aux0, p.aux0_ld, M, mb, col, t);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = sigmoid_bf(v[r]) * t[r];
-      dst = p.out1;
-      ld = p.out1_ld;
-    }
-  } else if (epi == RAFT_EPI_GRU_Q) {
-    float h[16], z[16];
-    load_rows(p.aux0, p.aux0_ld, M, mb, nc, h);
-    load_rows(p.aux1, p.aux1_ld, M, mb, nc, z);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = (1.0f - z[r]) * h[r] + z[r] * tanh_bf(v[r]);
-  } else if (epi == RAFT_EPI_TANH_RELU) {
-    if (nc < p.split) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = tanh_bf(v[r]);
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = fmaxf(v[r], 0.f);
-      dst = p.out1;
-      ld = p.out1_ld;
-      col = n - p.split;
-    }
-  } else if (epi == RAFT_EPI_ADD_TO_OUT) {
-    float t[16];
-    load_rows(p.out, p.out_ld, M, mb, nc, t);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] += t[r];
-  }
-#pragma unroll
-  for (int r = 0; r < 16; ++r)
-    if (ncol && row_of(mb, r) < M) dst[row_of(mb, r) * ld + col] = v[r];
-}
-
 // Per-thread staging state: two A rows (output pixels) of the tile.
 struct AWalk {
   int pb[2], py[2], px[2];  // pb: the row's image base pixel (b * in_h * in_w)
   bool pv[2];
 };
-
-constexpr unsigned OFF_INVALID = 0x80000000u;  // > num_records of every buffer (host-checked)
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
-}
-
-__device__ __forceinline__ f32x4 buf_load4(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
-}
 
 // GATHER mode (small / unaligned inputs): element-wise loads through the
 // k -> (ky, kx, c) LDS table, issued unconditionally from clamped addresses;
@@ -516,7 +360,9 @@ __global__ __launch_bounds__(256 * KG, 4) void conv_gemm_kernel(ConvArgs a) {  /
 #endif
 #ifdef ABL_NOLOOP
   if (a.M > 0) {
-    tile_epilogue(p, a.M, m0 + wm * 32 + 4 * (lane >> 5), n0 + wn * 32 + (lane & 31), acc);
+    int rows[16];
+    for (int r = 0; r < 16; ++r) rows[r] = -1;
+    tile_epilogue(p, rows, n0 + wn * 32 + (lane & 31), acc);
     return;
   }
 #endif
@@ -608,7 +454,13 @@ __global__ __launch_bounds__(256 * KG, 4) void conv_gemm_kernel(ConvArgs a) {  /
   }
 
   // ---- epilogue: lane owns column n, rows (r&3) + 8*(r>>2) + 4*(lane>>5)
-  tile_epilogue(p, a.M, m0 + wm * 32 + 4 * (lane >> 5), n0 + wn * 32 + (lane & 31), acc);
+  int rows[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = (int)row_of(m0 + wm * 32 + 4 * (lane >> 5), r);
+    rows[r] = m < a.M ? m : -1;
+  }
+  tile_epilogue(p, rows, n0 + wn * 32 + (lane & 31), acc);
 }
 
 // Small-N convolution (N <= 4, VEC inputs): one wave per output pixel.
@@ -773,6 +625,15 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
                  "raft_conv2d GATHER: kh*kw*cin must be <= %d (got %d)", MAX_GATHER_K, p.kh * p.kw * ctot);
   }
   RAFT_REQUIRE(((uintptr_t)p.weight & 15) == 0, "raft_conv2d: weight must be 16-byte aligned");
+  {
+    // the epilogue indexes rows with 32-bit element offsets
+    int ldmax = p.out_ld;
+    if (p.out1) ldmax = ldmax > p.out1_ld ? ldmax : p.out1_ld;
+    if (p.aux0) ldmax = ldmax > p.aux0_ld ? ldmax : p.aux0_ld;
+    if (p.aux1) ldmax = ldmax > p.aux1_ld ? ldmax : p.aux1_ld;
+    if (p.add0) ldmax = ldmax > p.add0_ld ? ldmax : p.add0_ld;
+    RAFT_REQUIRE((long)a.M * ldmax < (1L << 30), "raft_conv2d: output rows exceed 2^30 elements (split the batch)");
+  }
   switch (p.epilogue) {
     case RAFT_EPI_RESID_RELU:
       RAFT_REQUIRE(p.aux0, "raft_conv2d: RESID_RELU needs aux0");
@@ -806,6 +667,8 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
   }
   RAFT_REQUIRE(p.precision == RAFT_PREC_FP32 || p.precision == RAFT_PREC_F16X3 || p.precision == RAFT_PREC_F16,
                "raft_conv2d: unknown precision %d", p.precision);
+  if (p.mode == RAFT_CONV_VEC && conv_halo_launch(p, k_pad, n_pad, a.w_bytes, a.in0_bytes, a.in1_bytes, s) == 0)
+    return check_launch("raft_conv2d(halo)");
   a.gn = n_pad / BN;
   const long tiles = (long)cdiv(a.M, BM) * a.gn;
   RAFT_REQUIRE(tiles < (1L << 31), "raft_conv2d: too many tiles");

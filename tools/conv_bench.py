@@ -49,6 +49,17 @@ for name, cin, cout, kh, kw, pad in SHAPES:
     e1.record()
     e1.synchronize()
     us = e0.elapsed_time(e1) / reps * 1e3
+    if __import__("os").environ.get("HSTAMPS"):
+        import ctypes
+        import numpy as np
+        lib = _lib.load()
+        buf = np.zeros(4 * 16384, dtype=np.uint64)
+        lib.raft_debug_hstamps(ctypes.c_void_p(buf.ctypes.data), buf.size)
+        st = buf.reshape(-1, 4).astype(np.float64)
+        st = st[st.sum(1) > 0]
+        mean = st.mean(0)
+        print(f"   halo stamps over {len(st)} waves (cycles per wave): issue {mean[0]:.0f} compute {mean[1]:.0f} "
+              f"wait {mean[2]:.0f} barrier {mean[3]:.0f}")
     if __import__("os").environ.get("STAMPS"):
         import ctypes
         import numpy as np
