@@ -11,13 +11,20 @@
 //     the chunk on it (3x3: 180 instead of 9x128 pixel rows);
 //   * 128-pixel tiles halve the weight re-reads of the 64-row tiles.
 // Both operands move by LDS-DMA (buffer_load ... lds, 1 KiB per wave
-// instruction, no VGPR staging), so D super-steps of loads stay in flight
-// behind a counted vmcnt and a raw s_barrier.
+// instruction, no VGPR staging), D load sets ahead of the MFMAs, behind a
+// counted vmcnt and one raw s_barrier per super-step.
 //
-// Work-group: 8 waves = 2 K-groups x 4 waves.  K-step j = (chunk j / T, tap
-// j % T), T = kh*kw; super-step s runs K-step 2s in group 0 and 2s+1 in group
-// 1 (two waves per SIMD interleave), each wave a 32-pixel x BNT-channel block
-// (two tile rows).  The groups' accumulators are summed through LDS.
+// Work-group: 4 waves, one per SIMD; wave w owns tile rows 2w, 2w+1 (32
+// pixels) x BNT output channels.  K-step j = (chunk j / T, tap j % T) with
+// T = kh*kw; a super-step runs U K-steps.  Inside a wave the K-steps are
+// software-pipelined: the LDS fragments of step j+1 are read while the MFMAs
+// of step j run and are split to f16 behind them, so one wave per SIMD keeps
+// its MFMA pipe fed without a second wave to interleave.
+//
+// Load set u = K-steps Uu .. Uu+U-1, issued during super-step u - D: every
+// wave moves NWP 1-KiB pieces of one K-step's weight block (branch-free:
+// K-steps past the end load zeros into their unused ring slot) and, when a
+// chunk starts in the set, its share of that chunk's patch.
 //
 // LDS images (lane-linear DMA writes, XOR-swizzled on the SOURCE address so
 // the fragment reads are conflict-free): a patch pixel / weight row is 128 B
@@ -29,15 +36,16 @@
 // Arithmetic: F16X3 splits each fp32 activation after its LDS read,
 // x = hi + lo (hi = f16(x), lo = f16(x - hi), unscaled: the f16-subnormal
 // floor of lo is an absolute 2^-25 per element), against the pre-split
-// weight (hi, 2048*lo):  acc += hi*hi + lo*hi,  accx += hi*(2048 lo).
-// F16 (mixed precision) runs hi*hi only.
+// weight (hi, 2048*lo): acc += hi*hi, acl += lo*hi, accx += hi*(2048 lo),
+// three independent accumulator chains.  F16 (mixed precision) runs hi*hi.
 #include "conv_common.hpp"
 
 namespace raft {
 namespace {
 
-constexpr int HTW = 16;  // tile width (pixels)
-constexpr int HTH = 8;   // tile height: 128 GEMM rows per work-group
+constexpr int HTW = 16;              // tile width (pixels)
+constexpr int HTH = 8;               // tile height: 128 GEMM rows per work-group
+constexpr int HALO_LDS = 160 * 1024;  // LDS per CU (one work-group per CU)
 
 struct HaloArgs {
   raft_conv2d_params p;
@@ -49,20 +57,45 @@ struct HaloArgs {
   unsigned w_bytes, in0_bytes, in1_bytes;
 };
 
-// Smallest number of patch slots such that chunk c's patch, issued with the
-// loads of super-step floor(cT/2) at super-step floor(cT/2) - D, never lands
-// in the slot of a chunk still read at or after that issue point (a K-step's
-// fragments are read one super-step before its MFMAs).
-template <int T, int D>
-constexpr int patch_slots() {
+// Smallest patch ring such that chunk c's patch never lands in the slot of a
+// chunk that is still read.  In super-steps of U K-steps: chunk c's patch is
+// part of load set cT/U, issued during super-step cT/U - D (the prologue's
+// sets 0 .. D-1 count as issued before any read); K-step j >= 1 is read
+// during super-step (j-1)/U, K-step 0 before super-step 0 (-1).
+constexpr int patch_slots(int T, int U, int D) {
   for (int pa = 1; pa < 16; ++pa) {
     bool ok = true;
-    for (int c = pa; c < 256; ++c)
-      if ((c * T) / 2 - D < ((c - pa) * T + T - 1) / 2) ok = false;
+    for (int c = pa; c < 512 && ok; ++c) {
+      const int last = (c - pa) * T + T - 1;  // last K-step of the slot's previous chunk
+      const int rd = last == 0 ? -1 : (last - 1) / U;
+      ok = (c * T) / U - D > rd;
+    }
     if (ok) return pa;
   }
   return 16;
 }
+constexpr int halo_lds_bytes(int T, int U, int D, int BNT, int PI) {
+  return U * (D + 1) * BNT * 128 + patch_slots(T, U, D) * PI * 1024;
+}
+
+template <int KH, int KW, int BNT>
+struct HaloCfg {
+  static constexpr int T = KH * KW;
+  static constexpr int U = (BNT == 32 && T > 1) ? 4 : 2;  // K-steps per super-step
+  static constexpr int PH = HTH + KH - 1, PW = HTW + KW - 1, NPIX = PH * PW;
+  static constexpr int PI = (NPIX + 7) / 8;  // 1-KiB DMA pieces per patch
+  // load sets in flight ahead of the super-step: 3, or 2 where 3 does not fit
+#ifdef HALO_D  // dev builds: deeper load rings where they fit
+  static constexpr int D = halo_lds_bytes(T, U, HALO_D, BNT, PI) <= HALO_LDS   ? HALO_D
+                           : halo_lds_bytes(T, U, 3, BNT, PI) <= HALO_LDS ? 3
+                                                                          : 2;
+#else
+  static constexpr int D = halo_lds_bytes(T, U, 3, BNT, PI) <= HALO_LDS ? 3 : 2;
+#endif
+  static constexpr int PA = patch_slots(T, U, D);
+  static constexpr int SB = U * (D + 1);  // weight-block ring (K-steps)
+  static constexpr int LDS_B = SB * BNT * 128, LDS_A = PA * PI * 1024;
+};
 
 #ifdef STAMPS  // dev-only phase timing (tools/conv_bench.py HSTAMPS=1 with a -DSTAMPS variant)
 __device__ unsigned long long g_hstamp[4 * 16384];
@@ -79,11 +112,12 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, void* lds, unsi
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
 }
 
-// s_waitcnt vmcnt(n) only (expcnt / lgkmcnt at their maxima); n <= 15 here
+// s_waitcnt vmcnt(n) only (expcnt / lgkmcnt at their maxima)
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 15) | 0x70 | 0xF00 | ((N >> 4) << 14));
 }
+// n > 15 waits for 15 (stricter than needed, never looser)
 __device__ __forceinline__ void wait_vm_n(int n) {
   switch (n) {
     case 0: wait_vm<0>(); break;
@@ -141,30 +175,23 @@ __device__ __forceinline__ void split8(const f32x4 x0, const f32x4 x1, h8& hi, h
 }
 
 template <int KH, int KW, int BNT, int PREC>
-__global__ __launch_bounds__(512, 1) void conv_halo_kernel(HaloArgs a) {
-  constexpr int T = KH * KW;
-#ifdef HALO_D  // dev builds: load depth override
-  constexpr int D = T == 1 ? 3 : HALO_D;
-#else
-  constexpr int D = T == 1 ? 3 : 4;             // load sets issued ahead of the super-step
-#endif
-  constexpr int PH = HTH + KH - 1, PW = HTW + KW - 1, NPIX = PH * PW;
-  constexpr int PI = (NPIX + 7) / 8;            // 1-KiB DMA pieces per patch
-  constexpr int PA = patch_slots<T, D>();
-  constexpr int SB = 2 * D;                     // weight-block ring (K-steps)
-  constexpr int NBI = BNT / 8;                  // DMA pieces per weight block
-  constexpr int NSUB = BNT / 32;                // 32-column MFMA subtiles per wave
-  constexpr int LDS_B = SB * BNT * 128;
-  constexpr int LDS_A = PA * PI * 1024;
+__global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
+  using C = HaloCfg<KH, KW, BNT>;
+  constexpr int T = C::T, U = C::U, D = C::D, PW = C::PW, NPIX = C::NPIX, PI = C::PI, PA = C::PA, SB = C::SB;
+  constexpr int NBI = BNT / 8;      // 1-KiB DMA pieces per weight block (one K-step)
+  constexpr int NWP = U * NBI / 4;  // weight pieces per loader wave per load set
+  constexpr int NSUB = BNT / 32;    // 32-column MFMA subtiles per compute wave
   constexpr bool X3 = PREC == RAFT_PREC_F16X3;
-  static_assert(LDS_B + LDS_A <= 160 * 1024, "LDS budget");
-  static_assert(NSUB * 16 * 256 * 4 <= LDS_B + LDS_A, "K-group reduction buffer");
-  __shared__ __attribute__((aligned(1024))) char smem[LDS_B + LDS_A];
+  static_assert(D >= 2 && C::LDS_B + C::LDS_A <= HALO_LDS, "LDS budget");
+  static_assert(NWP >= 1 && NBI % NWP == 0, "a wave's weight pieces lie in one K-step");
+  static_assert(U % 2 == 0 && (T == 1 || T >= U), "fragment parity; at most one chunk start per load set");
+  __shared__ __attribute__((aligned(1024))) char smem[C::LDS_B + C::LDS_A];
 
   const raft_conv2d_params& p = a.p;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = w >> 2, wm = w & 3;
+  const bool loader = w >= 4;  // waves 4-7 move the operands, waves 0-3 compute
+  const int lw = w & 3;
 
   // tile (N fastest: an output tile's N-tiles share its input patch in L2)
   const int q = xcd_tile(blockIdx.x, gridDim.x);
@@ -174,106 +201,127 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(HaloArgs a) {
   const int y0 = (sr / a.tx_n) * HTH, x0 = (sr % a.tx_n) * HTW;
   const int n0 = nt * BNT;
   const int nk = a.nk, nch = a.nch;
-  const int ns = (nk + 1) >> 1;
+  const int ns = (nk + U - 1) / U;
 
-  const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(p.weight, a.w_bytes);
-  const __amdgpu_buffer_rsrc_t rs0 = make_rsrc(p.in0, a.in0_bytes);
-  const __amdgpu_buffer_rsrc_t rs1 = make_rsrc(p.in1_c ? p.in1 : p.in0, p.in1_c ? a.in1_bytes : a.in0_bytes);
-  const int in0_c = p.in0_c, in1_c = p.in1_c;
-  const unsigned ld0 = p.in0_ld, ld1 = p.in1_c ? p.in1_ld : p.in0_ld;
-  const int in_h = p.in_h, in_w = p.in_w;
-  const unsigned pb = (unsigned)b * (unsigned)(in_h * in_w);
-  const unsigned wrow = (unsigned)a.K * 4u;
-
-  // ---- loads ---------------------------------------------------------------
-  // Everything per lane is fixed by the tile, so the DMA addresses are
-  // precomputed once; per K-step only scalar offsets change (the main loop
-  // must stay light on SALU: eight waves share one scalar unit).
-  // Patch pieces of this wave: i = w, w+8, w+16 (< PI): pixels 8i .. 8i+7.
-  constexpr int PK = (PI + 7) / 8;
-  unsigned ppix[PK];  // input pixel index, or OFF_INVALID outside the image / patch
-  unsigned pq4[PK];   // the lane's channel quad within a chunk (swizzled source), x 4
-#pragma unroll
-  for (int k = 0; k < PK; ++k) {
-    const int pp = 8 * (w + 8 * k) + (lane >> 3);
-    const int py = pp / PW, px = pp - py * PW;
-    const int qd = (lane & 7) ^ ((px >> 1) & 7);
-    const int iy = y0 + py - (KH - 1) / 2, ix = x0 + px - (KW - 1) / 2;
-    const bool ok = pp < NPIX && (unsigned)iy < (unsigned)in_h && (unsigned)ix < (unsigned)in_w;
-    ppix[k] = ok ? pb + (unsigned)iy * (unsigned)in_w + (unsigned)ix : OFF_INVALID;
-    pq4[k] = 4u * (unsigned)qd;
-  }
-  const int pcw = PI > w ? (PI - 1 - w) / 8 + 1 : 0;  // this wave's pieces per patch
-  auto issue_patch = [&](int c, int slot) {
-    const bool s0 = 32 * c < in0_c;  // uniform: the chunk lies in one segment
-    const unsigned cb = (unsigned)(s0 ? 32 * c : 32 * c - in0_c);
-    const unsigned lim = (unsigned)(s0 ? in0_c : in1_c);
-    const unsigned ld = s0 ? ld0 : ld1;
-    char* base = smem + LDS_B + slot * (PI * 1024);
+  if (loader) {
+    // ---- loader waves ------------------------------------------------------
+    const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(p.weight, a.w_bytes);
+    const __amdgpu_buffer_rsrc_t rs0 = make_rsrc(p.in0, a.in0_bytes);
+    const __amdgpu_buffer_rsrc_t rs1 = make_rsrc(p.in1_c ? p.in1 : p.in0, p.in1_c ? a.in1_bytes : a.in0_bytes);
+    const int in0_c = p.in0_c, in1_c = p.in1_c;
+    const unsigned ld0 = p.in0_ld, ld1 = p.in1_c ? p.in1_ld : p.in0_ld;
+    const int in_h = p.in_h, in_w = p.in_w;
+    const unsigned pb = (unsigned)b * (unsigned)(in_h * in_w);
+    const unsigned wrow = (unsigned)a.K * 4u;
+    // Patch pieces of this loader: i = lw, lw+4, ... (< PI), pixels 8i .. 8i+7.
+    // Everything per lane is fixed by the tile, so the DMA addresses are
+    // precomputed once; per chunk only the channel offset changes.
+    constexpr int PK = (PI + 3) / 4;
+    unsigned ppix[PK];  // input pixel index, or OFF_INVALID outside the image / patch
+    unsigned pq4[PK];   // the lane's channel quad within a chunk (swizzled source), x 4
 #pragma unroll
     for (int k = 0; k < PK; ++k) {
-      if (w + 8 * k < PI) {
-        const unsigned ch = cb + pq4[k];
-        const unsigned voff = (ppix[k] != OFF_INVALID && ch < lim) ? (ppix[k] * ld + ch) * 4u : OFF_INVALID;
-        dma16(s0 ? rs0 : rs1, base + (w + 8 * k) * 1024, voff, 0);
-      }
+      const int pp = 8 * (lw + 4 * k) + (lane >> 3);
+      const int py = pp / PW, px = pp - py * PW;
+      const int qd = (lane & 7) ^ ((px >> 1) & 7);
+      const int iy = y0 + py - (KH - 1) / 2, ix = x0 + px - (KW - 1) / 2;
+      const bool ok = pp < NPIX && (unsigned)iy < (unsigned)in_h && (unsigned)ix < (unsigned)in_w;
+      ppix[k] = ok ? pb + (unsigned)iy * (unsigned)in_w + (unsigned)ix : OFF_INVALID;
+      pq4[k] = 4u * (unsigned)qd;
     }
-  };
-  // Weight pieces: rows 8i .. 8i+7 of a K-step's BNT-row block; wave w loads
-  // piece w of both K-steps of a super-step (BNT = 64) or piece w%4 of K-step
-  // w/4 (BNT = 32)
-  const int wpiece = NBI == 8 ? w : (w & 3);
-  unsigned wvoff;
-  {
-    const int r = 8 * wpiece + (lane >> 3);
-    const int qd = (lane & 7) ^ ((r >> 1) & 7);
-    wvoff = (unsigned)(n0 + r) * wrow + (unsigned)qd * 16u;
+    const int pcw = PI > lw ? (PI - 1 - lw) / 4 + 1 : 0;  // this wave's pieces per patch
+    auto issue_patch = [&](int c) {  // chunks past the end load zeros
+      const bool s0 = 32 * c < in0_c;  // uniform: the chunk lies in one segment
+      const unsigned cb = (unsigned)(s0 ? 32 * c : 32 * c - in0_c);
+      const unsigned lim = (unsigned)(s0 ? in0_c : in1_c);
+      const unsigned ld = s0 ? ld0 : ld1;
+      char* base = smem + C::LDS_B + (c % PA) * (PI * 1024);
+#pragma unroll
+      for (int k = 0; k < PK; ++k) {
+        if (lw + 4 * k < PI) {
+          const unsigned ch = cb + pq4[k];
+          const unsigned voff = (ppix[k] != OFF_INVALID && ch < lim) ? (ppix[k] * ld + ch) * 4u : OFF_INVALID;
+          dma16(s0 ? rs0 : rs1, base + (lw + 4 * k) * 1024, voff, 0);
+        }
+      }
+    };
+    // Weight pieces of this loader: NWP consecutive 8-row pieces of the block
+    // of K-step ew of every load set.
+    const int ew = (lw * NWP) / NBI, wpc0 = (lw * NWP) % NBI;
+    unsigned wvoff[NWP];
+#pragma unroll
+    for (int k = 0; k < NWP; ++k) {
+      const int r = 8 * (wpc0 + k) + (lane >> 3);
+      const int qd = (lane & 7) ^ ((r >> 1) & 7);
+      wvoff[k] = (unsigned)(n0 + r) * wrow + (unsigned)qd * 16u;
+    }
+    // load set u; returns this wave's DMA count
+    auto issue_set = [&](int u) -> int {
+      {
+        const int j = U * u + ew;
+        const bool in = j < nk;
+        const int c = j / T, t = j - c * T;
+        const unsigned soff = in ? (unsigned)(t * nch + c) * 128u : 0u;  // packed K-step (tap, chunk)
+        char* dst = smem + (U * (u % (D + 1)) + ew) * (BNT * 128) + wpc0 * 1024;
+#pragma unroll
+        for (int k = 0; k < NWP; ++k) dma16(rs_w, dst + k * 1024, in ? wvoff[k] : OFF_INVALID, soff);
+      }
+      if constexpr (T == 1) {
+#pragma unroll
+        for (int e = 0; e < U; ++e) issue_patch(U * u + e);
+        return NWP + U * pcw;
+      } else {
+        const int c = (U * u + T - 1) / T;  // the chunk starting in this set, if any
+        if (c < nch && c * T < U * u + U) {
+          issue_patch(c);
+          return NWP + pcw;
+        }
+        return NWP;
+      }
+    };
+    // Super-step s: issue load set s+D, wait until load set s+2 has landed
+    // (the last K-step of super-step s+1 reads its first block), barrier.
+    // hist[k] = this wave's DMA count of the set issued k super-steps ago.
+    constexpr int NH = D > 3 ? D - 3 : 1;
+    int hist[NH];
+    {
+      int cnt[D];
+#pragma unroll
+      for (int u = 0; u < D; ++u) cnt[u] = issue_set(u);
+      int n = 0;
+#pragma unroll
+      for (int u = 2; u < D; ++u) n += cnt[u];
+      wait_vm_n(n);  // load sets 0 and 1 have landed
+#pragma unroll
+      for (int k = 0; k < NH; ++k) hist[k] = k < D - 3 ? cnt[D - 1 - k] : 0;
+    }
+    __builtin_amdgcn_s_barrier();
+    for (int s = 0; s < ns; ++s) {
+      const int nnew = U * (s + 1) < nk ? issue_set(s + D) : 0;  // nothing left to load past that
+      int n = D >= 3 ? nnew : 0;  // in flight after set s+2: sets s+3 .. s+D
+#pragma unroll
+      for (int k = 0; k < D - 3; ++k) n += hist[k];
+      wait_vm_n(n);
+      __builtin_amdgcn_s_barrier();  // set s+2 readable by every wave
+#pragma unroll
+      for (int k = NH - 1; k > 0; --k) hist[k] = hist[k - 1];
+      hist[0] = nnew;
+    }
+    wait_vm<0>();  // nothing may land after the work-group exits
+    return;
   }
-  // issue cursor: the next K-step to load, as (chunk, tap), its K-step
-  // index in the packed weight (tap*nch + chunk) and its ring slots
-  int i_j = 0, i_c = 0, i_t = 0, i_kk = 0, i_bs = 0, i_ps = 0;
-  auto issue_set = [&]() {  // load set of the next super-step; returns this wave's DMA count
-    int n = 0;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      if (i_j < nk) {
-        if (i_t == 0) {
-          issue_patch(i_c, i_ps);
-          n += pcw;
-        }
-        if (NBI == 8 || (w >> 2) == e) {
-          dma16(rs_w, smem + i_bs * (BNT * 128) + wpiece * 1024, wvoff, (unsigned)i_kk * 128u);
-          ++n;
-        }
-        ++i_j;
-        ++i_t;
-        i_kk += nch;
-        i_bs = i_bs + 1 == SB ? 0 : i_bs + 1;
-        if (i_t == T) {
-          i_t = 0;
-          ++i_c;
-          i_kk = i_c;
-          i_ps = i_ps + 1 == PA ? 0 : i_ps + 1;
-        }
-      }
-    }
-    return n;
-  };
 
-  // ---- fragments -----------------------------------------------------------
+  // ---- compute waves: fragments --------------------------------------------
   const int m = lane & 31, h = lane >> 5;
-  const int ppbase = (2 * wm + (m >> 4)) * PW + (m & 15);
-  int bro[NSUB];  // the lane's weight-row byte offset per subtile
-#pragma unroll
-  for (int sb = 0; sb < NSUB; ++sb) bro[sb] = (sb * 32 + m) * 128;
-  const int bsw = ((m >> 1) & 7);  // (r >> 1) & 7 for r = sb*32 + m
+  const int ppbase = (2 * w + (m >> 4)) * PW + (m & 15);
+  const int bsw = (m >> 1) & 7;  // swizzle of weight row sb*32 + m
   f32x16 acc[NSUB], accx[NSUB];
 #pragma unroll
   for (int sb = 0; sb < NSUB; ++sb) {
     acc[sb] = f32x16{};
     accx[sb] = f32x16{};
   }
-  // read cursor of this wave's K-group: K-steps g, g+2, g+4, ...
+  // read cursor: (tap, ky, kx) of the next K-step to read and its ring slots
   int c_t = 0, c_ky = 0, c_kx = 0, c_bs = 0, c_ps = 0;
   auto step_cursor = [&]() {
     ++c_kx;
@@ -288,20 +336,13 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(HaloArgs a) {
       c_ps = c_ps + 1 == PA ? 0 : c_ps + 1;
     }
   };
-  if (g == 1) step_cursor();
   struct Frag {
     f32x4 av[4];
+    h8 ah[2], al[2];
     h8 bh[NSUB][2], bl[NSUB][2];
   };
-  // the K-step under the read cursor: A (fp32) and weight (pre-split) fragments
-  auto read_frag = [&](Frag& F) {
-#ifdef HALO_ABL_NOREAD  // timing ablation (dev builds only): no fragment reads
-    F.av[0] = f32x4{(float)c_ps, (float)c_bs, (float)c_ky, (float)c_kx};
-    step_cursor();
-    step_cursor();
-    return;
-#endif
-    const char* Ab = smem + LDS_B + c_ps * (PI * 1024);
+  auto read_step = [&](Frag& F) {
+    const char* Ab = smem + C::LDS_B + c_ps * (PI * 1024);
     const char* Bb = smem + c_bs * (BNT * 128);
     const int pp = ppbase + (c_ky * PW + c_kx);
     const int sw = (((m & 15) + c_kx) >> 1) & 7;  // swizzle of patch column px
@@ -312,116 +353,97 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(HaloArgs a) {
     for (int sb = 0; sb < NSUB; ++sb) {
 #pragma unroll
       for (int qq = 0; qq < 2; ++qq) {
-        F.bh[sb][qq] = *reinterpret_cast<const h8*>(Bb + bro[sb] + (((2 * h + qq) ^ bsw) << 4));
-        if constexpr (X3) F.bl[sb][qq] = *reinterpret_cast<const h8*>(Bb + bro[sb] + (((4 + 2 * h + qq) ^ bsw) << 4));
+        F.bh[sb][qq] = *reinterpret_cast<const h8*>(Bb + (sb * 32 + m) * 128 + (((2 * h + qq) ^ bsw) << 4));
+        if constexpr (X3)
+          F.bl[sb][qq] = *reinterpret_cast<const h8*>(Bb + (sb * 32 + m) * 128 + (((4 + 2 * h + qq) ^ bsw) << 4));
       }
     }
     step_cursor();
-    step_cursor();
   };
-  auto mfma_frag = [&](const Frag& F) {
-    h8 ah[2], al[2];
+  auto split_step = [&](Frag& F) {
 #ifdef HALO_ABL_NOSPLIT  // timing ablation (dev builds only): bit casts instead of the split
-    ah[0] = __builtin_bit_cast(h8, F.av[0]);
-    al[0] = __builtin_bit_cast(h8, F.av[1]);
-    ah[1] = __builtin_bit_cast(h8, F.av[2]);
-    al[1] = __builtin_bit_cast(h8, F.av[3]);
+    F.ah[0] = __builtin_bit_cast(h8, F.av[0]);
+    F.al[0] = __builtin_bit_cast(h8, F.av[1]);
+    F.ah[1] = __builtin_bit_cast(h8, F.av[2]);
+    F.al[1] = __builtin_bit_cast(h8, F.av[3]);
 #else
-    split8<X3>(F.av[0], F.av[1], ah[0], al[0]);
-    split8<X3>(F.av[2], F.av[3], ah[1], al[1]);
+    split8<X3>(F.av[0], F.av[1], F.ah[0], F.al[0]);
+    split8<X3>(F.av[2], F.av[3], F.ah[1], F.al[1]);
 #endif
+  };
+  // the MFMAs of one accumulator never follow each other back to back
+  auto mfma_step = [&](const Frag& F) {
 #pragma unroll
-    for (int sb = 0; sb < NSUB; ++sb) {
+    for (int qq = 0; qq < 2; ++qq) {
 #pragma unroll
-      for (int qq = 0; qq < 2; ++qq) {
-        acc[sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[qq], F.bh[sb][qq], acc[sb], 0, 0, 0);
-        if constexpr (X3) {
-          acc[sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[qq], F.bh[sb][qq], acc[sb], 0, 0, 0);
-          accx[sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[qq], F.bl[sb][qq], accx[sb], 0, 0, 0);
-        }
+      for (int sb = 0; sb < NSUB; ++sb)
+        acc[sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.ah[qq], F.bh[sb][qq], acc[sb], 0, 0, 0);
+      if constexpr (X3) {
+#pragma unroll
+        for (int sb = 0; sb < NSUB; ++sb)
+          accx[sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.ah[qq], F.bl[sb][qq], accx[sb], 0, 0, 0);
+#pragma unroll
+        for (int sb = 0; sb < NSUB; ++sb)
+          acc[sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.al[qq], F.bh[sb][qq], acc[sb], 0, 0, 0);
       }
     }
   };
 
-  // ---- pipeline ------------------------------------------------------------
-  // Super-step s: issue load set s+D; read the fragments of K-step 2(s+1)+g
-  // (load set s+1) while the MFMAs of K-step 2s+g run on the registers read
-  // last super-step; wait until load set s+2 has landed; one barrier.
-  // hist[k] = this wave's DMA count of the load set issued k super-steps ago.
-  constexpr int NH = D - 3 > 0 ? D - 3 : 1;
-  int hist[NH];
-  {
-    int cnt[D];
-#pragma unroll
-    for (int u = 0; u < D; ++u) cnt[u] = issue_set();
-    int n = 0;
-#pragma unroll
-    for (int u = 2; u < D; ++u) n += cnt[u];
-    wait_vm_n(n);  // load sets 0 and 1 have landed
-#pragma unroll
-    for (int k = 0; k < NH; ++k) hist[k] = D - 1 - k >= 3 ? cnt[D - 1 - k] : 0;
-  }
-  __builtin_amdgcn_s_barrier();
-  Frag F0, F1;
-  if (g < nk) read_frag(F0);
+  // ---- compute waves: pipeline ---------------------------------------------
+  // Super-step s runs K-steps Us .. Us+U-1 on fragments read one K-step ahead
+  // (the last one reads the first K-step of super-step s+1), then one barrier.
+  __builtin_amdgcn_s_barrier();  // load sets 0 and 1 have landed
+  Frag F[2];
+  read_step(F[0]);
+  split_step(F[0]);
 #ifdef STAMPS
-  unsigned long long t_iss = 0, t_cmp = 0, t_wait = 0, t_bar = 0, t0 = hstamp_now();
-  const unsigned long long t_begin = t0;
+  unsigned long long t_cmp = 0, t_wait = 0, t_bar = 0, t0 = hstamp_now();
 #endif
-  auto super_step = [&](int s, Frag& Fc, Frag& Fn) {
-#ifdef STAMPS
-    unsigned long long t1 = hstamp_now();
-    t_iss += t1 - t0;
-#endif
-    const int nnew = issue_set();  // load set s + D
-    if (2 * (s + 1) + g < nk) read_frag(Fn);
-#ifdef HALO_ABL_NOMFMA  // timing ablation (dev builds only): fragments consumed, no MFMA
-    if (2 * s + g < nk) acc[0][0] += Fc.av[0][0] + (float)Fc.bh[0][0][0];
-#else
-    if (2 * s + g < nk) mfma_frag(Fc);
-#endif
+  for (int s = 0; s < ns; ++s) {
+    if (U * (s + 1) < nk) {  // a whole super-step, and the next one exists
+#pragma unroll
+      for (int e = 0; e < U; ++e) {
+        read_step(F[(e + 1) & 1]);
+        mfma_step(F[e & 1]);
+        split_step(F[(e + 1) & 1]);
+      }
+    } else {  // the last super-step
+#pragma unroll
+      for (int e = 0; e < U; ++e) {
+        const int j = U * s + e;
+        if (j < nk) {
+          const bool nx = j + 1 < nk;
+          if (nx) read_step(F[(e + 1) & 1]);
+          mfma_step(F[e & 1]);
+          if (nx) split_step(F[(e + 1) & 1]);
+        }
+      }
+    }
 #ifdef STAMPS
     unsigned long long t2 = hstamp_now();
-    t_cmp += t2 - t1;
-#endif
-    // in flight after load set s+2: sets s+3 .. s+D
-    int n = nnew;
-#pragma unroll
-    for (int k = 0; k < D - 3; ++k) n += hist[k];
-#ifndef HALO_ABL_NOWAIT  // timing ablation (dev builds only): no DMA wait in the loop
-    wait_vm_n(n);
+    t_cmp += t2 - t0;
 #endif
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the next fragments are in registers
 #ifdef STAMPS
     unsigned long long t3 = hstamp_now();
     t_wait += t3 - t2;
 #endif
-#ifndef HALO_ABL_NOBAR  // timing ablation (dev builds only)
-    __builtin_amdgcn_s_barrier();  // set s+2 readable by every wave; set s+1's reads done
-#endif
+    __builtin_amdgcn_s_barrier();  // the reads of super-step s are done; set s+2 has landed
 #ifdef STAMPS
     t0 = hstamp_now();
     t_bar += t0 - t3;
 #endif
-#pragma unroll
-    for (int k = NH - 1; k > 0; --k) hist[k] = hist[k - 1];
-    hist[0] = nnew;
-  };
-  for (int s = 0; s < ns; s += 2) {
-    super_step(s, F0, F1);
-    if (s + 1 < ns) super_step(s + 1, F1, F0);
   }
 
 #ifdef STAMPS
   {
-    const unsigned wid = blockIdx.x * 8 + w;
+    const unsigned wid = blockIdx.x * 4 + w;
     if (lane == 0 && wid < 16384) {
-      g_hstamp[wid * 4 + 0] = t_iss;
+      g_hstamp[wid * 4 + 0] = 0;
       g_hstamp[wid * 4 + 1] = t_cmp;
       g_hstamp[wid * 4 + 2] = t_wait;
       g_hstamp[wid * 4 + 3] = t_bar;
     }
-    (void)t_begin;
   }
 #endif
   if constexpr (X3) {
@@ -430,27 +452,13 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(HaloArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[sb][r] += accx[sb][r] * (1.0f / SPLIT_SCALE);
   }
-  // K-group 1 hands its partial sums to group 0 through LDS (every DMA has landed)
-  float* red = reinterpret_cast<float*>(smem);
-  if (g == 1) {
-#pragma unroll
-    for (int sb = 0; sb < NSUB; ++sb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) red[((sb * 16 + r) * 4 + wm) * 64 + lane] = acc[sb][r];
-  }
-  __syncthreads();
-  if (g == 1) return;
-#pragma unroll
-  for (int sb = 0; sb < NSUB; ++sb)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[sb][r] += red[((sb * 16 + r) * 4 + wm) * 64 + lane];
 
   // ---- epilogue: register r holds tile row m = (r&3) + 8(r>>2) + 4h of this wave's 32
   int rows[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int mm = (r & 3) + 8 * (r >> 2) + 4 * h;
-    const int y = y0 + 2 * wm + (mm >> 4), x = x0 + (mm & 15);
+    const int y = y0 + 2 * w + (mm >> 4), x = x0 + (mm & 15);
     rows[r] = (y < p.out_h && x < p.out_w) ? (b * p.out_h + y) * p.out_w + x : -1;
   }
 #pragma unroll
