@@ -98,7 +98,16 @@ struct HaloCfg {
 };
 
 #ifdef STAMPS  // dev-only phase timing (tools/conv_bench.py HSTAMPS=1 with a -DSTAMPS variant)
-__device__ unsigned long long g_hstamp[4 * 16384];
+// per compute wave: realtime at entry / exit (100 MHz), then shader cycles of
+// the prologue, compute, wait + barrier, epilogue
+__device__ unsigned long long g_hstamp[8 * 16384];
+__device__ __forceinline__ unsigned long long hstamp_real() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
 __device__ __forceinline__ unsigned long long hstamp_now() {
   unsigned long long t;
   __builtin_amdgcn_sched_barrier(0);
@@ -187,6 +196,9 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
   static_assert(U % 2 == 0 && (T == 1 || T >= U), "fragment parity; at most one chunk start per load set");
   __shared__ __attribute__((aligned(1024))) char smem[C::LDS_B + C::LDS_A];
 
+#ifdef STAMPS
+  const unsigned long long r_entry = hstamp_real(), c_entry = hstamp_now();
+#endif
   const raft_conv2d_params& p = a.p;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -271,8 +283,8 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
         for (int e = 0; e < U; ++e) issue_patch(U * u + e);
         return NWP + U * pcw;
       } else {
-        const int c = (U * u + T - 1) / T;  // the chunk starting in this set, if any
-        if (c < nch && c * T < U * u + U) {
+        const int c = (U * u + T - 1) / T;  // the chunk starting in this set, if any (zeros past nch)
+        if (c * T < U * u + U) {
           issue_patch(c);
           return NWP + pcw;
         }
@@ -297,7 +309,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
     }
     __builtin_amdgcn_s_barrier();
     for (int s = 0; s < ns; ++s) {
-      const int nnew = U * (s + 1) < nk ? issue_set(s + D) : 0;  // nothing left to load past that
+      const int nnew = s + D < ns ? issue_set(s + D) : 0;
       int n = D >= 3 ? nnew : 0;  // in flight after set s+2: sets s+3 .. s+D
 #pragma unroll
       for (int k = 0; k < D - 3; ++k) n += hist[k];
@@ -321,34 +333,21 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
     acc[sb] = f32x16{};
     accx[sb] = f32x16{};
   }
-  // read cursor: (tap, ky, kx) of the next K-step to read and its ring slots
-  int c_t = 0, c_ky = 0, c_kx = 0, c_bs = 0, c_ps = 0;
-  auto step_cursor = [&]() {
-    ++c_kx;
-    if (c_kx == KW) {
-      c_kx = 0;
-      ++c_ky;
-    }
-    c_bs = c_bs + 1 == SB ? 0 : c_bs + 1;
-    if (++c_t == T) {
-      c_t = 0;
-      c_ky = 0;
-      c_ps = c_ps + 1 == PA ? 0 : c_ps + 1;
-    }
-  };
+  // Fragment reads run ahead of the MFMAs: the B fragments of K-step j+1 and
+  // the A (activation) values of K-step j+2 are read while K-step j's MFMAs
+  // run, and A of j+1 (read one K-step earlier) is split to f16 behind them,
+  // so neither the LDS latency nor the split stalls the MFMA stream.
+  // B cursor: the weight ring slot of the next K-step to read; A cursor:
+  // (tap, ky, kx) and the patch ring slot of the next K-step to read.
+  int b_bs = 0;
+  int a_t = 0, a_ky = 0, a_kx = 0, a_ps = 0;
   struct Frag {
-    f32x4 av[4];
     h8 ah[2], al[2];
     h8 bh[NSUB][2], bl[NSUB][2];
   };
-  auto read_step = [&](Frag& F) {
-    const char* Ab = smem + C::LDS_B + c_ps * (PI * 1024);
-    const char* Bb = smem + c_bs * (BNT * 128);
-    const int pp = ppbase + (c_ky * PW + c_kx);
-    const int sw = (((m & 15) + c_kx) >> 1) & 7;  // swizzle of patch column px
-#pragma unroll
-    for (int jq = 0; jq < 4; ++jq)
-      F.av[jq] = *reinterpret_cast<const f32x4*>(Ab + pp * 128 + (((4 * h + jq) ^ sw) << 4));
+  f32x4 av[4];  // raw A values of the K-step after the next
+  auto read_b = [&](Frag& F) {
+    const char* Bb = smem + b_bs * (BNT * 128);
 #pragma unroll
     for (int sb = 0; sb < NSUB; ++sb) {
 #pragma unroll
@@ -358,17 +357,34 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
           F.bl[sb][qq] = *reinterpret_cast<const h8*>(Bb + (sb * 32 + m) * 128 + (((4 + 2 * h + qq) ^ bsw) << 4));
       }
     }
-    step_cursor();
+    b_bs = b_bs + 1 == SB ? 0 : b_bs + 1;
   };
-  auto split_step = [&](Frag& F) {
+  auto read_a = [&]() {
+    const char* Ab = smem + C::LDS_B + a_ps * (PI * 1024);
+    const int pp = ppbase + (a_ky * PW + a_kx);
+    const int sw = (((m & 15) + a_kx) >> 1) & 7;  // swizzle of patch column px
+#pragma unroll
+    for (int jq = 0; jq < 4; ++jq) av[jq] = *reinterpret_cast<const f32x4*>(Ab + pp * 128 + (((4 * h + jq) ^ sw) << 4));
+    ++a_kx;
+    if (a_kx == KW) {
+      a_kx = 0;
+      ++a_ky;
+    }
+    if (++a_t == T) {
+      a_t = 0;
+      a_ky = 0;
+      a_ps = a_ps + 1 == PA ? 0 : a_ps + 1;
+    }
+  };
+  auto split_a = [&](Frag& F) {
 #ifdef HALO_ABL_NOSPLIT  // timing ablation (dev builds only): bit casts instead of the split
-    F.ah[0] = __builtin_bit_cast(h8, F.av[0]);
-    F.al[0] = __builtin_bit_cast(h8, F.av[1]);
-    F.ah[1] = __builtin_bit_cast(h8, F.av[2]);
-    F.al[1] = __builtin_bit_cast(h8, F.av[3]);
+    F.ah[0] = __builtin_bit_cast(h8, av[0]);
+    F.al[0] = __builtin_bit_cast(h8, av[1]);
+    F.ah[1] = __builtin_bit_cast(h8, av[2]);
+    F.al[1] = __builtin_bit_cast(h8, av[3]);
 #else
-    split8<X3>(F.av[0], F.av[1], F.ah[0], F.al[0]);
-    split8<X3>(F.av[2], F.av[3], F.ah[1], F.al[1]);
+    split8<X3>(av[0], av[1], F.ah[0], F.al[0]);
+    split8<X3>(av[2], av[3], F.ah[1], F.al[1]);
 #endif
   };
   // the MFMAs of one accumulator never follow each other back to back
@@ -390,34 +406,27 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
   };
 
   // ---- compute waves: pipeline ---------------------------------------------
-  // Super-step s runs K-steps Us .. Us+U-1 on fragments read one K-step ahead
-  // (the last one reads the first K-step of super-step s+1), then one barrier.
+  // Super-step s runs K-steps Us .. Us+U-1 (its reads reach K-step U(s+1)+1,
+  // all in load sets s and s+1), then one barrier.  K-steps past nk (up to
+  // U*ns) run on zero weights and zero patches: they add exact zeros, and the
+  // loop body has no branches.
   __builtin_amdgcn_s_barrier();  // load sets 0 and 1 have landed
   Frag F[2];
-  read_step(F[0]);
-  split_step(F[0]);
+  read_a();
+  read_b(F[0]);
+  split_a(F[0]);
+  read_a();
 #ifdef STAMPS
   unsigned long long t_cmp = 0, t_wait = 0, t_bar = 0, t0 = hstamp_now();
+  const unsigned long long c_loop = t0;
 #endif
   for (int s = 0; s < ns; ++s) {
-    if (U * (s + 1) < nk) {  // a whole super-step, and the next one exists
 #pragma unroll
-      for (int e = 0; e < U; ++e) {
-        read_step(F[(e + 1) & 1]);
-        mfma_step(F[e & 1]);
-        split_step(F[(e + 1) & 1]);
-      }
-    } else {  // the last super-step
-#pragma unroll
-      for (int e = 0; e < U; ++e) {
-        const int j = U * s + e;
-        if (j < nk) {
-          const bool nx = j + 1 < nk;
-          if (nx) read_step(F[(e + 1) & 1]);
-          mfma_step(F[e & 1]);
-          if (nx) split_step(F[(e + 1) & 1]);
-        }
-      }
+    for (int e = 0; e < U; ++e) {
+      read_b(F[(e + 1) & 1]);
+      mfma_step(F[e & 1]);
+      split_a(F[(e + 1) & 1]);
+      read_a();
     }
 #ifdef STAMPS
     unsigned long long t2 = hstamp_now();
@@ -436,15 +445,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
   }
 
 #ifdef STAMPS
-  {
-    const unsigned wid = blockIdx.x * 4 + w;
-    if (lane == 0 && wid < 16384) {
-      g_hstamp[wid * 4 + 0] = 0;
-      g_hstamp[wid * 4 + 1] = t_cmp;
-      g_hstamp[wid * 4 + 2] = t_wait;
-      g_hstamp[wid * 4 + 3] = t_bar;
-    }
-  }
+  const unsigned long long c_epi = hstamp_now();
 #endif
   if constexpr (X3) {
 #pragma unroll
@@ -463,6 +464,22 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
   }
 #pragma unroll
   for (int sb = 0; sb < NSUB; ++sb) tile_epilogue(p, rows, n0 + sb * 32 + m, acc[sb]);
+#ifdef STAMPS
+  {
+    const unsigned long long c_exit = hstamp_now(), r_exit = hstamp_real();
+    const unsigned wid = blockIdx.x * 4 + w;
+    if (lane == 0 && wid < 16384) {
+      unsigned long long* g = g_hstamp + wid * 8;
+      g[0] = r_entry;
+      g[1] = r_exit;
+      g[2] = c_loop - c_entry;
+      g[3] = t_cmp;
+      g[4] = t_wait + t_bar;
+      g[5] = c_exit - c_epi;
+      g[6] = c_exit - c_entry;
+    }
+  }
+#endif
 }
 
 template <int KH, int KW, int PREC>

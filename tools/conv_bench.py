@@ -53,13 +53,17 @@ for name, cin, cout, kh, kw, pad in SHAPES:
         import ctypes
         import numpy as np
         lib = _lib.load()
-        buf = np.zeros(4 * 16384, dtype=np.uint64)
+        buf = np.zeros(8 * 16384, dtype=np.uint64)
         lib.raft_debug_hstamps(ctypes.c_void_p(buf.ctypes.data), buf.size)
-        st = buf.reshape(-1, 4).astype(np.float64)
-        st = st[st.sum(1) > 0]
+        st = buf.reshape(-1, 8).astype(np.float64)
+        st = st[st[:, 0] > 0]
+        st = st[st[:, 0] > st[:, 0].max() - 20000]  # the last launch (realtime ticks of 10 ns)
         mean = st.mean(0)
-        print(f"   halo stamps over {len(st)} waves (cycles per wave): issue {mean[0]:.0f} compute {mean[1]:.0f} "
-              f"wait {mean[2]:.0f} barrier {mean[3]:.0f}")
+        span = (st[:, 1].max() - st[:, 0].min()) * 0.01
+        clk = (st[:, 6] / np.maximum(st[:, 1] - st[:, 0], 1)).mean() * 100
+        print(f"   halo stamps, {len(st)} compute waves: span {span:.1f} us, entry skew {(st[:, 0].max() - st[:, 0].min()) * 0.01:.1f} us, "
+              f"clock {clk:.0f} MHz; cycles/wave: prologue {mean[2]:.0f} compute {mean[3]:.0f} "
+              f"wait+barrier {mean[4]:.0f} epilogue {mean[5]:.0f} total {mean[6]:.0f}")
     if __import__("os").environ.get("STAMPS"):
         import ctypes
         import numpy as np
