@@ -313,7 +313,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
       int n = D >= 3 ? nnew : 0;  // in flight after set s+2: sets s+3 .. s+D
 #pragma unroll
       for (int k = 0; k < D - 3; ++k) n += hist[k];
-      wait_vm_n(n);
+      wait_vm_n(s + 1 < ns ? n : 0);  // nothing may land after the last barrier
       __builtin_amdgcn_s_barrier();  // set s+2 readable by every wave
 #pragma unroll
       for (int k = NH - 1; k > 0; --k) hist[k] = hist[k - 1];
