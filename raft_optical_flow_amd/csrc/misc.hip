@@ -202,6 +202,46 @@ __global__ __launch_bounds__(256) void instnorm_partial_kernel(const float* x, i
   }
 }
 
+// Vectorised stage 1 (C and ld multiples of 4, x 16-B aligned): thread =
+// (row r, channel quad q), 16-B loads, the same shifted sums per channel.
+__global__ __launch_bounds__(256) void instnorm_partial4_kernel(const float* x, int ld, int HW, int C, float* part) {
+  __shared__ f32x4 red[2][256];
+  const int b = blockIdx.y, chunk = blockIdx.x;
+  const int nchunk = gridDim.x;
+  const int p0 = chunk * IN_CHUNK, p1 = min(HW, p0 + IN_CHUNK);
+  const float* xb = x + (long)b * HW * ld;
+  const int nq = C >> 2;
+  for (int qg = 0; qg < nq; qg += 256) {
+    const int qe = min(256, nq - qg);
+    const int R = 256 / qe;
+    const int q = qg + threadIdx.x % qe, r = threadIdx.x / qe;
+    f32x4 s = {0.f, 0.f, 0.f, 0.f}, ss = s;
+    if (r < R) {
+      const f32x4 shift = *reinterpret_cast<const f32x4*>(xb + 4 * q);
+#pragma unroll 4
+      for (int p = p0 + r; p < p1; p += R) {
+        const f32x4 d = *reinterpret_cast<const f32x4*>(xb + (long)p * ld + 4 * q) - shift;
+        s += d;
+        ss += d * d;
+      }
+    }
+    red[0][threadIdx.x] = s;
+    red[1][threadIdx.x] = ss;
+    __syncthreads();
+    if (threadIdx.x < qe) {
+      f32x4 S = {0.f, 0.f, 0.f, 0.f}, SS = S;
+      for (int k = 0; k < R; ++k) {
+        S += red[0][k * qe + threadIdx.x];
+        SS += red[1][k * qe + threadIdx.x];
+      }
+      f32x4* o = reinterpret_cast<f32x4*>(part + (((long)b * nchunk + chunk) * C + 4 * (qg + threadIdx.x)) * 2);
+      o[0] = f32x4{S[0], SS[0], S[1], SS[1]};
+      o[1] = f32x4{S[2], SS[2], S[3], SS[3]};
+    }
+    __syncthreads();
+  }
+}
+
 // stage 2: one 256-thread block per (image, 16-channel group); 16 chunk rows per
 // channel summed in double, then a fixed-order LDS reduction (deterministic).
 __global__ __launch_bounds__(256) void instnorm_finalize_kernel(const float* x, int ld, int HW, int C, int nchunk,
@@ -260,6 +300,40 @@ __global__ void instnorm_apply_kernel(const float* x, int ld, const float* stats
     out[pix * old + c] = v;
   }
 }
+
+// Vectorised apply (C, ld, resid_ld, out_ld multiples of 4, 16-B aligned rows):
+// thread = (pixel, channel quad), 32-bit indexing (B*HW*C/4 < 2^31).
+__global__ __launch_bounds__(256) void instnorm_apply4_kernel(const float* x, int ld, const float* stats,
+                                                              const float* resid, int rld, const float* rstats, int mode,
+                                                              float* out, int old, int HW, int nq, unsigned total) {
+  for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const unsigned pix = i / (unsigned)nq, q = i - pix * (unsigned)nq;
+    const unsigned b = pix / (unsigned)HW;
+    const unsigned si = (b * (unsigned)nq + q) * 8u;  // (mean, rstd) of channels 4q .. 4q+3
+    const f32x4 s0 = *reinterpret_cast<const f32x4*>(stats + si), s1 = *reinterpret_cast<const f32x4*>(stats + si + 4);
+    const f32x4 xv = *reinterpret_cast<const f32x4*>(x + (size_t)pix * ld + 4 * q);
+    f32x4 v = {(xv[0] - s0[0]) * s0[1], (xv[1] - s0[2]) * s0[3], (xv[2] - s1[0]) * s1[1], (xv[3] - s1[2]) * s1[3]};
+    if (mode >= 1) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    if (resid) {
+      f32x4 r = *reinterpret_cast<const f32x4*>(resid + (size_t)pix * rld + 4 * q);
+      if (rstats) {
+        const f32x4 r0 = *reinterpret_cast<const f32x4*>(rstats + si), r1 = *reinterpret_cast<const f32x4*>(rstats + si + 4);
+        r = f32x4{(r[0] - r0[0]) * r0[1], (r[1] - r0[2]) * r0[3], (r[2] - r1[0]) * r1[1], (r[3] - r1[2]) * r1[3]};
+      }
+      v = r + v;
+      if (mode == 2) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+    }
+    *reinterpret_cast<f32x4*>(out + (size_t)pix * old + 4 * q) = v;
+  }
+}
+
+bool aligned16(const void* q) { return ((uintptr_t)q & 15) == 0; }
 
 }  // namespace
 }  // namespace raft
@@ -341,7 +415,10 @@ extern "C" int raft_instnorm_stats(const float* x, int ld, int B, int HW, int C,
   RAFT_REQUIRE(x && stats && workspace && B > 0 && HW > 0 && C > 0 && ld >= C, "raft_instnorm_stats: bad arguments");
   const int nchunk = (int)cdiv_l(HW, IN_CHUNK);
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(instnorm_partial_kernel, dim3(nchunk, B), dim3(256), 0, s, x, ld, HW, C, workspace);
+  if (C % 4 == 0 && ld % 4 == 0 && aligned16(x) && aligned16(workspace))
+    hipLaunchKernelGGL(instnorm_partial4_kernel, dim3(nchunk, B), dim3(256), 0, s, x, ld, HW, C, workspace);
+  else
+    hipLaunchKernelGGL(instnorm_partial_kernel, dim3(nchunk, B), dim3(256), 0, s, x, ld, HW, C, workspace);
   int rc = check_launch("raft_instnorm_stats(partial)");
   if (rc) return rc;
   hipLaunchKernelGGL(instnorm_finalize_kernel, dim3(cdiv(C, 16), B), dim3(256), 0, s, x, ld, HW, C, nchunk,
@@ -357,7 +434,14 @@ extern "C" int raft_instnorm_apply(const float* x, int ld, const float* stats, c
   RAFT_REQUIRE(relu_mode >= 0 && relu_mode <= 2, "raft_instnorm_apply: bad relu_mode");
   RAFT_REQUIRE(!resid || resid_ld >= C, "raft_instnorm_apply: bad resid_ld");
   const long n = (long)B * HW * C;
-  hipLaunchKernelGGL(instnorm_apply_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, ld, stats, resid,
-                     resid_ld, resid_stats, relu_mode, out, out_ld, B, HW, C);
+  const bool vec = C % 4 == 0 && ld % 4 == 0 && out_ld % 4 == 0 && aligned16(x) && aligned16(out) &&
+                   aligned16(stats) && (!resid || (resid_ld % 4 == 0 && aligned16(resid))) &&
+                   (!resid_stats || aligned16(resid_stats)) && n / 4 < (1L << 31);
+  if (vec)
+    hipLaunchKernelGGL(instnorm_apply4_kernel, dim3(grid_for(n / 4)), dim3(256), 0, as_stream(stream), x, ld, stats,
+                       resid, resid_ld, resid_stats, relu_mode, out, out_ld, HW, C / 4, (unsigned)(n / 4));
+  else
+    hipLaunchKernelGGL(instnorm_apply_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, ld, stats, resid,
+                       resid_ld, resid_stats, relu_mode, out, out_ld, B, HW, C);
   return check_launch("raft_instnorm_apply");
 }

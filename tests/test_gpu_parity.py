@@ -166,6 +166,9 @@ CONV_CASES = [
     (64, 96, 3, 3, 2, (1, 1), 19, 24, 1),
     (96, 96, 1, 1, 2, (0, 0), 19, 24, 1),
     (256, 2, 3, 3, 1, (1, 1), 7, 9, 1),
+    (256, 2, 3, 3, 1, (1, 1), 13, 35, 2),
+    (96, 3, 3, 3, 1, (1, 1), 9, 21, 1),
+    (128, 2, 1, 1, 1, (0, 0), 6, 10, 1),
     (128, 576, 1, 1, 1, (0, 0), 5, 6, 1),
     (256, 126, 3, 3, 1, (1, 1), 12, 12, 1),
 ]

@@ -19,6 +19,7 @@ SHAPES = [  # name, cin, cout, kh, kw, pad
     ("convc1", 324, 256, 1, 1, (0, 0)), ("convc2", 256, 192, 3, 3, (1, 1)), ("convf2", 128, 64, 3, 3, (1, 1)),
     ("conv", 256, 126, 3, 3, (1, 1)), ("zr", 384, 256, 1, 5, (0, 2)), ("q", 384, 128, 1, 5, (0, 2)),
     ("zr_split", 256, 256, 1, 5, (0, 2)), ("q_split", 256, 128, 1, 5, (0, 2)), ("fh1", 128, 256, 3, 3, (1, 1)), ("fh1mask", 128, 512, 3, 3, (1, 1)), ("mask2", 256, 576, 1, 1, (0, 0)),
+    ("fh2", 256, 2, 3, 3, (1, 1)),
 ]
 tot_t = 0
 for name, cin, cout, kh, kw, pad in SHAPES:
