@@ -360,7 +360,11 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
 #pragma unroll
   for (int k = 0; k < LMAX; ++k)
     *reinterpret_cast<f32x4*>(&patch[wv][pidx<LMAX>(ti * 4 + rr, tj * 4, k)]) = ok[k] ? v[k] : zero;
-  __syncthreads();
+  // the patch and y-table are this wave's own: a wave-local barrier (the
+  // block's four pixels never wait for each other)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (!valid) return;
 
   // phase 3: lane (l, ix) walks its column iy = 0 .. 2r of output channels
