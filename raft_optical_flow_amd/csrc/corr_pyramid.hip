@@ -277,6 +277,24 @@ __device__ __forceinline__ int pidx(int r, int c, int l) {
   return ((r * 4 + (c >> 2)) * LMAX + l) * 4 + (c & 3);
 }
 
+#ifdef LK_STAMPS  // dev-only phase timing of the lookup (tools/lookup_bench.py LKSTAMPS=1)
+__device__ unsigned long long g_lkstamp[8 * 65536];
+__device__ __forceinline__ unsigned long long lk_clock(bool real) {
+  unsigned long long t;
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_sched_barrier(0);
+  if (real)
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  else
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define LK_STAMP(k) const unsigned long long lk_t##k = lk_clock(false)
+#else
+#define LK_STAMP(k)
+#endif
+
 template <int R, int LMAX>
 __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
 #pragma clang fp contract(off)  // the reference's bilinear is separate multiplies and adds
@@ -298,7 +316,15 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
   const int b = gpc / P;
   const int p = gpc - b * P;
   float x = 0.f, y = 0.f;
+#ifdef LK_STAMPS
+  const unsigned long long lk_r0 = lk_clock(true);
+#endif
+  LK_STAMP(0);
   load_coords(a.coords, a.coords_layout, b, p, P, x, y);
+#ifdef LK_STAMPS
+  asm volatile("" ::"v"(x), "v"(y));
+#endif
+  LK_STAMP(1);
 
   // phase 1: per level, the <= 4x4 tiles covering the (2r+2)^2 integer window,
   // one 16-B load per lane (lane = tile row ti, tile col tj, row-in-tile rr),
@@ -328,6 +354,7 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
 #endif
   }
 
+  LK_STAMP(2);
   // phase 2 (while the loads fly): lane (l, d) = (lane / RD, lane % RD)
   // evaluates x-entry d (kept: this lane's column in phase 3) and y-entry d
   // (shared through LDS) of level l, with the reference's arithmetic — offset
@@ -360,6 +387,7 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
 #pragma unroll
   for (int k = 0; k < LMAX; ++k)
     *reinterpret_cast<f32x4*>(&patch[wv][pidx<LMAX>(ti * 4 + rr, tj * 4, k)]) = ok[k] ? v[k] : zero;
+  LK_STAMP(3);
   // the patch and y-table are this wave's own: a wave-local barrier (the
   // block's four pixels never wait for each other)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -421,6 +449,7 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
       }
     }
   }
+  LK_STAMP(4);
 #ifdef LK_ABL_NOSTORE  // timing ablation (dev builds only): no output stores
   if (val[0] != -12345.f) return;
 #endif
@@ -454,7 +483,22 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
     const float g = lane == 0 ? (float)(p % a.W) : (float)(p / a.W);
     a.flow[(long)gp * a.flow_ld + lane] = (lane == 0 ? x : y) - g;
   }
+#ifdef LK_STAMPS
+  LK_STAMP(5);
+  const unsigned long long lk_r1 = lk_clock(true);
+  if (lane == 0 && gp < 65536) {
+    unsigned long long* g = g_lkstamp + gp * 8;
+    g[0] = lk_r0;
+    g[1] = lk_r1;
+    g[2] = lk_t1 - lk_t0;  // coords load
+    g[3] = lk_t2 - lk_t1;  // tile-load issue
+    g[4] = lk_t3 - lk_t2;  // phase 2 + landing of the tiles + patch writes
+    g[5] = lk_t4 - lk_t3;  // taps
+    g[6] = lk_t5 - lk_t4;  // stores (issued and completed)
+  }
+#endif
 }
+
 
 int grid_for(long n, int block = 256) {
   long g = (n + block - 1) / block;
@@ -487,6 +531,12 @@ bool pyramid_levels(int B, int H, int W, int L, Level* lv) {
 }  // namespace raft
 
 using namespace raft;
+
+#ifdef LK_STAMPS
+extern "C" int raft_debug_lkstamps(unsigned long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_lkstamp), sizeof(unsigned long long) * (size_t)n);
+}
+#endif
 
 extern "C" size_t raft_corr_pyramid_floats(int B, int H, int W, int L) {
   if (B <= 0 || H <= 0 || W <= 0 || L <= 0 || L > LK_MAXL) return 0;

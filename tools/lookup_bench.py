@@ -68,3 +68,17 @@ for _ in range(reps):
     calib()
 torch.cuda.synchronize()
 print(f"calib copy: {calib_src.numel()*4/1e6:.1f} MB read + written per launch")
+
+if os.environ.get("LKSTAMPS"):
+    import ctypes
+    import numpy as np
+    lib = _lib.load()
+    buf = np.zeros(8 * 65536, dtype=np.uint64)
+    lib.raft_debug_lkstamps(ctypes.c_void_p(buf.ctypes.data), buf.size)
+    st = buf.reshape(-1, 8).astype(np.float64)
+    st = st[st[:, 0] > 0]
+    st = st[st[:, 0] > st[:, 0].max() - 20000]
+    m = st.mean(0)
+    print(f"   lookup stamps, {len(st)} waves: span {(st[:, 1].max() - st[:, 0].min()) * 0.01:.2f} us, entry skew "
+          f"{(st[:, 0].max() - st[:, 0].min()) * 0.01:.2f} us, life {((st[:, 1] - st[:, 0]) * 0.01).mean():.2f} us; "
+          f"cycles: coords {m[2]:.0f} issue {m[3]:.0f} phase2+land {m[4]:.0f} taps {m[5]:.0f} stores {m[6]:.0f}")
