@@ -411,6 +411,9 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
   // U*ns) run on zero weights and zero patches: they add exact zeros, and the
   // loop body has no branches.
   __builtin_amdgcn_s_barrier();  // load sets 0 and 1 have landed
+#ifdef HALO_PRIO
+  __builtin_amdgcn_s_setprio(HALO_PRIO);
+#endif
   Frag F[2];
   read_a();
   read_b(F[0]);
@@ -423,10 +426,15 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
   for (int s = 0; s < ns; ++s) {
 #pragma unroll
     for (int e = 0; e < U; ++e) {
+#ifdef HALO_ABL_MFMAONLY  // timing ablation (dev builds only): MFMAs on fragments read once
+      mfma_step(F[e & 1]);
+      asm volatile("" ::"v"(F[0].ah[0]), "v"(F[1].ah[0]));
+#else
       read_b(F[(e + 1) & 1]);
       mfma_step(F[e & 1]);
       split_a(F[(e + 1) & 1]);
       read_a();
+#endif
     }
 #ifdef STAMPS
     unsigned long long t2 = hstamp_now();
