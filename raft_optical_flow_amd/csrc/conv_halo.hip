@@ -191,6 +191,11 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
   constexpr int NWP = U * NBI / 4;  // weight pieces per loader wave per load set
   constexpr int NSUB = BNT / 32;    // 32-column MFMA subtiles per compute wave
   constexpr bool X3 = PREC == RAFT_PREC_F16X3;
+  // LSPLIT: the loaders stage each patch through registers and store it
+  // pre-split (f16 hi | lo, the weight-row format), so the MFMA waves read
+  // ready fragments; 1x1 convs (a patch per K-step, D = 2) keep fp32 patches
+  // moved by LDS-DMA and split in the MFMA waves.
+  constexpr bool LSPLIT = T > 1 && D == 3;
   static_assert(D >= 2 && C::LDS_B + C::LDS_A <= HALO_LDS, "LDS budget");
   static_assert(NWP >= 1 && NBI % NWP == 0, "a wave's weight pieces lie in one K-step");
   static_assert(U % 2 == 0 && (T == 1 || T >= U), "fragment parity; at most one chunk start per load set");
@@ -291,6 +296,119 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
         return NWP;
       }
     };
+    if constexpr (LSPLIT) {
+      // 8-channel patch task t = (patch pixel t/4, channel group t%4), NT = 4*NPIX;
+      // this wave's tasks t = 64*lw + lane + 256*i.  A chunk's patch is loaded in
+      // the super-step that issues its load set and split + stored in the next one
+      // (still a super-step before its first read; its slot was free already).
+      constexpr int NT = 4 * NPIX, TI = (NT + 255) / 256;
+      unsigned tpix[TI];  // input pixel, or OFF_INVALID
+      unsigned tg8[TI];   // channel offset 8g within the chunk
+      int tlds[TI];       // byte offset of the task's hi quad in a patch slot (lo: ^ 64), -1 past NT
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int t = 64 * lw + lane + 256 * i;
+        const int pp = t >> 2, g = t & 3;
+        const int py = pp / PW, px = pp - py * PW;
+        const int iy = y0 + py - (KH - 1) / 2, ix = x0 + px - (KW - 1) / 2;
+        const bool ok = t < NT && (unsigned)iy < (unsigned)in_h && (unsigned)ix < (unsigned)in_w;
+        tpix[i] = ok ? pb + (unsigned)iy * (unsigned)in_w + (unsigned)ix : OFF_INVALID;
+        tg8[i] = 8u * (unsigned)g;
+        tlds[i] = t < NT ? pp * 128 + ((g ^ ((px >> 1) & 7)) << 4) : -1;
+      }
+      using Staged = f32x4[TI][2];
+      auto load_patch = [&](int c, Staged& dst) {  // chunks past the end load zeros
+        const bool s0 = 32 * c < in0_c;
+        const unsigned cb = (unsigned)(s0 ? 32 * c : 32 * c - in0_c);
+        const unsigned lim = (unsigned)(s0 ? in0_c : in1_c);
+        const unsigned ld = s0 ? ld0 : ld1;
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const unsigned ch = cb + tg8[i] + 4u * q;
+            const unsigned voff = (tpix[i] != OFF_INVALID && ch < lim) ? (tpix[i] * ld + ch) * 4u : OFF_INVALID;
+            dst[i][q] = buf_load4(s0 ? rs0 : rs1, voff, 0);
+          }
+      };
+      auto store_patch = [&](int c, const Staged& src) {
+        char* base = smem + C::LDS_B + (c % PA) * (PI * 1024);
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          if (tlds[i] >= 0) {
+            h8 hi, lo;
+            split8<true>(src[i][0], src[i][1], hi, lo);
+            *reinterpret_cast<h8*>(base + tlds[i]) = hi;
+            *reinterpret_cast<h8*>(base + (tlds[i] ^ 64)) = lo;
+          }
+        }
+      };
+      auto issue_weights = [&](int u) {
+        const int j = U * u + ew;
+        const bool in = j < nk;
+        const int c = j / T, t = j - c * T;
+        const unsigned soff = in ? (unsigned)(t * nch + c) * 128u : 0u;
+        char* dst = smem + (U * (u % (D + 1)) + ew) * (BNT * 128) + wpc0 * 1024;
+#pragma unroll
+        for (int k = 0; k < NWP; ++k) dma16(rs_w, dst + k * 1024, in ? wvoff[k] : OFF_INVALID, soff);
+      };
+      // the chunk starting in load set u, or -1 (at most one: T >= U)
+      auto chunk_of = [&](int u) {
+        const int c = (U * u + T - 1) / T;
+        return c * T < U * u + U ? c : -1;
+      };
+      constexpr int PMAX = (U * D + T - 1) / T + 1;  // chunk starts in the prologue's sets
+      Staged pv[PMAX];
+      int pcs[PMAX];
+      int nst = 0;
+#pragma unroll
+      for (int u = 0; u < D; ++u) {
+        const int c = chunk_of(u);
+        if (c >= 0) {
+#pragma unroll
+          for (int k = 0; k < PMAX; ++k)
+            if (k == nst) {
+              load_patch(c, pv[k]);
+              pcs[k] = c;
+            }
+          ++nst;
+        }
+        issue_weights(u);
+      }
+      wait_vm<0>();
+#pragma unroll
+      for (int k = 0; k < PMAX; ++k)
+        if (k < nst) store_patch(pcs[k], pv[k]);
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the patches are in LDS
+      __builtin_amdgcn_s_barrier();
+      // Super-step s: store the patch loaded in super-step s-1, load the patch
+      // and issue the weights of set s+D, wait until set s+2's weights (issued
+      // in s-1) have landed, barrier.
+      int pend = -1;  // chunk staged in pv[0], loaded during the previous super-step
+      for (int s = 0; s < ns; ++s) {
+        if (pend >= 0) {
+          wait_vm<NWP>();  // that patch's loads (the weights issued after them may fly on)
+          store_patch(pend, pv[0]);
+          pend = -1;
+        }
+        int nnew = 0;
+        if (s + D < ns) {
+          const int c = chunk_of(s + D);
+          if (c >= 0) {
+            load_patch(c, pv[0]);
+            pend = c;
+            nnew = 2 * TI;
+          }
+          issue_weights(s + D);
+          nnew += NWP;
+        }
+        wait_vm_n(s + 1 < ns ? nnew : 0);
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): a patch stored this super-step is in LDS
+        __builtin_amdgcn_s_barrier();
+      }
+      wait_vm<0>();
+      return;
+    }
     // Super-step s: issue load set s+D, wait until load set s+2 has landed
     // (the last K-step of super-step s+1 reads its first block), barrier.
     // hist[k] = this wave's DMA count of the set issued k super-steps ago.
@@ -376,6 +494,26 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
       a_ps = a_ps + 1 == PA ? 0 : a_ps + 1;
     }
   };
+  auto read_a_split = [&](Frag& F) {  // LSPLIT: the patch holds f16 hi | lo quads
+    const char* Ab = smem + C::LDS_B + a_ps * (PI * 1024);
+    const char* row = Ab + (ppbase + (a_ky * PW + a_kx)) * 128;
+    const int sw = (((m & 15) + a_kx) >> 1) & 7;
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      F.ah[qq] = *reinterpret_cast<const h8*>(row + (((2 * h + qq) ^ sw) << 4));
+      if constexpr (X3) F.al[qq] = *reinterpret_cast<const h8*>(row + (((4 + 2 * h + qq) ^ sw) << 4));
+    }
+    ++a_kx;
+    if (a_kx == KW) {
+      a_kx = 0;
+      ++a_ky;
+    }
+    if (++a_t == T) {
+      a_t = 0;
+      a_ky = 0;
+      a_ps = a_ps + 1 == PA ? 0 : a_ps + 1;
+    }
+  };
   auto split_a = [&](Frag& F) {
 #ifdef HALO_ABL_NOSPLIT  // timing ablation (dev builds only): bit casts instead of the split
     F.ah[0] = __builtin_bit_cast(h8, av[0]);
@@ -415,10 +553,15 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
   __builtin_amdgcn_s_setprio(HALO_PRIO);
 #endif
   Frag F[2];
-  read_a();
-  read_b(F[0]);
-  split_a(F[0]);
-  read_a();
+  if constexpr (LSPLIT) {
+    read_b(F[0]);
+    read_a_split(F[0]);
+  } else {
+    read_a();
+    read_b(F[0]);
+    split_a(F[0]);
+    read_a();
+  }
 #ifdef STAMPS
   unsigned long long t_cmp = 0, t_wait = 0, t_bar = 0, t0 = hstamp_now();
   const unsigned long long c_loop = t0;
@@ -430,10 +573,16 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
       mfma_step(F[e & 1]);
       asm volatile("" ::"v"(F[0].ah[0]), "v"(F[1].ah[0]));
 #else
-      read_b(F[(e + 1) & 1]);
-      mfma_step(F[e & 1]);
-      split_a(F[(e + 1) & 1]);
-      read_a();
+      if constexpr (LSPLIT) {
+        read_b(F[(e + 1) & 1]);
+        read_a_split(F[(e + 1) & 1]);
+        mfma_step(F[e & 1]);
+      } else {
+        read_b(F[(e + 1) & 1]);
+        mfma_step(F[e & 1]);
+        split_a(F[(e + 1) & 1]);
+        read_a();
+      }
 #endif
     }
 #ifdef STAMPS
