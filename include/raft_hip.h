@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RAFT_HIP_ABI_VERSION 2
+#define RAFT_HIP_ABI_VERSION 3
 
 /* Negative return codes (argument errors, raised before any launch). */
 #define RAFT_E_INVALID (-1)   /* bad size / null pointer / unsupported shape */
@@ -67,6 +67,12 @@ const char* raft_hip_last_error(void);  /* message of the last failure on this t
 size_t raft_corr_pyramid_floats(int B, int H, int W, int num_levels);
 int raft_corr_build(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C,
                     int num_levels, float sqrt_c, float* pyramid, raft_stream_t stream);
+/* The same with the GEMM arithmetic chosen: RAFT_PREC_FP32 (raft_corr_build: f32
+ * MFMA) or RAFT_PREC_F16X3 (both fmaps split into f16 hi + lo at staging,
+ * hi*hi + lo*hi + hi*lo with fp32 accumulation: ~2^-22 relative per product,
+ * 5x the MFMA rate).  The RAFT forward uses F16X3 unless conv_precision="fp32". */
+int raft_corr_build_prec(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C,
+                         int num_levels, float sqrt_c, int precision, float* pyramid, raft_stream_t stream);
 /* Row-major copy of one level, out [B*H*W][H_l][W_l] (the reference's corr_pyramid[l]). */
 int raft_corr_pyramid_level(const float* pyramid, int B, int H, int W, int num_levels, int level,
                             float* out, raft_stream_t stream);

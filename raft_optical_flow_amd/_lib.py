@@ -28,7 +28,7 @@ PREC_F16X3 = 1   # fp32-accurate hi/lo f16 split on v_mfma_f32_32x32x16_f16
 PREC_F16 = 2     # single f16 product (mixed precision)
 PRECISIONS = {"fp32": PREC_FP32, "f16x3": PREC_F16X3, "f16": PREC_F16}
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 EPI_LINEAR = 0
 EPI_RELU = 1
@@ -68,6 +68,7 @@ _PROTOS = {
     "raft_hip_last_error": (c_char_p, []),
     "raft_corr_pyramid_floats": (c_size_t, [c_int, c_int, c_int, c_int]),
     "raft_corr_build": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, P, P]),
+    "raft_corr_build_prec": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, P, P]),
     "raft_corr_pyramid_level": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "raft_corr_lookup": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, c_int, c_int, P, c_int, P]),
     "raft_alt_corr_forward": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, P]),

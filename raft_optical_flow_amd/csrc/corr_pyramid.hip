@@ -11,6 +11,9 @@
 namespace raft {
 namespace {
 
+using h4 = __attribute__((ext_vector_type(4))) _Float16;
+using h8 = __attribute__((ext_vector_type(8))) _Float16;
+
 constexpr int LK_MAXL = 6;
 
 struct Level {
@@ -47,8 +50,14 @@ struct CorrBuildArgs {
   int nbx;  // 8x8 blocks along w2
 };
 
+// X3: fp32-accurate split-f16 MFMA (RAFT_PREC_F16X3): both fmaps are split at
+// staging into hi = f16(x) and lo = f16(x - hi) (unscaled; the LDS row holds
+// the K-step's 32 hi then 32 lo halves, 128 B + 16 B pad) and every product is
+// hi*hi + lo*hi + hi*lo on v_mfma_f32_32x32x16_f16 in three accumulators (the
+// dropped lo*lo term is 2^-22 relative).  Otherwise fp32 MFMA 32x32x2.
+template <bool X3>
 __global__ __launch_bounds__(256) void corr_build_kernel(CorrBuildArgs a) {
-  constexpr int STAGE = (CB_BM + CB_BN) * CB_LDSK;
+  constexpr int STAGE = (CB_BM + CB_BN) * CB_LDSK;  // floats per stage (fp32 rows; x3 rows use the same 144 B)
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
@@ -88,16 +97,35 @@ __global__ __launch_bounds__(256) void corr_build_kernel(CorrBuildArgs a) {
     float* A = smem + buf * STAGE;
     float* Bt = A + CB_BM * CB_LDSK;
     const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-    *reinterpret_cast<f32x4*>(A + lr * CB_LDSK + lq * 4) = ok_a[0] ? ra[0] : z;
-    *reinterpret_cast<f32x4*>(A + (lr + 32) * CB_LDSK + lq * 4) = ok_a[1] ? ra[1] : z;
-    *reinterpret_cast<f32x4*>(Bt + lr * CB_LDSK + lq * 4) = ok_b[0] ? rb[0] : z;
-    *reinterpret_cast<f32x4*>(Bt + (lr + 32) * CB_LDSK + lq * 4) = ok_b[1] ? rb[1] : z;
+    if constexpr (X3) {
+      auto put = [&](float* base, int row, f32x4 v) {
+        h4 hi, lo;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const _Float16 hh = (_Float16)v[e];
+          hi[e] = hh;
+          lo[e] = (_Float16)(v[e] - (float)hh);
+        }
+        char* r = reinterpret_cast<char*>(base) + row * (CB_LDSK * 4) + lq * 8;
+        *reinterpret_cast<h4*>(r) = hi;
+        *reinterpret_cast<h4*>(r + 64) = lo;
+      };
+      put(A, lr, ok_a[0] ? ra[0] : z);
+      put(A, lr + 32, ok_a[1] ? ra[1] : z);
+      put(Bt, lr, ok_b[0] ? rb[0] : z);
+      put(Bt, lr + 32, ok_b[1] ? rb[1] : z);
+    } else {
+      *reinterpret_cast<f32x4*>(A + lr * CB_LDSK + lq * 4) = ok_a[0] ? ra[0] : z;
+      *reinterpret_cast<f32x4*>(A + (lr + 32) * CB_LDSK + lq * 4) = ok_a[1] ? ra[1] : z;
+      *reinterpret_cast<f32x4*>(Bt + lr * CB_LDSK + lq * 4) = ok_b[0] ? rb[0] : z;
+      *reinterpret_cast<f32x4*>(Bt + (lr + 32) * CB_LDSK + lq * 4) = ok_b[1] ? rb[1] : z;
+    }
   };
   const int nk = cdiv(a.C, CB_BK);
   gload(0);
   sstore(0);
   __syncthreads();
-  f32x16 acc = {};
+  f32x16 acc = {}, acc2 = {}, acc3 = {};
   const int ao = (wm * 32 + (lane & 31)) * CB_LDSK + (lane >> 5) * 16;
   const int bo = (wn * 32 + (lane & 31)) * CB_LDSK + (lane >> 5) * 16;
   for (int kc = 0; kc < nk; ++kc) {
@@ -106,17 +134,35 @@ __global__ __launch_bounds__(256) void corr_build_kernel(CorrBuildArgs a) {
     if (more) gload(kc + 1);
     const float* A = smem + cur * STAGE;
     const float* Bt = A + CB_BM * CB_LDSK;
-    f32x4 x[4], y[4];
+    if constexpr (X3) {
+      // lane (m, h): channels 16qq + 8h .. +7 of row m: hi at byte 32qq + 16h, lo 64 bytes on
+      const char* Ar = reinterpret_cast<const char*>(A) + (wm * 32 + (lane & 31)) * (CB_LDSK * 4) + (lane >> 5) * 16;
+      const char* Br = reinterpret_cast<const char*>(Bt) + (wn * 32 + (lane & 31)) * (CB_LDSK * 4) + (lane >> 5) * 16;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      x[j] = *reinterpret_cast<const f32x4*>(A + ao + 4 * j);
-      y[j] = *reinterpret_cast<const f32x4*>(Bt + bo + 4 * j);
+      for (int qq = 0; qq < 2; ++qq) {
+        const h8 xh = *reinterpret_cast<const h8*>(Ar + 32 * qq), xl = *reinterpret_cast<const h8*>(Ar + 64 + 32 * qq);
+        const h8 yh = *reinterpret_cast<const h8*>(Br + 32 * qq), yl = *reinterpret_cast<const h8*>(Br + 64 + 32 * qq);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, yh, acc, 0, 0, 0);
+        acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, yh, acc2, 0, 0, 0);
+        acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, yl, acc3, 0, 0, 0);
+      }
+    } else {
+      f32x4 x[4], y[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x[j] = *reinterpret_cast<const f32x4*>(A + ao + 4 * j);
+        y[j] = *reinterpret_cast<const f32x4*>(Bt + bo + 4 * j);
+      }
+#pragma unroll
+      for (int s = 0; s < 16; ++s)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x[s >> 2][s & 3], y[s >> 2][s & 3], acc, 0, 0, 0);
     }
-#pragma unroll
-    for (int s = 0; s < 16; ++s)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x[s >> 2][s & 3], y[s >> 2][s & 3], acc, 0, 0, 0);
     if (more) sstore(cur ^ 1);
     __syncthreads();
+  }
+  if constexpr (X3) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] += acc2[r] + acc3[r];
   }
 
   // epilogue: scaled tile -> LDS T[64 p1][64 = 8 rows x 8 cols of the (h2, w2) block]
@@ -547,6 +593,13 @@ extern "C" size_t raft_corr_pyramid_floats(int B, int H, int W, int L) {
 
 extern "C" int raft_corr_build(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C, int L,
                                float sqrt_c, float* pyramid, raft_stream_t stream) {
+  return raft_corr_build_prec(fmap1, fmap2, ld, B, H, W, C, L, sqrt_c, RAFT_PREC_FP32, pyramid, stream);
+}
+
+extern "C" int raft_corr_build_prec(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C, int L,
+                                    float sqrt_c, int precision, float* pyramid, raft_stream_t stream) {
+  RAFT_REQUIRE(precision == RAFT_PREC_FP32 || precision == RAFT_PREC_F16X3,
+               "raft_corr_build_prec: precision must be RAFT_PREC_FP32 or RAFT_PREC_F16X3 (got %d)", precision);
   RAFT_REQUIRE(fmap1 && fmap2 && pyramid, "raft_corr_build: null pointer");
   RAFT_REQUIRE(B > 0 && H > 0 && W > 0 && C > 0 && L >= 1 && L <= LK_MAXL, "raft_corr_build: bad sizes");
   RAFT_REQUIRE(C % 4 == 0, "raft_corr_build: C must be a multiple of 4 (got %d)", C);
@@ -572,7 +625,10 @@ extern "C" int raft_corr_build(const float* fmap1, const float* fmap2, int ld, i
   a.nbx = cdiv(W, 8);
   hipStream_t s = as_stream(stream);
   dim3 grid(cdiv((int)P, CB_BM), cdiv(H, 8) * a.nbx, B);
-  hipLaunchKernelGGL(corr_build_kernel, grid, dim3(256), 0, s, a);
+  if (precision == RAFT_PREC_FP32)
+    hipLaunchKernelGGL(corr_build_kernel<false>, grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(corr_build_kernel<true>, grid, dim3(256), 0, s, a);
   int rc = check_launch("raft_corr_build");
   if (rc) return rc;
   for (int l = 2; l < L; ++l) {

@@ -411,8 +411,11 @@ class RaftPlan:
         div = K.sqrt_c(C)
         if not alternate:
             self.pyramid = A.flat(K.pyramid_floats(B, h, w, lv))
-            L.append(Launch("raft_corr_build", fmap1.data_ptr(), fmap2.data_ptr(), C, B, h, w, C, lv, div,
-                            self.pyramid.data_ptr()))
+            # the correlation GEMM follows the conv arithmetic: exact f32 MFMA in "fp32"
+            # mode, the fp32-accurate f16 split otherwise (raft_hip.h)
+            cprec = _lib.PREC_FP32 if pk.precision == _lib.PREC_FP32 else _lib.PREC_F16X3
+            L.append(Launch("raft_corr_build_prec", fmap1.data_ptr(), fmap2.data_ptr(), C, B, h, w, C, lv, div,
+                            cprec, self.pyramid.data_ptr()))
         else:
             # AlternateCorrBlock pools num_levels times (core/corr.py:157-161); the
             # last level is never used, but its existence is the reference's size check.

@@ -73,6 +73,28 @@ def test_pyramid_vs_oracle_ragged():
         assert maxabs(cb.corr_pyramid[i], ref[i]) < 1e-5 * max(1.0, scale)
 
 
+def test_pyramid_f16x3_vs_oracle():
+    """raft_corr_build_prec(RAFT_PREC_F16X3): the split-f16 correlation GEMM of the RAFT
+    forward, every level within 1e-5 (relative to the level's max) of the fp64 oracle."""
+    from raft_optical_flow_amd import _lib
+    from raft_optical_flow_amd import kernels as K
+    rng = np.random.default_rng(5)
+    B, C, H, W, L = 2, 256, 23, 37, 4
+    f1 = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    f2 = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    r1, r2 = K.nchw_to_rows(t(f1)), K.nchw_to_rows(t(f2))
+    pyr = torch.empty(K.pyramid_floats(B, H, W, L), device=DEV)
+    _lib.call("raft_corr_build_prec", r1.data_ptr(), r2.data_ptr(), C, B, H, W, C, L, K.sqrt_c(C), _lib.PREC_F16X3,
+              pyr.data_ptr(), K.stream_handle())
+    ref = O.corr_pyramid(f1.astype(np.float64), f2.astype(np.float64), L)
+    dims = K.pyramid_dims(H, W, L)
+    for i, (lh, lw) in enumerate(dims):
+        out = torch.empty(B * H * W, lh, lw, device=DEV)
+        _lib.call("raft_corr_pyramid_level", pyr.data_ptr(), B, H, W, L, i, out.data_ptr(), K.stream_handle())
+        scale = np.abs(ref[i]).max()
+        assert maxabs(out.view(ref[i].shape), ref[i]) < 1e-5 * max(1.0, scale), i
+
+
 @pytest.mark.parametrize("r", [4, 3])
 def test_lookup_golden(r):
     from raft_optical_flow_amd import CorrBlock

@@ -21,16 +21,25 @@ SHAPES = [  # name, cin, cout, kh, kw, pad
     ("zr_split", 256, 256, 1, 5, (0, 2)), ("q_split", 256, 128, 1, 5, (0, 2)), ("fh1", 128, 256, 3, 3, (1, 1)), ("fh1mask", 128, 512, 3, 3, (1, 1)), ("mask2", 256, 576, 1, 1, (0, 0)),
     ("fh2", 256, 2, 3, 3, (1, 1)),
 ]
+# encoder 3x3 convs at config 2 (fnet runs on both frames: B x 2), as (name, cin, cout, kh, kw, pad, b, h, w)
+ENC = [("l1", 64, 64, 3, 3, (1, 1), 2, 220, 512), ("l2", 96, 96, 3, 3, (1, 1), 2, 110, 256),
+       ("l3", 128, 128, 3, 3, (1, 1), 2, 55, 128)]
+if __import__("os").environ.get("SHAPESET") == "enc":
+    SHAPES = [(n, ci, co, kh, kw, pd) for n, ci, co, kh, kw, pd, _, _, _ in ENC]
+    DIMS = {n: (bb * B, hh, ww) for n, _, _, _, _, _, bb, hh, ww in ENC}
+else:
+    DIMS = {}
 tot_t = 0
 for name, cin, cout, kh, kw, pad in SHAPES:
     if ONLY and name not in ONLY:
         continue
-    x = torch.randn(B * H * W, cin, device=dev)
+    Bq, H, W = DIMS.get(name, (B, 55, 128))
+    x = torch.randn(Bq * H * W, cin, device=dev)
     w = torch.randn(cout, cin, kh, kw) * 0.05
     pc = K.pack_conv(w, torch.zeros(cout), 1, pad, device=dev)
     pc.precision = _lib.PRECISIONS[PREC]
-    out = torch.empty(B * H * W, cout, device=dev)
-    prm = K.conv_params(pc, K.Rows(x), B, H, W, K.Rows(out), epilogue=_lib.EPI_RELU)
+    out = torch.empty(Bq * H * W, cout, device=dev)
+    prm = K.conv_params(pc, K.Rows(x), Bq, H, W, K.Rows(out), epilogue=_lib.EPI_RELU)
     L = [K.conv_launch(prm)]
     for _ in range(3):
         L[0](K.stream_handle())
@@ -76,7 +85,7 @@ for name, cin, cout, kh, kw, pad in SHAPES:
         mean = st.mean(0)
         print(f"   stamps over {len(st)} waves (cycles per wave): work {mean[0]:.0f} barrier {mean[1]:.0f} "
               f"issue {mean[2]:.0f} loop {mean[3]:.0f}; max loop {st[:, 3].max():.0f}")
-    fl = 2.0 * B * H * W * cout * cin * kh * kw
+    fl = 2.0 * Bq * H * W * cout * cin * kh * kw
     tot_t += us
-    print(f"{name:8s} M={B*H*W:6d} N={cout:4d} K={cin*kh*kw:5d}  {us:8.1f} us  {fl/us/1e6:7.1f} TF/s")
+    print(f"{name:8s} M={Bq*H*W:6d} N={cout:4d} K={cin*kh*kw:5d}  {us:8.1f} us  {fl/us/1e6:7.1f} TF/s")
 print(f"total {tot_t:.1f} us ({PREC})")
