@@ -389,8 +389,10 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
     const int ntx = ((x0 + WD - 1) >> 2) - txo + 1;
     const int ty = tyo + ti, tx = txo + tj;
     const Level& lv = a.lv[l];
+    // tile rows outside the window's WD rows are not fetched (their lanes read
+    // the map's first element, an L2 hit shared by the wave)
     ok[l] = (l < a.L) & valid & (ti < nty) & (tj < ntx) & ((unsigned)ty < (unsigned)lv.th) &
-            ((unsigned)tx < (unsigned)lv.tw);
+            ((unsigned)tx < (unsigned)lv.tw) & ((unsigned)(ty * 4 + rr - y0) < (unsigned)WD);
     const float* mapb = a.pyr + lv.off + (long)gpc * lv.mapsz;
     const int off = ok[l] ? (ty * lv.tw + tx) * 16 + rr * 4 : 0;  // unconditional load, zeroed below
 #ifdef LK_ABL_NOLOAD  // timing ablation (dev builds only): no tile loads
