@@ -314,13 +314,20 @@ __device__ __forceinline__ void axis_entry(float c, int d, float m1, float rcp, 
 }
 
 // LDS patch of one wave: element (row r, column c) of level l at
-// ((r*4 + c/4)*LMAX + l)*4 + c%4 — levels interleaved at 16-B granularity, so
-// a tile row of one level is one ds_write_b128, and with LMAX = 4 the bank of
-// (r, c, l) is 16(c/4) + 4l + c%4: one bank per (column, level) whatever the
-// rows, so phase 3 (every level's lanes reading its own row) is conflict-free
+// r*RSP + ((c/4)*LMAX + l)*4 + c%4 with the row stride RSP = 16*LMAX + 4 —
+// levels interleaved at 16-B granularity, so a tile row of one level is one
+// ds_write_b128.  The 4-float row pad makes those writes conflict-free: the 32
+// lanes of a half-wave (8 rows x 4 tile columns) land on 8 distinct 16-B bank
+// slots, 4 lanes each (the minimum for 512 B), where an unpadded 256-B row put
+// 16 lanes on one slot.  The phase-3 reads (a level's lanes on consecutive
+// columns of one row) keep distinct banks within a level.
+template <int LMAX>
+constexpr int patch_rs() {
+  return 16 * LMAX + 4;
+}
 template <int LMAX>
 __device__ __forceinline__ int pidx(int r, int c, int l) {
-  return ((r * 4 + (c >> 2)) * LMAX + l) * 4 + (c & 3);
+  return r * patch_rs<LMAX>() + ((c >> 2) * LMAX + l) * 4 + (c & 3);
 }
 
 #ifdef LK_STAMPS  // dev-only phase timing of the lookup (tools/lookup_bench.py LKSTAMPS=1)
@@ -346,7 +353,7 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
 #pragma clang fp contract(off)  // the reference's bilinear is separate multiplies and adds
   constexpr int RD = 2 * R + 1;
   constexpr int WD = 2 * R + 2;  // integer window (<= 10 -> <= 4 tiles per axis)
-  constexpr int RS = 16 * LMAX;  // patch row stride (floats)
+  constexpr int RS = patch_rs<LMAX>();  // patch row stride (floats)
   static_assert(WD <= 13, "window must fit 4 tiles");
   static_assert(LMAX * RD <= 64, "one lane per (level, x offset)");
   static_assert(RS + 16 <= 255, "ds_read2 offsets");
