@@ -396,16 +396,19 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
     const int ntx = ((x0 + WD - 1) >> 2) - txo + 1;
     const int ty = tyo + ti, tx = txo + tj;
     const Level& lv = a.lv[l];
-    // tile rows outside the window's WD rows are not fetched (their lanes read
-    // the map's first element, an L2 hit shared by the wave)
+    // tile rows outside the window's WD rows are not fetched
     ok[l] = (l < a.L) & valid & (ti < nty) & (tj < ntx) & ((unsigned)ty < (unsigned)lv.th) &
             ((unsigned)tx < (unsigned)lv.tw) & ((unsigned)(ty * 4 + rr - y0) < (unsigned)WD);
+    // a raw buffer over this pixel's level map: lanes without a tile row to
+    // fetch pass an out-of-range offset and get zeros without a memory access
     const float* mapb = a.pyr + lv.off + (long)gpc * lv.mapsz;
-    const int off = ok[l] ? (ty * lv.tw + tx) * 16 + rr * 4 : 0;  // unconditional load, zeroed below
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(mapb), (short)0, (int)(lv.mapsz * 4), 0x00020000);
+    const unsigned off = ok[l] ? (unsigned)((ty * lv.tw + tx) * 16 + rr * 4) * 4u : 0x80000000u;
 #ifdef LK_ABL_NOLOAD  // timing ablation (dev builds only): no tile loads
     v[l] = f32x4{(float)off, (float)(long)mapb, 0.f, 0.f};
 #else
-    v[l] = *reinterpret_cast<const f32x4*>(mapb + off);
+    v[l] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
 #endif
   }
 
@@ -675,6 +678,7 @@ extern "C" int raft_corr_lookup(const float* pyramid, int B, int H, int W, int L
   RAFT_REQUIRE(!flow_out || flow_ld >= 2, "raft_corr_lookup: flow_ld < 2");
   RAFT_REQUIRE(((uintptr_t)pyramid & 15) == 0, "raft_corr_lookup: pyramid must be 16-byte aligned");
   RAFT_REQUIRE((long)B * H * W < (1L << 30), "raft_corr_lookup: more than 2^30 query pixels (split the batch)");
+  RAFT_REQUIRE((long)H * W * 16 * 4 < (1L << 31), "raft_corr_lookup: a per-pixel map exceeds 2 GiB");
   LookupArgs a;
   RAFT_REQUIRE(pyramid_levels(B, H, W, L, a.lv), "raft_corr_lookup: a pyramid level is empty");
   for (int l = L; l < LK_MAXL; ++l) a.lv[l] = a.lv[L - 1];
