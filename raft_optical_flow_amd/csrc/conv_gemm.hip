@@ -512,15 +512,19 @@ __global__ __launch_bounds__(256) void conv_smalln_kernel(ConvArgs a) {
 
 // Small-N 3x3 "same" convolution (the flow head's 256 -> 2 conv, core/update.py:6-16)
 // over 4x16 output tiles: one 512-thread work-group per tile; wave w owns the
-// input channels 32w + 256k, stages their 6x18 input patch in LDS as
-// [channel quad][patch pixel] (16-B elements: lane = output pixel reads
-// consecutive 16-B slots) and accumulates the 9 taps against wave-uniform
-// (scalar) weights; the 8 waves' partial sums meet in LDS in a fixed order.
+// input channels 32w + 256k.  Lane (q, pb) = (lane & 7, lane >> 3) holds the
+// weights of channel quad q for all 9 taps in registers (loaded with the
+// patch: one memory round trip, no scalar-load chain) and accumulates the 8
+// pixels of block pb (tile row pb/2, columns 8(pb%2) .. +7) over its 4
+// channels; the 6x18 input patch is staged in LDS as [channel quad][patch
+// pixel] (row stride padded to 109 pixels).  Partial sums meet through lane
+// shuffles (the 8 quads) and LDS (the 8 waves) in a fixed order.
 constexpr int SN_TH = 4, SN_TW = 16, SN_PH = SN_TH + 2, SN_PW = SN_TW + 2, SN_NP = SN_PH * SN_PW;
+constexpr int SN_QS = SN_NP + 1;  // patch stride per channel quad (f32x4 elements)
 
 template <int NOUT>
 __global__ __launch_bounds__(512) void conv_smalln3x3_kernel(ConvArgs a, const float* __restrict__ wt) {
-  __shared__ f32x4 patch[8][8][SN_NP];
+  __shared__ f32x4 patch[8][8 * SN_QS];
   __shared__ float red[8][NOUT][64];
   const raft_conv2d_params& p = a.p;
   const int lane = threadIdx.x & 63;
@@ -529,21 +533,31 @@ __global__ __launch_bounds__(512) void conv_smalln3x3_kernel(ConvArgs a, const f
   const int per = tx_n * ty_n;
   const int b = blockIdx.x / per, sr = blockIdx.x - b * per;
   const int y0 = (sr / tx_n) * SN_TH, x0 = (sr % tx_n) * SN_TW;
-  const int oy = lane >> 4, ox = lane & 15;
   const long pbase = (long)b * p.in_h * p.in_w;
-  float acc[NOUT];
+  const int q = lane & 7, pb = lane >> 3;
+  const int prow = pb >> 1, pcol = 8 * (pb & 1);  // the block's first output pixel in the tile
+  float acc[8][NOUT];
 #pragma unroll
-  for (int j = 0; j < NOUT; ++j) acc[j] = 0.f;
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NOUT; ++j) acc[i][j] = 0.f;
   for (int cg = 32 * w; cg < a.ctot; cg += 256) {
+    // weights of this lane's quad (zero-padded to cpad in the packed matrix)
+    f32x4 wr[9][NOUT];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int j = 0; j < NOUT; ++j)
+        wr[t][j] = *reinterpret_cast<const f32x4*>(wt + (long)j * a.K + t * a.cpad + cg + 4 * q);
     // stage: piece i = (patch pixel i >> 3, channel quad i & 7); zeros outside the image
     f32x4 v[(SN_NP * 8 + 63) / 64];
 #pragma unroll
     for (int k = 0; k < (SN_NP * 8 + 63) / 64; ++k) {
       const int i = lane + 64 * k;
-      const int pp = i >> 3, q = i & 7;
+      const int pp = i >> 3, qq = i & 7;
       const int py = pp / SN_PW, px = pp - py * SN_PW;
       const int iy = y0 + py - 1, ix = x0 + px - 1;
-      const int c = cg + 4 * q;
+      const int c = cg + 4 * qq;
       const bool ok = i < SN_NP * 8 && (unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w && c < a.ctot;
       const long pix = pbase + (long)(ok ? iy : 0) * p.in_w + (ok ? ix : 0);
       const float* src = c < p.in0_c ? p.in0 + pix * p.in0_ld + c : p.in1 + pix * p.in1_ld + (c - p.in0_c);
@@ -552,44 +566,56 @@ __global__ __launch_bounds__(512) void conv_smalln3x3_kernel(ConvArgs a, const f
 #pragma unroll
     for (int k = 0; k < (SN_NP * 8 + 63) / 64; ++k) {
       const int i = lane + 64 * k;
-      if (i < SN_NP * 8) patch[w][i & 7][i >> 3] = v[k];
+      if (i < SN_NP * 8) patch[w][(i & 7) * SN_QS + (i >> 3)] = v[k];
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const f32x4* pq = &patch[w][q * SN_QS];
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
+    for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int pp = (oy + ky) * SN_PW + ox + kx;
-        const float* wtap = wt + (ky * 3 + kx) * a.cpad + cg;
+      for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const f32x4 x = patch[w][q][pp];
+        for (int i = 0; i < 8; ++i) {
+          const f32x4 x = pq[(prow + ky) * SN_PW + pcol + i + kx];
 #pragma unroll
           for (int j = 0; j < NOUT; ++j) {
-            const float* wj = wtap + j * a.K + 4 * q;
-            acc[j] = fmaf(x[0], wj[0], acc[j]);
-            acc[j] = fmaf(x[1], wj[1], acc[j]);
-            acc[j] = fmaf(x[2], wj[2], acc[j]);
-            acc[j] = fmaf(x[3], wj[3], acc[j]);
+            const f32x4 wv = wr[ky * 3 + kx][j];
+            acc[i][j] = fmaf(x[0], wv[0], acc[i][j]);
+            acc[i][j] = fmaf(x[1], wv[1], acc[i][j]);
+            acc[i][j] = fmaf(x[2], wv[2], acc[i][j]);
+            acc[i][j] = fmaf(x[3], wv[3], acc[i][j]);
           }
         }
-      }
-    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+  // the 8 channel quads of a pixel block: lanes q = 0..7 (xor 1, 2, 4)
 #pragma unroll
-  for (int j = 0; j < NOUT; ++j) red[w][j][lane] = acc[j];
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NOUT; ++j) {
+      float t = acc[i][j];
+      t += __shfl_xor(t, 1);
+      t += __shfl_xor(t, 2);
+      t += __shfl_xor(t, 4);
+      acc[i][j] = t;
+    }
+  if (q == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < NOUT; ++j) red[w][j][prow * 16 + pcol + i] = acc[i][j];
+  }
   __syncthreads();
   if (threadIdx.x < 64 * NOUT) {
     const int j = threadIdx.x >> 6;
     float v = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) v += red[k][j][lane];
-    const int y = y0 + oy, x = x0 + ox;
+    const int y = y0 + (lane >> 4), x = x0 + (lane & 15);
     if (j < p.n && y < p.out_h && x < p.out_w)
       epilogue(p, ((long)b * p.out_h + y) * p.out_w + x, j, v + (p.bias ? p.bias[j] : 0.f));
   }
@@ -743,13 +769,10 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
   }
   hipStream_t s = as_stream(stream);
   if (p.n <= 4 && p.mode == RAFT_CONV_VEC) {
-    if (p.kh == 3 && p.kw == 3 && p.stride_h == 1 && p.stride_w == 1 && p.pad_h == 1 && p.pad_w == 1 &&
-        p.out_h == p.in_h && p.out_w == p.in_w) {
+    if (p.n <= 2 && p.kh == 3 && p.kw == 3 && p.stride_h == 1 && p.stride_w == 1 && p.pad_h == 1 &&
+        p.pad_w == 1 && p.out_h == p.in_h && p.out_w == p.in_w) {
       dim3 grid((unsigned)((long)p.batch * cdiv(p.out_h, SN_TH) * cdiv(p.out_w, SN_TW)));
-      if (p.n <= 2)
-        hipLaunchKernelGGL(conv_smalln3x3_kernel<2>, grid, dim3(512), 0, s, a, p.weight);
-      else
-        hipLaunchKernelGGL(conv_smalln3x3_kernel<4>, grid, dim3(512), 0, s, a, p.weight);
+      hipLaunchKernelGGL(conv_smalln3x3_kernel<2>, grid, dim3(512), 0, s, a, p.weight);
       return check_launch("raft_conv2d(small n 3x3)");
     }
     dim3 grid((unsigned)cdiv_l(a.M, 4));
