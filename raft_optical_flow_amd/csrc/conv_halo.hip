@@ -220,16 +220,39 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
   const int nk = a.nk, nch = a.nch;
   const int ns = (nk + U - 1) / U;
 
+  // Weight pieces of wave lw (a loader, or in the prologue the MFMA wave of the
+  // same index): NWP consecutive 8-row pieces of the block of K-step ew of
+  // every load set.
+  const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(p.weight, a.w_bytes);
+  const int ew = (lw * NWP) / NBI, wpc0 = (lw * NWP) % NBI;
+  unsigned wvoff[NWP];
+#pragma unroll
+  for (int k = 0; k < NWP; ++k) {
+    const int r = 8 * (wpc0 + k) + (lane >> 3);
+    const int qd = (lane & 7) ^ ((r >> 1) & 7);
+    wvoff[k] = (unsigned)(n0 + r) * ((unsigned)a.K * 4u) + (unsigned)qd * 16u;
+  }
+  auto issue_weights = [&](int u) {
+    const int j = U * u + ew;
+    const bool in = j < nk;
+    const int c = j / T, t = j - c * T;
+    const unsigned soff = in ? (unsigned)(t * nch + c) * 128u : 0u;  // packed K-step (tap, chunk)
+    char* dst = smem + (U * (u % (D + 1)) + ew) * (BNT * 128) + wpc0 * 1024;
+#pragma unroll
+    for (int k = 0; k < NWP; ++k) dma16(rs_w, dst + k * 1024, in ? wvoff[k] : OFF_INVALID, soff);
+  };
+
   if (loader) {
     // ---- loader waves ------------------------------------------------------
-    const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(p.weight, a.w_bytes);
+    // (the weights of the prologue's load sets 0 .. D-1 are issued by the MFMA
+    // waves, which have nothing else to do then: an LDS-DMA costs its issuing
+    // wave 100+ cycles, so the prologue's issue is split over eight waves)
     const __amdgpu_buffer_rsrc_t rs0 = make_rsrc(p.in0, a.in0_bytes);
     const __amdgpu_buffer_rsrc_t rs1 = make_rsrc(p.in1_c ? p.in1 : p.in0, p.in1_c ? a.in1_bytes : a.in0_bytes);
     const int in0_c = p.in0_c, in1_c = p.in1_c;
     const unsigned ld0 = p.in0_ld, ld1 = p.in1_c ? p.in1_ld : p.in0_ld;
     const int in_h = p.in_h, in_w = p.in_w;
     const unsigned pb = (unsigned)b * (unsigned)(in_h * in_w);
-    const unsigned wrow = (unsigned)a.K * 4u;
     // Patch pieces of this loader: i = lw, lw+4, ... (< PI), pixels 8i .. 8i+7.
     // Everything per lane is fixed by the tile, so the DMA addresses are
     // precomputed once; per chunk only the channel offset changes.
@@ -262,38 +285,24 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
         }
       }
     };
-    // Weight pieces of this loader: NWP consecutive 8-row pieces of the block
-    // of K-step ew of every load set.
-    const int ew = (lw * NWP) / NBI, wpc0 = (lw * NWP) % NBI;
-    unsigned wvoff[NWP];
-#pragma unroll
-    for (int k = 0; k < NWP; ++k) {
-      const int r = 8 * (wpc0 + k) + (lane >> 3);
-      const int qd = (lane & 7) ^ ((r >> 1) & 7);
-      wvoff[k] = (unsigned)(n0 + r) * wrow + (unsigned)qd * 16u;
-    }
     // load set u; returns this wave's DMA count
-    auto issue_set = [&](int u) -> int {
-      {
-        const int j = U * u + ew;
-        const bool in = j < nk;
-        const int c = j / T, t = j - c * T;
-        const unsigned soff = in ? (unsigned)(t * nch + c) * 128u : 0u;  // packed K-step (tap, chunk)
-        char* dst = smem + (U * (u % (D + 1)) + ew) * (BNT * 128) + wpc0 * 1024;
-#pragma unroll
-        for (int k = 0; k < NWP; ++k) dma16(rs_w, dst + k * 1024, in ? wvoff[k] : OFF_INVALID, soff);
+    auto issue_set = [&](int u, bool weights) -> int {
+      int n = 0;
+      if (weights) {
+        issue_weights(u);
+        n = NWP;
       }
       if constexpr (T == 1) {
 #pragma unroll
         for (int e = 0; e < U; ++e) issue_patch(U * u + e);
-        return NWP + U * pcw;
+        return n + U * pcw;
       } else {
         const int c = (U * u + T - 1) / T;  // the chunk starting in this set, if any (zeros past nch)
         if (c * T < U * u + U) {
           issue_patch(c);
-          return NWP + pcw;
+          return n + pcw;
         }
-        return NWP;
+        return n;
       }
     };
     if constexpr (LSPLIT) {
@@ -343,15 +352,6 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
           }
         }
       };
-      auto issue_weights = [&](int u) {
-        const int j = U * u + ew;
-        const bool in = j < nk;
-        const int c = j / T, t = j - c * T;
-        const unsigned soff = in ? (unsigned)(t * nch + c) * 128u : 0u;
-        char* dst = smem + (U * (u % (D + 1)) + ew) * (BNT * 128) + wpc0 * 1024;
-#pragma unroll
-        for (int k = 0; k < NWP; ++k) dma16(rs_w, dst + k * 1024, in ? wvoff[k] : OFF_INVALID, soff);
-      };
       // the chunk starting in load set u, or -1 (at most one: T >= U)
       auto chunk_of = [&](int u) {
         const int c = (U * u + T - 1) / T;
@@ -373,7 +373,6 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
             }
           ++nst;
         }
-        issue_weights(u);
       }
       wait_vm<0>();
 #pragma unroll
@@ -417,7 +416,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
     {
       int cnt[D];
 #pragma unroll
-      for (int u = 0; u < D; ++u) cnt[u] = issue_set(u);
+      for (int u = 0; u < D; ++u) cnt[u] = issue_set(u, false);
       int n = 0;
 #pragma unroll
       for (int u = 2; u < D; ++u) n += cnt[u];
@@ -427,7 +426,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
     }
     __builtin_amdgcn_s_barrier();
     for (int s = 0; s < ns; ++s) {
-      const int nnew = s + D < ns ? issue_set(s + D) : 0;
+      const int nnew = s + D < ns ? issue_set(s + D, true) : 0;
       int n = D >= 3 ? nnew : 0;  // in flight after set s+2: sets s+3 .. s+D
 #pragma unroll
       for (int k = 0; k < D - 3; ++k) n += hist[k];
@@ -548,6 +547,9 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
   // all in load sets s and s+1), then one barrier.  K-steps past nk (up to
   // U*ns) run on zero weights and zero patches: they add exact zeros, and the
   // loop body has no branches.
+#pragma unroll
+  for (int u = 0; u < D; ++u) issue_weights(u);
+  wait_vm<NWP * (D - 2)>();      // the weights of sets 0 and 1 (sets 2 .. D-1: before the first loop barrier)
   __builtin_amdgcn_s_barrier();  // load sets 0 and 1 have landed
 #ifdef HALO_PRIO
   __builtin_amdgcn_s_setprio(HALO_PRIO);
@@ -590,6 +592,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
     t_cmp += t2 - t0;
 #endif
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the next fragments are in registers
+    if (s == 0) wait_vm<0>();             // the prologue's weight sets 2 .. D-1 (this wave's only VMEM)
 #ifdef STAMPS
     unsigned long long t3 = hstamp_now();
     t_wait += t3 - t2;
