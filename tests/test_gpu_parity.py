@@ -127,6 +127,24 @@ def test_lookup_far_out_of_bounds_and_large_coords():
     assert maxabs(cb(t(coords)), ref) < 2e-5
 
 
+@pytest.mark.parametrize("B,h,w", [(32, 16, 20), (33, 17, 21)])
+def test_lookup_pipelined_grid_vs_oracle(B, h, w):
+    """Batches past one resident wave of the one-shot lookup (> 8 blocks per CU) run the
+    pipelined kernel (corr_lookup_pipe_kernel: waves walk several pixels, the next pixel's
+    tiles in flight); ragged pixel count, coords spread over and beyond the maps."""
+    from raft_optical_flow_amd import CorrBlock
+    rng = np.random.default_rng(7)
+    f1 = rng.standard_normal((B, 32, h, w)).astype(np.float32)
+    f2 = rng.standard_normal((B, 32, h, w)).astype(np.float32)
+    ys, xs = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    grid = np.stack([xs, ys])[None].astype(np.float32)
+    coords = (grid + rng.normal(0, 3.0, (B, 2, h, w))).astype(np.float32)
+    coords[B - 1] = rng.uniform(-40, 60, (2, h, w)).astype(np.float32)
+    cb = CorrBlock(t(f1), t(f2), num_levels=4, radius=4)
+    ref = O.corr_lookup(O.corr_pyramid(f1, f2, 4), coords, 4)
+    assert maxabs(cb(t(coords)), ref) < 2e-5
+
+
 @pytest.mark.parametrize("n", [1, 2])
 def test_alt_cuda_corr_forward_vs_oracle(n):
     from raft_optical_flow_amd import alt_cuda_corr
