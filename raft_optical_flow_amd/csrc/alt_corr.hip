@@ -12,8 +12,10 @@ namespace {
 // 4 channels per lane per 256-channel slab.  The (2r+2)^2 integer taps
 // around floor(coords) - r are visited 64 at a time: every lane reads the
 // tap's fmap2 row slice (one coalesced 1 KiB read per tap per slab) and keeps
-// a private partial dot product per tap; a transposing butterfly (halving
-// exchange, 63 shuffles per 64 taps) leaves lane j holding tap j's full sum.
+// a private partial dot product per tap; per batch of 8 taps a transposing
+// butterfly (7 shuffles) and 3 lane-group butterflies leave lane j holding tap
+// j's full sum.  The tap loads are branch-free buffer loads (out-of-map taps
+// read zeros), issued a batch ahead of the products.
 // Tap sums go to LDS and the bilinear weights of frac(coords) scatter them
 // into the (2r+1)^2 bins exactly as the reference (bins gathered per lane).
 // ============================================================================
@@ -32,24 +34,43 @@ struct AltArgs {
   int flow_ld;
 };
 
+// Partial dot product of one tap: this lane's channel quads of fmap1[p] (registers)
+// and of the tap's fmap2 row, read through a raw buffer over the batch's fmap2.
+// An out-of-map (or beyond-C) read passes an out-of-range offset and returns
+// zeros without a memory access, so every tap's load is issued unconditionally
+// (no exec-masked branch per tap: the loads of a tap group go out back to back
+// instead of one L2 round trip per tap).
+// One tap's fmap2 row slice for this lane's channel quads, read through a raw
+// buffer over the batch's fmap2.  An out-of-map (or beyond-C) read passes an
+// out-of-range offset and returns zeros without a memory access, so every
+// tap's load is issued unconditionally — no exec-masked branch per tap, and
+// a batch of taps goes out back to back instead of one L2 round trip per tap.
 template <int NV>
-__device__ __forceinline__ float tap_partial(const f32x4 (&f1)[NV], const float* row, int lane, int C) {
-  float s = 0.f;
+__device__ __forceinline__ void tap_load(f32x4 (&d)[NV], __amdgpu_buffer_rsrc_t rs, bool in, int row_off, int lane,
+                                         int C) {
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int c = k * 256 + lane * 4;
-    if (c < C) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(row + c);
-      s += f1[k][0] * v[0] + f1[k][1] * v[1] + f1[k][2] * v[2] + f1[k][3] * v[3];
-    }
+    const unsigned off = (in && c < C) ? (unsigned)(row_off + c) * 4u : 0x80000000u;
+    d[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
   }
+}
+
+template <int NV>
+__device__ __forceinline__ float tap_dot(const f32x4 (&f1)[NV], const f32x4 (&d)[NV]) {
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) s += f1[k][0] * d[k][0] + f1[k][1] * d[k][1] + f1[k][2] * d[k][2] + f1[k][3] * d[k][3];
   return s;
 }
 
-// Reduce v[0..63] (one partial per tap, per lane) so that lane j ends with sum over lanes of v[j].
-__device__ __forceinline__ float transpose_reduce64(float (&v)[64], int lane) {
+// Reduce v[0..N-1] (one partial per tap, per lane) so that lane l ends with the
+// sum over its N-lane group (lanes sharing l / N) of v[l % N]: log2(N) halving
+// exchanges, N - 1 shuffles.
+template <int N>
+__device__ __forceinline__ float transpose_reduce(float (&v)[N], int lane) {
 #pragma unroll
-  for (int half = 32; half >= 1; half >>= 1) {
+  for (int half = N / 2; half >= 1; half >>= 1) {
     const bool hi = (lane & half) != 0;
 #pragma unroll
     for (int i = 0; i < half; ++i) {
@@ -61,8 +82,19 @@ __device__ __forceinline__ float transpose_reduce64(float (&v)[64], int lane) {
   return v[0];
 }
 
+// waves per SIMD the forward kernel is compiled for at C <= 256 (8 / NV above; register budget: its tap
+// group's loads all in flight vs more waves); dev builds may override it
+#ifndef ALT_WAVES
+#define ALT_WAVES 8
+#endif
+#ifndef ALT_PF  // 1: the next batch's loads go out before this batch's products
+#define ALT_PF 1
+#endif
+#ifndef ALT_TB  // taps per load batch
+#define ALT_TB 2
+#endif
 template <int NV>
-__global__ __launch_bounds__(256) void alt_corr_kernel(AltArgs a) {
+__global__ __launch_bounds__(256, NV == 1 ? ALT_WAVES : 8 / NV) void alt_corr_kernel(AltArgs a) {
   __shared__ float tapsum[4][128];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -98,20 +130,60 @@ __global__ __launch_bounds__(256) void alt_corr_kernel(AltArgs a) {
     f1[k] = (valid && c < a.C) ? *reinterpret_cast<const f32x4*>(f1row + c) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   const float* f2b = a.f2 + (long)b * a.H2 * a.W2 * a.C;
+  // < 2 GiB per batch item (host-checked)
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(f2b), (short)0, (int)((long)a.H2 * a.W2 * a.C * 4), 0x00020000);
+  // the window origin is the wave's (one pixel per wave): scalar tap geometry
+  const int sx0 = __builtin_amdgcn_readfirstlane(x0), sy0 = __builtin_amdgcn_readfirstlane(y0);
+  // taps in batches of TB: batch k + 1's loads are issued before batch k's
+  // products, so each wave keeps 2 x TB tap rows in flight
+  constexpr int TB = ALT_TB;
+  auto tap_in = [&](int t, int& row_off) {
+    const int iy = t / wd, ix = t - iy * wd;
+    const int h2 = sy0 + iy, w2 = sx0 + ix;
+    row_off = (h2 * a.W2 + w2) * a.C;
+    return valid && t < ntaps && (unsigned)h2 < (unsigned)a.H2 && (unsigned)w2 < (unsigned)a.W2;
+  };
   for (int g = 0; g < ntaps; g += 64) {
-    float v[64];
+    f32x4 buf[ALT_PF ? 2 : 1][TB][NV];
 #pragma unroll
-    for (int j = 0; j < 64; ++j) {
-      const int t = g + j;
-      const int iy = t / wd, ix = t - iy * wd;
-      const int h2 = y0 + iy, w2 = x0 + ix;
-      float s = 0.f;
-      if (valid && t < ntaps && h2 >= 0 && h2 < a.H2 && w2 >= 0 && w2 < a.W2)
-        s = tap_partial<NV>(f1, f2b + ((long)h2 * a.W2 + w2) * a.C, lane, a.C);
-      v[j] = s;
+    for (int j = 0; j < TB; ++j) {
+      int ro;
+      const bool in = tap_in(g + j, ro);
+      tap_load<NV>(buf[0][j], rs, in, ro, lane, a.C);
     }
-    const float tot = transpose_reduce64(v, lane);
-    if (g + lane < ntaps) tapsum[wv][g + lane] = tot;
+#pragma unroll
+    for (int jb = 0; jb < 64; jb += TB) {
+      if (g + jb >= ntaps) break;  // wave-uniform
+      const int cur = ALT_PF ? (jb / TB) & 1 : 0;
+      if (!ALT_PF && jb > 0) {
+#pragma unroll
+        for (int j = 0; j < TB; ++j) {
+          int ro;
+          const bool in = tap_in(g + jb + j, ro);
+          tap_load<NV>(buf[0][j], rs, in, ro, lane, a.C);
+        }
+      }
+      if (ALT_PF && jb + TB < 64) {
+#pragma unroll
+        for (int j = 0; j < TB; ++j) {
+          int ro;
+          const bool in = tap_in(g + jb + TB + j, ro);
+          tap_load<NV>(buf[ALT_PF ? cur ^ 1 : 0][j], rs, in, ro, lane, a.C);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      float v[TB];
+#pragma unroll
+      for (int j = 0; j < TB; ++j) v[j] = tap_dot<NV>(f1, buf[cur][j]);
+      // lane l ends with the full sum of tap jb + (l % TB): a transposing
+      // butterfly over the batch, then a plain one over the lane groups
+      float tot = transpose_reduce<TB>(v, lane);
+#pragma unroll
+      for (int m = TB; m < 64; m <<= 1) tot += __shfl_xor(tot, m);
+      if (lane < TB && g + jb + lane < ntaps) tapsum[wv][g + jb + lane] = tot;
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
   __syncthreads();
   if (!valid) return;
@@ -234,6 +306,7 @@ static int alt_checks(const float* f1, const float* f2, const float* coords, con
   RAFT_REQUIRE(C % 4 == 0 && C <= 1024, "raft_alt_corr: C must be a multiple of 4 and <= 1024 (got %d)", C);
   RAFT_REQUIRE(r >= 0 && (2 * r + 2) * (2 * r + 2) <= 128, "raft_alt_corr: radius must be 0..4 (got %d)", r);
   RAFT_REQUIRE((((uintptr_t)f1 | (uintptr_t)f2) & 15) == 0, "raft_alt_corr: fmaps must be 16-byte aligned");
+  RAFT_REQUIRE((long)H2 * W2 * C * 4 < (1L << 31), "raft_alt_corr: one fmap2 exceeds 2 GiB");
   return 0;
 }
 

@@ -129,9 +129,8 @@ def test_lookup_far_out_of_bounds_and_large_coords():
 
 @pytest.mark.parametrize("B,h,w", [(32, 16, 20), (33, 17, 21)])
 def test_lookup_pipelined_grid_vs_oracle(B, h, w):
-    """Batches past one resident wave of the one-shot lookup (> 8 blocks per CU) run the
-    pipelined kernel (corr_lookup_pipe_kernel: waves walk several pixels, the next pixel's
-    tiles in flight); ragged pixel count, coords spread over and beyond the maps."""
+    """Batches past one resident grid of the lookup (> 8 blocks per CU), a ragged pixel
+    count, coords spread over and beyond the maps."""
     from raft_optical_flow_amd import CorrBlock
     rng = np.random.default_rng(7)
     f1 = rng.standard_normal((B, 32, h, w)).astype(np.float32)
@@ -146,10 +145,12 @@ def test_lookup_pipelined_grid_vs_oracle(B, h, w):
 
 
 @pytest.mark.parametrize("n", [1, 2])
-def test_alt_cuda_corr_forward_vs_oracle(n):
+@pytest.mark.parametrize("C", [96, 260])
+def test_alt_cuda_corr_forward_vs_oracle(n, C):
+    """C = 96: a partial 256-channel slab; C = 260: two slabs (NV = 2), the second a single quad."""
     from raft_optical_flow_amd import alt_cuda_corr
     rng = np.random.default_rng(2)
-    B, H1, W1, H2, W2, C, r = 2, 9, 13, 5, 7, 96, 4
+    B, H1, W1, H2, W2, r = 2, 9, 13, 5, 7, 4
     f1 = rng.standard_normal((B, H1, W1, C)).astype(np.float32)
     f2 = rng.standard_normal((B, H2, W2, C)).astype(np.float32)
     coords = rng.uniform(-4, 12, (B, n, H1, W1, 2)).astype(np.float32)
