@@ -511,19 +511,31 @@ __global__ __launch_bounds__(256) void conv_smalln_kernel(ConvArgs a) {
 }
 
 // Small-N 3x3 "same" convolution (the flow head's 256 -> 2 conv, core/update.py:6-16)
-// over 4x16 output tiles: one 512-thread work-group per tile; wave w owns the
+// over TH x 16 output tiles (4x16, or 2x16 when 4x16 tiles would leave CUs
+// idle: config 2 at B = 1 has 110): one 512-thread work-group per tile; wave w owns the
 // input channels 32w + 256k.  Lane (q, pb) = (lane & 7, lane >> 3) holds the
 // weights of channel quad q for all 9 taps in registers (loaded with the
-// patch: one memory round trip, no scalar-load chain) and accumulates the 8
-// pixels of block pb (tile row pb/2, columns 8(pb%2) .. +7) over its 4
-// channels; the 6x18 input patch is staged in LDS as [channel quad][patch
+// patch: one memory round trip, no scalar-load chain) and accumulates the
+// TH*2 pixels of block pb (4x16: tile row pb/2, columns 8(pb%2) .. +7) over its
+// 4 channels; the (TH+2)x18 input patch is staged in LDS as [channel quad][patch
 // pixel] (row stride padded to 109 pixels).  Partial sums meet through lane
 // shuffles (the 8 quads) and LDS (the 8 waves) in a fixed order.
-constexpr int SN_TH = 4, SN_TW = 16, SN_PH = SN_TH + 2, SN_PW = SN_TW + 2, SN_NP = SN_PH * SN_PW;
-constexpr int SN_QS = SN_NP + 1;  // patch stride per channel quad (f32x4 elements)
+#ifndef SN_TH4_MIN_TILES  // dev builds: 0 = always 4x16 tiles
+#define SN_TH4_MIN_TILES 512
+#endif
+// TH x 16 output tiles (TH = 4 or 2); SN_PXB = TH*16/8 pixels per lane block
+template <int TH>
+struct SnGeom {
+  static constexpr int TW = 16, PH = TH + 2, PW = TW + 2, NP = PH * PW;
+  static constexpr int QS = NP + 1;        // patch stride per channel quad (f32x4 elements)
+  static constexpr int PXB = TH * TW / 8;  // pixels per lane block
+  static constexpr int BPR = TW / PXB;     // lane blocks per tile row
+};
 
-template <int NOUT>
+template <int NOUT, int TH>
 __global__ __launch_bounds__(512) void conv_smalln3x3_kernel(ConvArgs a, const float* __restrict__ wt) {
+  using G = SnGeom<TH>;
+  constexpr int SN_TH = TH, SN_TW = G::TW, SN_PW = G::PW, SN_NP = G::NP, SN_QS = G::QS, PXB = G::PXB;
   __shared__ f32x4 patch[8][8 * SN_QS];
   __shared__ float red[8][NOUT][64];
   const raft_conv2d_params& p = a.p;
@@ -535,10 +547,10 @@ __global__ __launch_bounds__(512) void conv_smalln3x3_kernel(ConvArgs a, const f
   const int y0 = (sr / tx_n) * SN_TH, x0 = (sr % tx_n) * SN_TW;
   const long pbase = (long)b * p.in_h * p.in_w;
   const int q = lane & 7, pb = lane >> 3;
-  const int prow = pb >> 1, pcol = 8 * (pb & 1);  // the block's first output pixel in the tile
-  float acc[8][NOUT];
+  const int prow = pb / G::BPR, pcol = PXB * (pb % G::BPR);  // the block's first output pixel in the tile
+  float acc[PXB][NOUT];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < PXB; ++i)
 #pragma unroll
     for (int j = 0; j < NOUT; ++j) acc[i][j] = 0.f;
   for (int cg = 32 * w; cg < a.ctot; cg += 256) {
@@ -577,7 +589,7 @@ __global__ __launch_bounds__(512) void conv_smalln3x3_kernel(ConvArgs a, const f
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < PXB; ++i) {
           const f32x4 x = pq[(prow + ky) * SN_PW + pcol + i + kx];
 #pragma unroll
           for (int j = 0; j < NOUT; ++j) {
@@ -594,7 +606,7 @@ __global__ __launch_bounds__(512) void conv_smalln3x3_kernel(ConvArgs a, const f
   }
   // the 8 channel quads of a pixel block: lanes q = 0..7 (xor 1, 2, 4)
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < PXB; ++i)
 #pragma unroll
     for (int j = 0; j < NOUT; ++j) {
       float t = acc[i][j];
@@ -605,9 +617,9 @@ __global__ __launch_bounds__(512) void conv_smalln3x3_kernel(ConvArgs a, const f
     }
   if (q == 0) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < PXB; ++i)
 #pragma unroll
-      for (int j = 0; j < NOUT; ++j) red[w][j][prow * 16 + pcol + i] = acc[i][j];
+      for (int j = 0; j < NOUT; ++j) red[w][j][prow * SN_TW + pcol + i] = acc[i][j];
   }
   __syncthreads();
   if (threadIdx.x < 64 * NOUT) {
@@ -616,7 +628,7 @@ __global__ __launch_bounds__(512) void conv_smalln3x3_kernel(ConvArgs a, const f
 #pragma unroll
     for (int k = 0; k < 8; ++k) v += red[k][j][lane];
     const int y = y0 + (lane >> 4), x = x0 + (lane & 15);
-    if (j < p.n && y < p.out_h && x < p.out_w)
+    if (j < p.n && lane < SN_TH * SN_TW && y < p.out_h && x < p.out_w)
       epilogue(p, ((long)b * p.out_h + y) * p.out_w + x, j, v + (p.bias ? p.bias[j] : 0.f));
   }
 }
@@ -771,8 +783,14 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
   if (p.n <= 4 && p.mode == RAFT_CONV_VEC) {
     if (p.n <= 2 && p.kh == 3 && p.kw == 3 && p.stride_h == 1 && p.stride_w == 1 && p.pad_h == 1 &&
         p.pad_w == 1 && p.out_h == p.in_h && p.out_w == p.in_w) {
-      dim3 grid((unsigned)((long)p.batch * cdiv(p.out_h, SN_TH) * cdiv(p.out_w, SN_TW)));
-      hipLaunchKernelGGL(conv_smalln3x3_kernel<2>, grid, dim3(512), 0, s, a, p.weight);
+      // 4x16 tiles while they fill the CUs; 2x16 (twice the work-groups) when not
+      const long t4 = (long)p.batch * cdiv(p.out_h, 4) * cdiv(p.out_w, 16);
+      if (t4 >= SN_TH4_MIN_TILES) {
+        hipLaunchKernelGGL((conv_smalln3x3_kernel<2, 4>), dim3((unsigned)t4), dim3(512), 0, s, a, p.weight);
+      } else {
+        const long t2 = (long)p.batch * cdiv(p.out_h, 2) * cdiv(p.out_w, 16);
+        hipLaunchKernelGGL((conv_smalln3x3_kernel<2, 2>), dim3((unsigned)t2), dim3(512), 0, s, a, p.weight);
+      }
       return check_launch("raft_conv2d(small n 3x3)");
     }
     dim3 grid((unsigned)cdiv_l(a.M, 4));
