@@ -93,14 +93,11 @@ __device__ __forceinline__ float transpose_reduce(float (&v)[N], int lane) {
 #ifndef ALT_TB  // taps per load batch
 #define ALT_TB 2
 #endif
+// One query pixel gid = (b*N + n)*P1 + p by one wave (ts: the wave's 128-float
+// LDS row of tap sums).
 template <int NV>
-__global__ __launch_bounds__(256, NV == 1 ? ALT_WAVES : 8 / NV) void alt_corr_kernel(AltArgs a) {
-  __shared__ float tapsum[4][128];
-  const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
+__device__ __forceinline__ void alt_pixel(const AltArgs& a, long gid, bool valid, int lane, float* ts) {
   const int P1 = a.H1 * a.W1;
-  const long gid = (long)blockIdx.x * 4 + wv;  // ((b*N + n)*P1 + p)
-  const bool valid = gid < (long)a.B * a.N * P1;
   const long bn = valid ? gid / P1 : 0;
   const int p = valid ? (int)(gid - bn * P1) : 0;
   const int b = (int)(bn / a.N);
@@ -181,15 +178,16 @@ __global__ __launch_bounds__(256, NV == 1 ? ALT_WAVES : 8 / NV) void alt_corr_ke
       float tot = transpose_reduce<TB>(v, lane);
 #pragma unroll
       for (int m = TB; m < 64; m <<= 1) tot += __shfl_xor(tot, m);
-      if (lane < TB && g + jb + lane < ntaps) tapsum[wv][g + jb + lane] = tot;
+      if (lane < TB && g + jb + lane < ntaps) ts[g + jb + lane] = tot;
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (!valid) return;
   for (int o = lane; o < rd * rd; o += 64) {
     const int ox = o / rd, oy = o - ox * rd;  // channel = oy + rd*ox
-    const float* ts = tapsum[wv];
     const float s00 = ts[oy * wd + ox], s01 = ts[oy * wd + ox + 1];
     const float s10 = ts[(oy + 1) * wd + ox], s11 = ts[(oy + 1) * wd + ox + 1];
     float val = s00 * ((1.f - dy) * (1.f - dx));
@@ -208,10 +206,199 @@ __global__ __launch_bounds__(256, NV == 1 ? ALT_WAVES : 8 / NV) void alt_corr_ke
   }
 }
 
+
+template <int NV>
+__global__ __launch_bounds__(256, NV == 1 ? ALT_WAVES : 8 / NV) void alt_corr_kernel(AltArgs a) {
+  __shared__ float tapsum[4][128];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const long gid = (long)blockIdx.x * 4 + wv;  // ((b*N + n)*P1 + p)
+  alt_pixel<NV>(a, gid, gid < (long)a.B * a.N * a.H1 * a.W1, lane, tapsum[wv]);
+}
+
+// ============================================================================
+// K3t: tiled on-the-fly correlation (the same forward, correlation_kernel.cu:18-119).
+//
+// One 256-thread work-group per 8x8 tile of query pixels and coordinate set.
+// Neighbouring pixels' (2r+2)^2 windows overlap, so the union of the tile's
+// windows (its bounding box, <= ATB x ATB fmap2 pixels) is staged in LDS one
+// ACC-channel chunk at a time and every (pixel, tap) dot product reads it from
+// there: fmap2 crosses L2 once per tile instead of once per pixel and tap
+// (the per-pixel kernel above moves 100 KiB per pixel and level).  Thread
+// (g, q) = (wave, lane) accumulates taps g, g + 4, ... of tile pixel q; its
+// fmap1 chunk sits in registers.  A tile whose box does not fit (large flow
+// divergence, non-finite coords) is finished per pixel by its waves
+// (alt_pixel, the per-pixel kernel's body).  Bilinear binning and the output layouts are those of
+// alt_corr_kernel.
+// ============================================================================
+constexpr int AT = 8;     // tile side (query pixels)
+constexpr int ACC = 16;   // channels per staged chunk
+constexpr int ATB = 24;   // max bounding-box side (fmap2 pixels)
+
+// bilinear binning of one pixel's tap sums ts[(2r+2)^2] into output channel o
+__device__ __forceinline__ void alt_bin_store(const AltArgs& a, long bn, int p, float x, float y, const float* ts,
+                                              int o) {
+  const int P1 = a.H1 * a.W1;
+  const int b = (int)(bn / a.N);
+  const int rd = 2 * a.r + 1, wd = 2 * a.r + 2;
+  const float fx = floorf(x), fy = floorf(y);
+  const float dx = x - fx, dy = y - fy;
+  const int ox = o / rd, oy = o - ox * rd;  // channel = oy + rd*ox
+  const float s00 = ts[oy * wd + ox], s01 = ts[oy * wd + ox + 1];
+  const float s10 = ts[(oy + 1) * wd + ox], s11 = ts[(oy + 1) * wd + ox + 1];
+  float val = s00 * ((1.f - dy) * (1.f - dx));
+  val += s01 * ((1.f - dy) * dx);
+  val += s10 * (dy * (1.f - dx));
+  val += s11 * (dy * dx);
+  val = val / a.scale_div;
+  if (a.out_layout == 0)
+    a.out[(bn * (rd * rd) + o) * P1 + p] = val;
+  else
+    a.out[((long)b * P1 + p) * a.out_ld + o] = val;
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void alt_corr_tile_kernel(AltArgs a) {
+  constexpr int WD = 2 * R + 2, NT = WD * WD, RD = 2 * R + 1;
+  constexpr int TPT = (NT + 3) / 4;  // taps per thread
+  constexpr int SROW = ACC + 4;      // staged floats per box pixel (16-B pad against bank conflicts)
+  __shared__ __attribute__((aligned(16))) float st[ATB * ATB * SROW > AT * AT * (NT + 1) ? ATB * ATB * SROW
+                                                                                       : AT * AT * (NT + 1)];
+  const int lane = threadIdx.x & 63;
+  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int P1 = a.H1 * a.W1;
+  const int tiles_x = (a.W1 + AT - 1) / AT, tiles_y = (a.H1 + AT - 1) / AT;
+  const int per = tiles_x * tiles_y;
+  const long bn = blockIdx.x / per;
+  const int tr = (int)(blockIdx.x - bn * per);
+  const int b = (int)(bn / a.N);
+  const int qy = (tr / tiles_x) * AT + (lane >> 3), qx = (tr % tiles_x) * AT + (lane & 7);
+  const bool valid = qy < a.H1 && qx < a.W1;
+  const int p = valid ? qy * a.W1 + qx : 0;
+  const long gid = bn * P1 + p;
+
+  float x = 0.f, y = 0.f;
+  if (valid) {
+    if (a.coords_layout == 0) {
+      x = a.coords[2 * gid];
+      y = a.coords[2 * gid + 1];
+    } else {
+      x = a.coords[((long)b * 2) * P1 + p];
+      y = a.coords[((long)b * 2 + 1) * P1 + p];
+    }
+    x = x / a.coord_div;
+    y = y / a.coord_div;
+  }
+  const bool fin = isfinite(x) && isfinite(y) && fabsf(x) < 1e8f && fabsf(y) < 1e8f;
+  const int x0 = fin ? (int)floorf(x) - R : 0, y0 = fin ? (int)floorf(y) - R : 0;
+  // the tile's window box (every wave computes the same one)
+  int mnx = valid ? x0 : (1 << 30), mny = valid ? y0 : (1 << 30);
+  int mxx = valid ? x0 : -(1 << 30), mxy = valid ? y0 : -(1 << 30);
+  int bad = valid && !fin;
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    mnx = min(mnx, __shfl_xor(mnx, m));
+    mny = min(mny, __shfl_xor(mny, m));
+    mxx = max(mxx, __shfl_xor(mxx, m));
+    mxy = max(mxy, __shfl_xor(mxy, m));
+    bad |= __shfl_xor(bad, m);
+  }
+  const int bx0 = __builtin_amdgcn_readfirstlane(mnx), by0 = __builtin_amdgcn_readfirstlane(mny);
+  const int bw = __builtin_amdgcn_readfirstlane(mxx) - bx0 + WD, bh = __builtin_amdgcn_readfirstlane(mxy) - by0 + WD;
+  const bool fits = !__builtin_amdgcn_readfirstlane(bad) && bw <= ATB && bh <= ATB;
+
+  if (!fits) {
+    // wave g finishes pixels 16g .. 16g + 15 of the tile one at a time (per-pixel path)
+    for (int i = 0; i < 16; ++i) {
+      const int q = 16 * g + i;
+      const int pq = __shfl(p, q), vq = __shfl((int)valid, q);
+      alt_pixel<1>(a, bn * P1 + pq, vq != 0, lane, st + g * 128);
+    }
+    return;
+  }
+
+  // box-relative window origin of this thread's pixel
+  const int ox0 = valid ? x0 - bx0 : 0, oy0 = valid ? y0 - by0 : 0;
+  const float* f2b = a.f2 + (long)b * a.H2 * a.W2 * a.C;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(f2b), (short)0, (int)((long)a.H2 * a.W2 * a.C * 4), 0x00020000);
+  const float* f1row = a.f1 + ((long)b * P1 + p) * a.C;
+  float acc[TPT];
+#pragma unroll
+  for (int j = 0; j < TPT; ++j) acc[j] = 0.f;
+  constexpr int PIECES = ATB * ATB * (ACC / 4);  // 16-B pieces of a full box chunk
+  const int npieces = bw * bh * (ACC / 4);
+  for (int c0 = 0; c0 < a.C; c0 += ACC) {
+    // stage the box's chunk: piece i = (box pixel i / (ACC/4), quad i % (ACC/4)); zeros off the map
+    f32x4 v[(PIECES + 255) / 256];
+#pragma unroll
+    for (int k = 0; k < (PIECES + 255) / 256; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      const int bp = i / (ACC / 4), qd = i % (ACC / 4);
+      const int yy = bp / bw, xx = bp - (bp / bw) * bw;
+      const int h2 = by0 + yy, w2 = bx0 + xx;
+      const bool in = i < npieces && (unsigned)h2 < (unsigned)a.H2 && (unsigned)w2 < (unsigned)a.W2;
+      const unsigned off = in ? (unsigned)((h2 * a.W2 + w2) * a.C + c0 + 4 * qd) * 4u : 0x80000000u;
+      v[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    }
+    f32x4 f1c[ACC / 4];
+#pragma unroll
+    for (int k = 0; k < ACC / 4; ++k) f1c[k] = *reinterpret_cast<const f32x4*>(f1row + c0 + 4 * k);
+    __syncthreads();  // the previous chunk's reads are done
+#pragma unroll
+    for (int k = 0; k < (PIECES + 255) / 256; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      if (i < npieces) {
+        const int bp = i / (ACC / 4), qd = i % (ACC / 4);
+        const int yy = bp / bw, xx = bp - (bp / bw) * bw;
+        *reinterpret_cast<f32x4*>(&st[(yy * ATB + xx) * SROW + 4 * qd]) = v[k];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TPT; ++j) {
+      const int t = g + 4 * j;
+      if (t < NT) {
+        const int iy = t / WD, ix = t - (t / WD) * WD;
+        const float* sp = &st[((oy0 + iy) * ATB + ox0 + ix) * SROW];
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < ACC / 4; ++k) {
+          const f32x4 u = *reinterpret_cast<const f32x4*>(sp + 4 * k);
+          s += f1c[k][0] * u[0] + f1c[k][1] * u[1] + f1c[k][2] * u[2] + f1c[k][3] * u[3];
+        }
+        acc[j] += s;
+      }
+    }
+  }
+  __syncthreads();
+  // tap sums of the tile's pixels: ts[q][t] (reusing the staging area)
+  float* ts = st + lane * (NT + 1);
+#pragma unroll
+  for (int j = 0; j < TPT; ++j) {
+    const int t = g + 4 * j;
+    if (t < NT) ts[t] = acc[j];
+  }
+  __syncthreads();
+  if (!valid) return;
+  for (int o = g; o < RD * RD; o += 4) alt_bin_store(a, bn, p, x, y, ts, o);
+  if (a.flow && g == 0) {
+    a.flow[((long)b * P1 + p) * a.flow_ld + 0] = x * a.coord_div - (float)(p % a.W1);
+    a.flow[((long)b * P1 + p) * a.flow_ld + 1] = y * a.coord_div - (float)(p / a.W1);
+  }
+}
+
 int launch_alt(const AltArgs& a, raft_stream_t stream) {
+  hipStream_t s = as_stream(stream);
+#ifndef ALT_NO_TILE  // dev builds: the per-pixel kernel at every size
+  if (a.r == 4 && a.C % ACC == 0 && a.C <= 256) {
+    const long tiles = (long)a.B * a.N * cdiv_l(a.H1, AT) * cdiv_l(a.W1, AT);
+    hipLaunchKernelGGL(alt_corr_tile_kernel<4>, dim3((unsigned)tiles), dim3(256), 0, s, a);
+    return check_launch("raft_alt_corr");
+  }
+#endif
   const long waves = (long)a.B * a.N * a.H1 * a.W1;
   dim3 grid((unsigned)cdiv_l(waves, 4));
-  hipStream_t s = as_stream(stream);
   if (a.C <= 256)
     hipLaunchKernelGGL(alt_corr_kernel<1>, grid, dim3(256), 0, s, a);
   else if (a.C <= 512)

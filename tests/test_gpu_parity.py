@@ -160,6 +160,37 @@ def test_alt_cuda_corr_forward_vs_oracle(n, C):
     assert maxabs(corr, ref) < 1e-4
 
 
+@pytest.mark.parametrize("layout", [0, 1])
+def test_alt_corr_tiled_vs_oracle(layout):
+    """The tiled alt kernel (8x8 query tiles, window box staged in LDS): tiles whose box fits,
+    one tile forced onto the per-pixel path by a far coordinate, ragged edge tiles; the
+    reference's [B,N,81,H,W] output and the NHWC-row variant."""
+    from raft_optical_flow_amd import _lib
+    from raft_optical_flow_amd import kernels as K
+    rng = np.random.default_rng(5)
+    B, H1, W1, C, r = 2, 19, 29, 64, 4
+    H2, W2 = 19, 29
+    f1 = rng.standard_normal((B, H1, W1, C)).astype(np.float32)
+    f2 = rng.standard_normal((B, H2, W2, C)).astype(np.float32)
+    ys, xs = np.meshgrid(np.arange(H1), np.arange(W1), indexing="ij")
+    coords = np.stack([xs, ys], -1)[None, None].astype(np.float32).repeat(B, 0)
+    coords = (coords + rng.normal(0, 1.0, coords.shape)).astype(np.float32)
+    coords[1, 0, 9, 12] = (40.5, -7.25)  # that tile's box does not fit
+    ref = O.alt_corr_forward(f1, f2, coords, r)  # [B, 1, 81, H1, W1], unscaled
+    if layout == 0:
+        from raft_optical_flow_amd import alt_cuda_corr
+        corr, = alt_cuda_corr.forward(t(f1), t(f2), t(coords), r)
+        assert maxabs(corr, ref) < 1e-4
+    else:
+        out = torch.empty(B * H1 * W1, 81, device=DEV)
+        f1t, f2t, ct = t(f1), t(f2), t(coords)
+        _lib.call("raft_alt_corr_lookup_nhwc", f1t.data_ptr(), f2t.data_ptr(), ct.data_ptr(), 0, 1.0, out.data_ptr(),
+                  81, B, H1, W1, H2, W2, C, r, 8.0, None, 0, K.stream_handle())
+        torch.cuda.synchronize()
+        got = out.reshape(B, H1, W1, 81).permute(0, 3, 1, 2).cpu().numpy()
+        assert maxabs(got, ref[:, 0] / 8.0) < 2e-5
+
+
 @pytest.mark.parametrize("r", [4, 3])
 def test_alternate_corr_block_golden(r):
     from raft_optical_flow_amd import AlternateCorrBlock
