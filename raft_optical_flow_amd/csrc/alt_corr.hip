@@ -380,8 +380,20 @@ __global__ __launch_bounds__(256) void alt_corr_tile_kernel(AltArgs a) {
     if (t < NT) ts[t] = acc[j];
   }
   __syncthreads();
-  if (!valid) return;
-  for (int o = g; o < RD * RD; o += 4) alt_bin_store(a, bn, p, x, y, ts, o);
+  if (a.out_layout == 1) {
+    // NHWC rows: wave g writes pixels g, g + 4, ... with lanes along the row
+    // (a pixel-per-lane store would scatter 4-B writes 324 floats apart)
+    for (int q = g; q < AT * AT; q += 4) {
+      const float xq = __shfl(x, q), yq = __shfl(y, q);
+      const int pq = __shfl(p, q), vq = __shfl((int)valid, q);
+      if (!vq) continue;
+      for (int o = lane; o < RD * RD; o += 64) alt_bin_store(a, bn, pq, xq, yq, st + q * (NT + 1), o);
+    }
+    if (!valid) return;
+  } else {
+    if (!valid) return;
+    for (int o = g; o < RD * RD; o += 4) alt_bin_store(a, bn, p, x, y, ts, o);
+  }
   if (a.flow && g == 0) {
     a.flow[((long)b * P1 + p) * a.flow_ld + 0] = x * a.coord_div - (float)(p % a.W1);
     a.flow[((long)b * P1 + p) * a.flow_ld + 1] = y * a.coord_div - (float)(p / a.W1);
