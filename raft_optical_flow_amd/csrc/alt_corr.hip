@@ -222,7 +222,8 @@ __global__ __launch_bounds__(256, NV == 1 ? ALT_WAVES : 8 / NV) void alt_corr_ke
 // One 256-thread work-group per 8x8 tile of query pixels and coordinate set.
 // Neighbouring pixels' (2r+2)^2 windows overlap, so the union of the tile's
 // windows (its bounding box, <= ATB x ATB fmap2 pixels) is staged in LDS one
-// ACC-channel chunk at a time and every (pixel, tap) dot product reads it from
+// ACC-channel chunk at a time (ACC = 8: 27 KB of LDS, 4 waves/SIMD; 16 was 5 %
+// slower at 46 KB and 3 waves/SIMD) and every (pixel, tap) dot product reads it from
 // there: fmap2 crosses L2 once per tile instead of once per pixel and tap
 // (the per-pixel kernel above moves 100 KiB per pixel and level).  Thread
 // (g, q) = (wave, lane) accumulates taps g, g + 4, ... of tile pixel q; its
@@ -232,8 +233,14 @@ __global__ __launch_bounds__(256, NV == 1 ? ALT_WAVES : 8 / NV) void alt_corr_ke
 // alt_corr_kernel.
 // ============================================================================
 constexpr int AT = 8;     // tile side (query pixels)
-constexpr int ACC = 16;   // channels per staged chunk
-constexpr int ATB = 24;   // max bounding-box side (fmap2 pixels)
+#ifndef ALT_ACC  // (dev builds may override the chunk and box sizes)
+#define ALT_ACC 8
+#endif
+#ifndef ALT_ATB
+#define ALT_ATB 24
+#endif
+constexpr int ACC = ALT_ACC;  // channels per staged chunk
+constexpr int ATB = ALT_ATB;  // max bounding-box side (fmap2 pixels)
 
 // bilinear binning of one pixel's tap sums ts[(2r+2)^2] into output channel o
 __device__ __forceinline__ void alt_bin_store(const AltArgs& a, long bn, int p, float x, float y, const float* ts,
