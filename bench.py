@@ -14,8 +14,12 @@ The line also carries
   roofline      the corr-lookup kernel (the metric's "corr-lookup GB/s vs HBM
                 peak"): algorithmic bytes P*2904 per pair-iteration / its
                 average launch time measured with HIP events on its stream;
+                with --alternate-corr (config 3) the on-the-fly lookup's four
+                per-level launches instead, against the fp32 VALU peak
+                (2*P*L*(2r+2)^2*C flops per iteration);
   lookup_b8     the same kernel at B=8 (where the >=50% target is
-                quoted), on a random B=8 pyramid with the run's coords;
+                quoted), on a random B=8 pyramid with the run's coords (omitted
+                when the run itself is at B >= 8 or uses the alternate corr);
   update_gemm   the same accounting for the update-block convolutions (MFMA-bound;
                 peak per conv arithmetic: f32 MFMA 157.3 TF, f16x3 = f16 MFMA / 3);
   fp32_exact    with the default f16x3 conv arithmetic: the same run with exact
