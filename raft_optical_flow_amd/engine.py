@@ -28,6 +28,8 @@ inp slot stay 16-byte aligned).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -395,6 +397,12 @@ class RaftPlan:
         self.flow_init = torch.zeros(B, 2, h, w, device=device) if flow_init else None
         prep = Rows(A.rows(2 * B * H * W, 3))
         L.append(Launch("raft_prep_images", self.img1.data_ptr(), self.img2.data_ptr(), prep.ptr, B, H, W))
+        # the context network (below) runs on the side stream beside the feature network and
+        # the correlation build: independent work, and their 1/8-res stages alone leave CUs idle
+        # (RAFT_CTX_SIDE=0: all on the main stream)
+        ctx_side = os.environ.get("RAFT_CTX_SIDE", "1") != "0"
+        if ctx_side:
+            L.append(K.FORK)
         # feature network on [img1; img2] (core/raft.py:177-182)
         x, fh_, fw_ = plan_encoder_trunk(L, A, pk.fnet, prep, 2 * B, H, W)
         assert (fh_, fw_) == (h, w), ((fh_, fw_), (h, w))
@@ -433,9 +441,14 @@ class RaftPlan:
                 self.f2levels.append((dst, nh, nw))
                 hh, ww = nh, nw
         # context network (core/raft.py:193-200): tanh/relu split fused into its last conv
+        n_ctx = len(L)
         xc, _, _ = plan_encoder_trunk(L, A, pk.cnet, Rows(prep.t[: B * H * W]), B, H, W)
         _conv(L, pk.cnet.head, xc, B, h, w, ub.h(pu), epilogue=_lib.EPI_TANH_RELU, split=pk.hdim, out1=ub.inp(pu))
         plan_gru_context(L, pu, ub, B, h, w)
+        if ctx_side:
+            for l in L[n_ctx:]:
+                l.side = True
+            L.append(K.JOIN)
         L.append(Launch("raft_init_coords", ub.coords.data_ptr(),
                         self.flow_init.data_ptr() if self.flow_init is not None else None, B, h, w))
         self.loop_start = len(L)
