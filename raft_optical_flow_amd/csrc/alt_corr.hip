@@ -222,8 +222,9 @@ __global__ __launch_bounds__(256, NV == 1 ? ALT_WAVES : 8 / NV) void alt_corr_ke
 // One 256-thread work-group per 8x8 tile of query pixels and coordinate set.
 // Neighbouring pixels' (2r+2)^2 windows overlap, so the union of the tile's
 // windows (its bounding box, <= ATB x ATB fmap2 pixels) is staged in LDS one
-// ACC-channel chunk at a time (ACC = 8: 27 KB of LDS, 4 waves/SIMD; 16 was 5 %
-// slower at 46 KB and 3 waves/SIMD) and every (pixel, tap) dot product reads it from
+// ACC-channel chunk at a time (ACC = 8, ATB = 28: 37 KB of LDS, 4 waves/SIMD;
+// 16 channels was 5 % slower at 3 waves/SIMD; a 24-pixel box sent 30 % more
+// tiles of a divergent field to the per-pixel path) and every (pixel, tap) dot product reads it from
 // there: fmap2 crosses L2 once per tile instead of once per pixel and tap
 // (the per-pixel kernel above moves 100 KiB per pixel and level).  Thread
 // (g, q) = (wave, lane) accumulates taps g, g + 4, ... of tile pixel q; its
@@ -237,7 +238,7 @@ constexpr int AT = 8;     // tile side (query pixels)
 #define ALT_ACC 8
 #endif
 #ifndef ALT_ATB
-#define ALT_ATB 24
+#define ALT_ATB 28
 #endif
 constexpr int ACC = ALT_ACC;  // channels per staged chunk
 constexpr int ATB = ALT_ATB;  // max bounding-box side (fmap2 pixels)
