@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RAFT_HIP_ABI_VERSION 3
+#define RAFT_HIP_ABI_VERSION 4
 
 /* Negative return codes (argument errors, raised before any launch). */
 #define RAFT_E_INVALID (-1)   /* bad size / null pointer / unsupported shape */
@@ -149,6 +149,10 @@ int raft_avgpool2_nhwc(const float* in, float* out, int B, int H, int W, int C, 
  *   RAFT_PREC_F16    one f16 product (hi*hi), fp32 accumulation: the mixed-
  *                    precision mode (reference: autocast, core/raft.py:156);
  *                    uses the same split weight.
+ *   RAFT_PREC_BF16   one bf16 product, fp32 accumulation, on v_mfma_f32_32x32x16_bf16
+ *                    (bf16 mixed precision: the reference under a bf16 autocast;
+ *                    fp32's exponent range).  Weight: raft_conv2d_split_weight_prec
+ *                    with RAFT_PREC_BF16 (32 bf16 hi then 32 bf16 lo per K-step).
  * N <= 4 convolutions always take the fp32 packed weight (VALU kernel).
  * --------------------------------------------------------------------------- */
 #define RAFT_CONV_VEC 0
@@ -157,6 +161,7 @@ int raft_avgpool2_nhwc(const float* in, float* out, int B, int H, int W, int C, 
 #define RAFT_PREC_FP32 0
 #define RAFT_PREC_F16X3 1
 #define RAFT_PREC_F16 2
+#define RAFT_PREC_BF16 3
 
 /* epilogues: v = acc + bias[n] */
 #define RAFT_EPI_LINEAR 0         /* out = alpha * v                                          */
@@ -196,6 +201,10 @@ int raft_conv2d(const raft_conv2d_params* p, raft_stream_t stream);
  * per row and 32-wide K-step, 32 f16 hi then 32 f16 lo (lo scaled by 2048);
  * out holds n_pad*k_pad*4 bytes, like the input. */
 int raft_conv2d_split_weight(const float* w, void* out, int n_pad, int k_pad, raft_stream_t stream);
+/* The split form for a given precision: RAFT_PREC_F16X3 / RAFT_PREC_F16 as above;
+ * RAFT_PREC_BF16: per row and K-step 32 bf16 hi = bf16(x) then 32 bf16 lo = bf16(x - hi). */
+int raft_conv2d_split_weight_prec(const float* w, void* out, int n_pad, int k_pad, int precision,
+                                  raft_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * InstanceNorm2d (affine=False, eps): statistics per (image, channel) over

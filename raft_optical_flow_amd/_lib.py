@@ -26,9 +26,10 @@ RAFT_CONV_GATHER = 1
 PREC_FP32 = 0    # v_mfma_f32_32x32x2_f32
 PREC_F16X3 = 1   # fp32-accurate hi/lo f16 split on v_mfma_f32_32x32x16_f16
 PREC_F16 = 2     # single f16 product (mixed precision)
-PRECISIONS = {"fp32": PREC_FP32, "f16x3": PREC_F16X3, "f16": PREC_F16}
+PREC_BF16 = 3    # single bf16 product on v_mfma_f32_32x32x16_bf16 (bf16 mixed precision)
+PRECISIONS = {"fp32": PREC_FP32, "f16x3": PREC_F16X3, "f16": PREC_F16, "bf16": PREC_BF16}
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 EPI_LINEAR = 0
 EPI_RELU = 1
@@ -82,6 +83,7 @@ _PROTOS = {
                                          ctypes.POINTER(c_int)]),
     "raft_conv2d": (c_int, [ctypes.POINTER(ConvParams), P]),
     "raft_conv2d_split_weight": (c_int, [P, P, c_int, c_int, P]),
+    "raft_conv2d_split_weight_prec": (c_int, [P, P, c_int, c_int, c_int, P]),
     "raft_instnorm_workspace_floats": (c_size_t, [c_int, c_int, c_int]),
     "raft_instnorm_stats": (c_int, [P, c_int, c_int, c_int, c_int, c_float, P, P, P]),
     "raft_instnorm_apply": (c_int, [P, c_int, P, P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, P]),

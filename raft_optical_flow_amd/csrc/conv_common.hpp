@@ -9,6 +9,14 @@ namespace {
 
 using h4 = __attribute__((ext_vector_type(4))) _Float16;
 using h8 = __attribute__((ext_vector_type(8))) _Float16;
+using bf4 = __attribute__((ext_vector_type(4))) __bf16;
+using bf8 = __attribute__((ext_vector_type(8))) __bf16;
+
+// bf16 operands travel in the f16 containers (same 16-bit lanes): round to
+// nearest even (v_cvt_pk_bf16_f32), bit-cast at the MFMA
+__device__ __forceinline__ h4 to_bf16x4(const f32x4 x) {
+  return __builtin_bit_cast(h4, __builtin_convertvector(x, bf4));
+}
 
 constexpr float SPLIT_SCALE = 2048.f;  // lo is stored scaled by 2^11 (kept out of f16 subnormals)
 

@@ -21,6 +21,8 @@
 //    v_mfma_f32_32x32x16_f16 (16x the f32 rate): 6 x 32 cycles instead of
 //    16 x 64.  Result acc + accx/2048: ~22-bit operands, fp32 accumulation.
 //  * F16: hi*hi only (the mixed-precision mode).
+//  * BF16: one bf16 product on v_mfma_f32_32x32x16_bf16 (bf16 mixed precision:
+//    activations rounded to bf16 at staging, weights pre-converted).
 //
 // Pipeline: two register staging sets and two LDS buffers.  The global loads
 // of K-step k+2 are issued right after the barrier that publishes step k+1,
@@ -264,6 +266,11 @@ __global__ __launch_bounds__(256 * KG, 4) void conv_gemm_kernel(ConvArgs a) {  /
     if constexpr (PREC == RAFT_PREC_FP32) {
       *reinterpret_cast<f32x4*>(A + lr * LDSK + lq * 4) = x0;
       *reinterpret_cast<f32x4*>(A + (lr + 32) * LDSK + lq * 4) = x1;
+    } else if constexpr (PREC == RAFT_PREC_BF16) {
+      _Float16* a0 = reinterpret_cast<_Float16*>(A + lr * LDSK) + lq * 4;
+      _Float16* a1 = reinterpret_cast<_Float16*>(A + (lr + 32) * LDSK) + lq * 4;
+      *reinterpret_cast<h4*>(a0) = to_bf16x4(x0);
+      *reinterpret_cast<h4*>(a1) = to_bf16x4(x1);
     } else {
       // row: 32 hi halves (bytes 0..63) then 32 lo halves (64..127)
       h4 h0, l0, h1, l1;
@@ -324,6 +331,11 @@ __global__ __launch_bounds__(256 * KG, 4) void conv_gemm_kernel(ConvArgs a) {  /
           accx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[q], bl[q], accx, 0, 0, 0);
           accx = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[q], bh[q], accx, 0, 0, 0);
         }
+      } else if constexpr (PREC == RAFT_PREC_BF16) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8, ah[q]), __builtin_bit_cast(bf8, bh[q]),
+                                                        acc, 0, 0, 0);
       } else {
 #pragma unroll
         for (int q = 0; q < 2; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[q], bh[q], acc, 0, 0, 0);
@@ -339,7 +351,7 @@ __global__ __launch_bounds__(256 * KG, 4) void conv_gemm_kernel(ConvArgs a) {  /
   auto interleave = [&]() {
 #if CONV_SCHED
     constexpr int NMF = PREC == RAFT_PREC_FP32 ? 16 : PREC == RAFT_PREC_F16X3 ? 6 : 2;
-    constexpr int NRD = PREC == RAFT_PREC_F16 ? 4 : 8;
+    constexpr int NRD = (PREC == RAFT_PREC_F16 || PREC == RAFT_PREC_BF16) ? 4 : 8;
     constexpr int NVA = PREC == RAFT_PREC_FP32 ? 1 : PREC == RAFT_PREC_F16X3 ? 6 : 10;
     // operand reads in two halves (the second half after a third of the
     // MFMAs) keep fewer fragment registers live
@@ -651,6 +663,7 @@ void launch_gemm_m(const ConvArgs& a, dim3 grid, bool two, hipStream_t s) {
   switch (a.p.precision) {
     case RAFT_PREC_F16X3: launch_gemm_p<MODE, RAFT_PREC_F16X3>(a, grid, two, s); break;
     case RAFT_PREC_F16: launch_gemm_p<MODE, RAFT_PREC_F16>(a, grid, two, s); break;
+    case RAFT_PREC_BF16: launch_gemm_p<MODE, RAFT_PREC_BF16>(a, grid, two, s); break;
     default: launch_gemm_p<MODE, RAFT_PREC_FP32>(a, grid, two, s); break;
   }
 }
@@ -671,6 +684,16 @@ __global__ void split_weight_kernel(const float* __restrict__ w, _Float16* __res
   out[blk * 64 + k] = h;
   out[blk * 64 + 32 + k] = (_Float16)((x - (float)h) * SPLIT_SCALE);
 }
+// fp32 packed weight -> per (row, K-step): 32 bf16 hi then 32 bf16 lo = bf16(x - hi)
+__global__ void split_weight_bf16_kernel(const float* __restrict__ w, __bf16* __restrict__ out, long total) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const float x = w[i];
+  const __bf16 h = (__bf16)x;
+  const long blk = i >> 5, k = i & 31;
+  out[blk * 64 + k] = h;
+  out[blk * 64 + 32 + k] = (__bf16)(x - (float)h);
+}
 }  // namespace
 
 #ifdef STAMPS
@@ -686,6 +709,19 @@ extern "C" int raft_conv2d_split_weight(const float* w, void* out, int n_pad, in
   hipLaunchKernelGGL(split_weight_kernel, dim3((unsigned)cdiv_l(total, 256)), dim3(256), 0, as_stream(stream), w,
                      reinterpret_cast<_Float16*>(out), total);
   return check_launch("raft_conv2d_split_weight");
+}
+
+extern "C" int raft_conv2d_split_weight_prec(const float* w, void* out, int n_pad, int k_pad, int precision,
+                                             raft_stream_t stream) {
+  RAFT_REQUIRE(precision == RAFT_PREC_F16X3 || precision == RAFT_PREC_F16 || precision == RAFT_PREC_BF16,
+               "raft_conv2d_split_weight_prec: precision %d has no split form", precision);
+  if (precision != RAFT_PREC_BF16) return raft_conv2d_split_weight(w, out, n_pad, k_pad, stream);
+  RAFT_REQUIRE(w && out && n_pad > 0 && k_pad > 0 && k_pad % BK == 0, "raft_conv2d_split_weight_prec: bad args");
+  RAFT_REQUIRE((const void*)w != out, "raft_conv2d_split_weight_prec: in-place split is not supported");
+  const long total = (long)n_pad * k_pad;
+  hipLaunchKernelGGL(split_weight_bf16_kernel, dim3((unsigned)cdiv_l(total, 256)), dim3(256), 0, as_stream(stream), w,
+                     reinterpret_cast<__bf16*>(out), total);
+  return check_launch("raft_conv2d_split_weight_prec");
 }
 
 extern "C" int raft_conv2d_packed_shape(int mode, int n, int kh, int kw, int cin, int* n_pad, int* k_pad) {
@@ -800,7 +836,8 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
       hipLaunchKernelGGL(conv_smalln_kernel<4>, grid, dim3(256), 0, s, a);
     return check_launch("raft_conv2d(small n)");
   }
-  RAFT_REQUIRE(p.precision == RAFT_PREC_FP32 || p.precision == RAFT_PREC_F16X3 || p.precision == RAFT_PREC_F16,
+  RAFT_REQUIRE(p.precision == RAFT_PREC_FP32 || p.precision == RAFT_PREC_F16X3 || p.precision == RAFT_PREC_F16 ||
+                   p.precision == RAFT_PREC_BF16,
                "raft_conv2d: unknown precision %d", p.precision);
   if (p.mode == RAFT_CONV_VEC && conv_halo_launch(p, k_pad, n_pad, a.w_bytes, a.in0_bytes, a.in1_bytes, s) == 0)
     return check_launch("raft_conv2d(halo)");

@@ -37,7 +37,9 @@
 // x = hi + lo (hi = f16(x), lo = f16(x - hi), unscaled: the f16-subnormal
 // floor of lo is an absolute 2^-25 per element), against the pre-split
 // weight (hi, 2048*lo): acc += hi*hi, acl += lo*hi, accx += hi*(2048 lo),
-// three independent accumulator chains.  F16 (mixed precision) runs hi*hi.
+// three independent accumulator chains.  F16 (mixed precision) runs hi*hi;
+// BF16 rounds activations and weights to bf16 and runs one
+// v_mfma_f32_32x32x16_bf16 product (bf16 mixed precision).
 #include "conv_common.hpp"
 
 namespace raft {
@@ -163,9 +165,15 @@ __device__ __forceinline__ float sub_half_hi(unsigned hpk, float x) {
 using f2 = __attribute__((ext_vector_type(2))) float;
 using h2 = __attribute__((ext_vector_type(2))) _Float16;
 
-// 8 floats -> 8 f16 hi (+ 8 f16 lo = f16(x - hi)) : 4 VALU per 2 elements
-template <bool LO>
+// 8 floats -> 8 f16 hi (+ 8 f16 lo = f16(x - hi)) : 4 VALU per 2 elements;
+// BF: 8 bf16 (round to nearest even) in the f16 container, no lo
+template <bool LO, bool BF = false>
 __device__ __forceinline__ void split8(const f32x4 x0, const f32x4 x1, h8& hi, h8& lo) {
+  if constexpr (BF) {
+    const h4 a = to_bf16x4(x0), b = to_bf16x4(x1);
+    hi = h8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    return;
+  }
   const float v[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
   unsigned hp[4], lp[4];
 #pragma unroll
@@ -191,6 +199,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
   constexpr int NWP = U * NBI / 4;  // weight pieces per loader wave per load set
   constexpr int NSUB = BNT / 32;    // 32-column MFMA subtiles per compute wave
   constexpr bool X3 = PREC == RAFT_PREC_F16X3;
+  constexpr bool BF = PREC == RAFT_PREC_BF16;
   // LSPLIT: the loaders stage each patch through registers and store it
   // pre-split (f16 hi | lo, the weight-row format), so the MFMA waves read
   // ready fragments; 1x1 convs (a patch per K-step, D = 2) keep fp32 patches
@@ -346,9 +355,9 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
         for (int i = 0; i < TI; ++i) {
           if (tlds[i] >= 0) {
             h8 hi, lo;
-            split8<true>(src[i][0], src[i][1], hi, lo);
+            split8<X3, BF>(src[i][0], src[i][1], hi, lo);
             *reinterpret_cast<h8*>(base + tlds[i]) = hi;
-            *reinterpret_cast<h8*>(base + (tlds[i] ^ 64)) = lo;
+            if constexpr (X3) *reinterpret_cast<h8*>(base + (tlds[i] ^ 64)) = lo;
           }
         }
       };
@@ -520,17 +529,24 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
     F.ah[1] = __builtin_bit_cast(h8, av[2]);
     F.al[1] = __builtin_bit_cast(h8, av[3]);
 #else
-    split8<X3>(av[0], av[1], F.ah[0], F.al[0]);
-    split8<X3>(av[2], av[3], F.ah[1], F.al[1]);
+    split8<X3, BF>(av[0], av[1], F.ah[0], F.al[0]);
+    split8<X3, BF>(av[2], av[3], F.ah[1], F.al[1]);
 #endif
   };
   // the MFMAs of one accumulator never follow each other back to back
   auto mfma_step = [&](const Frag& F) {
 #pragma unroll
     for (int qq = 0; qq < 2; ++qq) {
+      if constexpr (BF) {
 #pragma unroll
-      for (int sb = 0; sb < NSUB; ++sb)
-        acc[sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.ah[qq], F.bh[sb][qq], acc[sb], 0, 0, 0);
+        for (int sb = 0; sb < NSUB; ++sb)
+          acc[sb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8, F.ah[qq]),
+                                                            __builtin_bit_cast(bf8, F.bh[sb][qq]), acc[sb], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int sb = 0; sb < NSUB; ++sb)
+          acc[sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.ah[qq], F.bh[sb][qq], acc[sb], 0, 0, 0);
+      }
       if constexpr (X3) {
 #pragma unroll
         for (int sb = 0; sb < NSUB; ++sb)
@@ -653,6 +669,8 @@ template <int KH, int KW>
 void launch_halo_k(const HaloArgs& a, int bn, dim3 grid, hipStream_t s) {
   if (a.p.precision == RAFT_PREC_F16X3)
     launch_halo_p<KH, KW, RAFT_PREC_F16X3>(a, bn, grid, s);
+  else if (a.p.precision == RAFT_PREC_BF16)
+    launch_halo_p<KH, KW, RAFT_PREC_BF16>(a, bn, grid, s);
   else
     launch_halo_p<KH, KW, RAFT_PREC_F16>(a, bn, grid, s);
 }
@@ -677,7 +695,7 @@ int conv_halo_launch(const raft_conv2d_params& p, int k_pad, int n_pad, unsigned
   }();
   if (!enabled) return 1;
   if (p.mode != RAFT_CONV_VEC || p.stride_h != 1 || p.stride_w != 1) return 1;
-  if (p.precision != RAFT_PREC_F16X3 && p.precision != RAFT_PREC_F16) return 1;
+  if (p.precision != RAFT_PREC_F16X3 && p.precision != RAFT_PREC_F16 && p.precision != RAFT_PREC_BF16) return 1;
   const int kh = p.kh, kw = p.kw;
   const bool shape = (kh == 1 && kw == 1) || (kh == 3 && kw == 3) || (kh == 1 && kw == 5) || (kh == 5 && kw == 1);
   if (!shape || p.pad_h != (kh - 1) / 2 || p.pad_w != (kw - 1) / 2) return 1;

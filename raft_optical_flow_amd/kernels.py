@@ -81,7 +81,8 @@ class PackedConv:
     mode: int
     cin_real: int = 0         # input channels of the original weight (FLOP accounting)
     precision: int = _lib.PREC_FP32
-    split: torch.Tensor | None = None   # hi/lo f16 form of `weight` (F16X3 / F16), made on first use
+    split: torch.Tensor | None = None   # hi/lo f16 (F16X3 / F16) or bf16 (BF16) form of `weight`, made on first use
+    split_prec: int = -1
 
     def launch_precision(self) -> int:
         # N <= 4 convs run on the VALU kernel, which reads the fp32 weight
@@ -90,11 +91,14 @@ class PackedConv:
     def launch_weight(self) -> torch.Tensor:
         if self.launch_precision() == _lib.PREC_FP32:
             return self.weight
-        if self.split is None:
+        # F16X3 and F16 share one split form; BF16 has its own
+        fmt = _lib.PREC_BF16 if self.precision == _lib.PREC_BF16 else _lib.PREC_F16X3
+        if self.split is None or self.split_prec != fmt:
             w = self.weight
             self.split = torch.empty_like(w)
-            _lib.call("raft_conv2d_split_weight", w.data_ptr(), self.split.data_ptr(), w.shape[0], w.shape[1],
-                      stream_handle())
+            _lib.call("raft_conv2d_split_weight_prec", w.data_ptr(), self.split.data_ptr(), w.shape[0], w.shape[1],
+                      fmt, stream_handle())
+            self.split_prec = fmt
         return self.split
 
 

@@ -158,6 +158,37 @@ def gen_raft_e2e(full_size: bool):
 
 
 @torch.no_grad()
+def gen_config4():
+    """Config 4 shape: 540x960 frames padded (InputPadder 'sintel') to 544x960, B=1, iters=32."""
+    i1, i2 = seeded_images(1, 544, 960, seed=2)
+    m = ref_model(False, 0)
+    low, up = m(i1, i2, iters=32, test_mode=True)
+    save("raft_full_rand_b1_544x960_i32.npz", iters=32, seed=0, img_seed=2, flow_low=low,
+         flow_up_rows8=up[:, :, ::8], flow_up_sum=up.double().sum(), flow_up_abs=up.double().abs().sum())
+
+
+@torch.no_grad()
+def gen_bf16():
+    """Config 5 arithmetic: the reference with mixed_precision=True under CPU bf16 autocast
+    (core/raft.py:177,193,225 enter `autocast(enabled=mixed_precision)`; the module attribute
+    is pointed at torch.autocast('cpu', bfloat16) for the run)."""
+    rraft, *_ = ref_modules()
+    saved = rraft.autocast
+    rraft.autocast = lambda enabled=True: torch.autocast("cpu", dtype=torch.bfloat16, enabled=enabled)
+    try:
+        for (h, w, iters, img_seed) in ((128, 192, 32, 1),):
+            i1, i2 = seeded_images(1, h, w, seed=img_seed)
+            m = rraft.RAFT(argparse.Namespace(small=False, mixed_precision=True, alternate_corr=False, dropout=0))
+            m.load_state_dict(seeded_state_dict(m, 0))
+            m.eval()
+            low, up = m(i1, i2, iters=iters, test_mode=True)
+            save(f"raft_full_rand_b1_{h}x{w}_i{iters}_bf16.npz", iters=iters, seed=0, img_seed=img_seed,
+                 flow_low=low.float(), flow_up=up.float())
+    finally:
+        rraft.autocast = saved
+
+
+@torch.no_grad()
 def gen_raft_small_demo():
     """Config 1: raft-small.pth on demo-frames 0016 -> 0017, iters=12 (reference demo.py path)."""
     from PIL import Image
@@ -190,7 +221,8 @@ if __name__ == "__main__":
     ap.add_argument("--only", default="")
     a = ap.parse_args()
     jobs = {"lookup": gen_lookup, "update": gen_update_and_upsample, "enc": gen_encoders,
-            "e2e": lambda: gen_raft_e2e(a.full_size), "demo": gen_raft_small_demo}
+            "e2e": lambda: gen_raft_e2e(a.full_size), "demo": gen_raft_small_demo,
+            "config4": gen_config4, "bf16": gen_bf16}
     for k, f in jobs.items():
         if not a.only or k in a.only.split(","):
             f()

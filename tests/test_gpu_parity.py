@@ -246,10 +246,10 @@ CONV_CASES = [
 ]
 
 
-CONV_TOL = {"fp32": 1e-4, "f16x3": 1e-4, "f16": 5e-3}
+CONV_TOL = {"fp32": 1e-4, "f16x3": 1e-4, "f16": 5e-3, "bf16": 3e-2}
 
 
-@pytest.mark.parametrize("prec", ["fp32", "f16x3", "f16"])
+@pytest.mark.parametrize("prec", ["fp32", "f16x3", "f16", "bf16"])
 @pytest.mark.parametrize("cin,cout,kh,kw,stride,pad,H,W,B", CONV_CASES)
 def test_conv2d_vs_torch_fp64(cin, cout, kh, kw, stride, pad, H, W, B, prec):
     from raft_optical_flow_amd import kernels as K
@@ -284,6 +284,20 @@ def test_conv2d_split_weight_layout():
     assert torch.equal(h[:, :, 0], hi) and torch.equal(h[:, :, 1], lo)
     rec = h[:, :, 0].double() + h[:, :, 1].double() / 2048
     assert float((rec - w.view(64, 3, 32).double()).abs().max()) < 2.0 ** -22 * 0.25
+
+
+def test_conv2d_split_weight_bf16_layout():
+    """raft_conv2d_split_weight_prec(RAFT_PREC_BF16): per K-step 32 bf16 hi (RNE) then 32 bf16 lo = bf16(x - hi)."""
+    from raft_optical_flow_amd import _lib
+    g = torch.Generator().manual_seed(12)
+    w = (torch.randn(64, 96, generator=g) * 0.05).to(DEV)
+    out = torch.empty_like(w)
+    _lib.call("raft_conv2d_split_weight_prec", w.data_ptr(), out.data_ptr(), 64, 96, _lib.PREC_BF16, 0)
+    torch.cuda.synchronize()
+    h = out.view(torch.bfloat16).view(64, 3, 2, 32)
+    hi = w.view(64, 3, 32).bfloat16()
+    lo = (w.view(64, 3, 32) - hi.float()).bfloat16()
+    assert torch.equal(h[:, :, 0], hi) and torch.equal(h[:, :, 1], lo)
 
 
 @pytest.mark.parametrize("prec", ["fp32", "f16x3"])

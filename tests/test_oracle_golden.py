@@ -123,3 +123,14 @@ def test_raft_full_size_matches_reference():
     low, up = O.raft_forward(p, i1.numpy(), i2.numpy(), iters=32)
     assert maxabs(low, g["flow_low"]) < 1e-3
     assert maxabs(up[:, :, ::8], g["flow_up_rows8"]) < 1e-3
+
+
+@pytest.mark.slow
+def test_raft_config4_shape_matches_reference():
+    """Config 4 shape (544x960 after InputPadder), iters=32."""
+    g = load_golden("raft_full_rand_b1_544x960_i32.npz")
+    p = params(False, int(g["seed"]))
+    i1, i2 = seeded_images(1, 544, 960, seed=int(g["img_seed"]))
+    low, up = O.raft_forward(p, i1.numpy(), i2.numpy(), iters=32)
+    assert maxabs(low, g["flow_low"]) < 1e-3
+    assert maxabs(up[:, :, ::8], g["flow_up_rows8"]) < 1e-3
