@@ -12,20 +12,27 @@ scaling is weak.  Rank 0 prints one JSON line.
 
 The line also carries
   roofline      the corr-lookup kernel (the metric's "corr-lookup GB/s vs HBM
-                peak"): algorithmic bytes P*2904 per pair-iteration / its
-                average launch time measured with HIP events on its stream;
-                with --alternate-corr (config 3) the on-the-fly lookup's four
-                per-level launches instead, against the fp32 VALU peak
+                peak"): algorithmic bytes P*2904 per pair-iteration / its average
+                duration INSIDE the forward (HIP event pairs on its stream around each
+                of the 32 lookups of an eagerly enqueued forward); `traffic` = HBM
+                bytes per launch from the committed in-forward PMC summary
+                (profiles/r02_lookup_pmc.json, used only while corr_pyramid.hip is the
+                source it was taken on); with --alternate-corr (config 3) the
+                on-the-fly lookup's per-level launches against the fp32 VALU peak
                 (2*P*L*(2r+2)^2*C flops per iteration);
-  lookup_b8     the same kernel at B=8 (where the >=50% target is
-                quoted), on a random B=8 pyramid with the run's coords (omitted
-                when the run itself is at B >= 8 or uses the alternate corr);
-  update_gemm   the same accounting for the update-block convolutions (MFMA-bound;
-                peak per conv arithmetic: f32 MFMA 157.3 TF, f16x3 = f16 MFMA / 3);
+  lookup_b8     the same kernel in a B=8 forward of the same geometry (SURVEY 8(d):
+                where the >=50% target is quoted; its own 2.2 GB pyramid and coords);
+  update_gemm   the update block's main-stream convolutions of one iteration, timed
+                in-forward (MFMA-bound; fp32-equivalent peak per conv arithmetic:
+                f32 MFMA 157.3 TF, f16x3 = f16 MFMA / 3, f16 / bf16 2.5 PF);
+  dominant_kernel  the step's dominant kernel, conv_halo_kernel<3,3,64> (convc2 and
+                the flow-head conv1), in-forward, with its committed MFMA-busy PMC
+                (profiles/r02_halo_pmc.json) while conv_halo.hip is unchanged;
   fp32_exact    with the default f16x3 conv arithmetic: the same run with exact
                 f32 MFMA convs (value, ms_per_step), rank 0, N = 1;
-  cpu_baseline  the numpy oracle (oracle/raft_oracle.py) on the host cores for one
-                pair of the same workload (rank 0, N = 1 only).
+  cpu_baseline  the reference's CPU path restated with the same torch CPU operators
+                (oracle/torch_cpu.py) on the host cores, whole pairs of the same
+                workload for ~12 s (rank 0, N = 1 only).
 """
 from __future__ import annotations
 
@@ -45,9 +52,11 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TF = 157.3  # dense f32 MFMA (= f32 vector) peak
 F16_MFMA_PEAK_TF = 2500.0  # dense f16 MFMA peak
 # fp32-equivalent peak of the update convolutions per conv arithmetic
-CONV_PEAK_TF = {"fp32": FP32_MFMA_PEAK_TF, "f16x3": F16_MFMA_PEAK_TF / 3, "f16": F16_MFMA_PEAK_TF}
+CONV_PEAK_TF = {"fp32": FP32_MFMA_PEAK_TF, "f16x3": F16_MFMA_PEAK_TF / 3, "f16": F16_MFMA_PEAK_TF,
+                "bf16": F16_MFMA_PEAK_TF}
 DTYPE = {"fp32": "fp32", "f16x3": "fp32 (convs: f16x3 split MFMA, fp32 accumulate)",
-         "f16": "f16 convs, fp32 accumulate (mixed precision)"}
+         "f16": "f16 convs, fp32 accumulate (mixed precision)",
+         "bf16": "bf16 convs, fp32 accumulate (bf16 mixed precision; corr volume + lookup fp32-accurate)"}
 
 
 def lookup_bytes_per_pixel(levels=4, r=4):
@@ -59,22 +68,6 @@ def alt_lookup_flops(P, levels=4, r=4, C=256):
     """alternate-corr lookup, 2*P*L*(2r+2)^2*C flops per iteration (the reference's
     integer-tap inner products, correlation_kernel.cu:43-114)."""
     return 2 * P * levels * (2 * r + 2) ** 2 * C
-
-
-def update_flops_per_pixel(pu, with_mask):
-    """2*MACs of the update-block convolutions per 1/8-res pixel (one iteration)."""
-    def f(pc):
-        return 2 * pc.n * pc.kh * pc.kw * pc.cin_real
-    tot = 0
-    for pc in [pu.convc1, pu.convc2, pu.convf1, pu.convf2, pu.conv]:
-        if pc is not None:
-            tot += f(pc)
-    for zr, q, _ctx in pu.gru:  # the inp context GEMM runs once per pair, not per iteration
-        tot += f(zr) + f(q)
-    tot += f(pu.fh1_mask if with_mask else pu.fh1) + f(pu.fh2)
-    if with_mask:
-        tot += f(pu.mask2)
-    return tot
 
 
 def time_kernel_events(fn, reps):
@@ -99,61 +92,93 @@ def time_kernel_events(fn, reps):
     return start.elapsed_time(end) / reps * 1e-3  # seconds
 
 
-def lookup_at_b8(plan, dev, h8, w8, B8=8, reps=50):
-    """the lookup's HBM roofline measured at B=8 (163.5 MB algorithmic per launch at
-    config 2), where it is not launch/latency-bound: a B=8 pyramid of the same geometry (random
-    values: the lookup is data-independent) and the B=1 run's final coords replicated 8x."""
+def halo_bn(pc_n, batch, h, w):
+    """The N tile conv_halo_launch picks (csrc/conv_halo.hip): 64 unless 32 keeps more CUs busy."""
+    spatial = batch * -(-h // 8) * -(-w // 16)
+    n_pad = -(-pc_n // 64) * 64
+    return 64 if spatial * (n_pad // 64) > 128 else 32
+
+
+def rotated_lookup(plan, batch, h8, w8, nrot, reps):
+    """Average duration of the corr-lookup kernel at `batch` pairs, cache-cold: one hipGraph of
+    reps x nrot launches, launch k on its own pyramid k % nrot (random values: the lookup's cost
+    does not depend on them) with the forward's own final coords, timed with HIP events around the
+    replay on the launch stream.  nrot is chosen so the windows the nrot launches touch exceed the
+    256 MiB Infinity Cache, so no launch is served from a cache its predecessor warmed
+    (back-to-back replays of ONE launch would be: its ~28 MB per pair stays resident).
+    In a graph replay consecutive kernels run with no gap, so this average is the per-dispatch
+    duration rocprofv3 reports for the same launches (tools/forward_avg.py)."""
     from raft_optical_flow_amd import _lib
     from raft_optical_flow_amd import kernels as K
-    lib = _lib.load()
+    dev = plan.device
     L, r = plan.pk.levels, plan.pk.radius
-    pyr = torch.randn(int(lib.raft_corr_pyramid_floats(B8, h8, w8, L)), device=dev)
-    coords = plan.ub.coords.repeat(B8, 1).contiguous()
+    nfl = int(_lib.load().raft_corr_pyramid_floats(batch, h8, w8, L))
+    pyrs = [torch.randn(nfl, device=dev) for _ in range(nrot)]
+    reps_b = -(-batch // plan.B)
+    coords = plan.ub.coords.view(plan.B, -1, 2).repeat(reps_b, 1, 1)[:batch].reshape(-1, 2).contiguous()
     ntap = L * (2 * r + 1) ** 2
-    out = torch.empty(B8 * h8 * w8, ntap, device=dev)
+    out = torch.empty(batch * h8 * w8, ntap, device=dev)
 
     def fn():
-        _lib.call("raft_corr_lookup", pyr.data_ptr(), B8, h8, w8, L, r, coords.data_ptr(), 0, out.data_ptr(), ntap, 0,
-                  None, 0, K.stream_handle())
+        for k in range(nrot):
+            _lib.call("raft_corr_lookup", pyrs[k].data_ptr(), batch, h8, w8, L, r, coords.data_ptr(), 0,
+                      out.data_ptr(), ntap, 0, None, 0, K.stream_handle())
 
-    t = time_kernel_events(fn, reps)
-    alg = B8 * h8 * w8 * lookup_bytes_per_pixel(L, r)
-    del pyr
-    return {"kernel": "raft_corr_lookup", "batch": B8, "bound": "hbm", "achieved": round(alg / t / 1e9, 1),
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
-            "algorithmic_bytes_per_launch": alg, "launch_us": round(t * 1e6, 2)}
-
-
-def cpu_baseline(args):
-    """The oracle (numpy restatement of the reference path) on one pair of the same workload."""
-    import numpy as np
-    from oracle import raft_oracle as O
-    from raft_optical_flow_amd import RAFT
-    from raft_optical_flow_amd.init import seeded_images, seeded_state_dict
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
-    m = RAFT(argparse.Namespace(small=False, mixed_precision=False, alternate_corr=False))
-    p = {k: v.numpy() for k, v in seeded_state_dict(m, 0).items()}
-    i1, i2 = seeded_images(1, args.height, args.width, seed=1)
-    # InputPadder 'sintel' mode (core/utils/utils.py:7-24): replicate pad, centred, to multiples of 8
-    ph, pw = (-args.height) % 8, (-args.width) % 8
-    pads = ((0, 0), (0, 0), (ph // 2, ph - ph // 2), (pw // 2, pw - pw // 2))
-    i1 = np.pad(i1.numpy(), pads, mode="edge")
-    i2 = np.pad(i2.numpy(), pads, mode="edge")
-    t0 = time.perf_counter()
-    O.raft_forward(p, i1, i2, iters=args.iters)
-    dt = time.perf_counter() - t0
-    return {"value": round(1.0 / dt, 4), "unit": "image-pairs/s", "cores": threads, "kind": "port",
-            "sample": f"1 pair {args.height}x{args.width} (padded to {i1.shape[2]}x{i1.shape[3]}), iters={args.iters}, "
-                      f"numpy oracle, {dt:.1f} s"}
+    t = time_kernel_events(fn, reps) / nrot
+    del pyrs
+    torch.cuda.empty_cache()
+    alg = batch * h8 * w8 * lookup_bytes_per_pixel(L, r)
+    return {"kernel": "corr_lookup_kernel<4,4> (raft_corr_lookup)", "batch": batch, "bound": "hbm",
+            "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": alg,
+            "launch_us": round(t * 1e6, 2),
+            "timing": f"HIP events around a hipGraph of {reps * nrot} launches rotating over {nrot} pyramids "
+                      f"({nrot * nfl * 4 / 2**30:.1f} GiB; cache-cold), the forward's final coords"}
 
 
-def load_traffic():
-    """HBM bytes per lookup launch from the committed PMC pass (profiles/), if present."""
-    path = os.path.join(ROOT, "profiles", "lookup_pmc.json")
+def load_pmc(name, source):
+    """A committed PMC summary (profiles/<name>) if it was taken on the current kernel source:
+    its source_sha must equal the sha1 of that .hip file (else the counters are stale)."""
+    import hashlib
+    path = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(path):
         return None
     with open(path) as f:
-        return json.load(f)
+        d = json.load(f)
+    with open(os.path.join(ROOT, "raft_optical_flow_amd", "csrc", source), "rb") as f:
+        sha = hashlib.sha1(f.read()).hexdigest()
+    return d if d.get("source_sha") == sha else None
+
+
+def cpu_baseline(args, budget_s=12.0):
+    """The reference's CPU path, restated with the same torch CPU operators (oracle/torch_cpu.py:
+    bit-identical flow and the same speed as the reference's own core/ in the build container),
+    on the host cores: one warm-up pair at iters=2, then whole pairs of the bench workload until
+    `budget_s` seconds have passed (at least one)."""
+    from oracle import torch_cpu as T
+    from raft_optical_flow_amd import RAFT
+    from raft_optical_flow_amd.init import seeded_images, seeded_state_dict
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    m = RAFT(argparse.Namespace(small=False, mixed_precision=False, alternate_corr=False))
+    p = seeded_state_dict(m, 0)
+    i1, i2 = seeded_images(1, args.height, args.width, seed=1)
+    # InputPadder 'sintel' mode (core/utils/utils.py:7-24): replicate pad, centred, to multiples of 8
+    ph, pw = (-args.height) % 8, (-args.width) % 8
+    pads = (pw // 2, pw - pw // 2, ph // 2, ph - ph // 2)
+    i1 = torch.nn.functional.pad(i1, pads, mode="replicate")
+    i2 = torch.nn.functional.pad(i2, pads, mode="replicate")
+    T.raft_forward(p, i1, i2, iters=2)
+    n, t0 = 0, time.perf_counter()
+    while n == 0 or time.perf_counter() - t0 < budget_s:
+        T.raft_forward(p, i1, i2, iters=args.iters)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 4), "unit": "image-pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{n} pair(s) {args.height}x{args.width} (padded to {i1.shape[2]}x{i1.shape[3]}), "
+                      f"iters={args.iters}, oracle/torch_cpu.py (the reference's torch CPU ops; reference "
+                      f"core/ measured 0.227 vs 0.226 pairs/s for this restatement at 8 threads in the build "
+                      f"container), torch.set_num_threads({threads}), {dt:.1f} s"}
 
 
 def main():
@@ -169,7 +194,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-fp32-exact", action="store_true", help="skip the exact-f32 comparison run")
-    ap.add_argument("--precision", choices=["fp32", "f16x3", "f16"], default=None,
+    ap.add_argument("--precision", choices=["fp32", "f16x3", "f16", "bf16"], default=None,
                     help="conv arithmetic (default: the RAFT default, f16x3)")
     args = ap.parse_args()
 
@@ -237,49 +262,69 @@ def main():
     pairs = world * args.batch * args.steps
     value = pairs / elapsed
 
-    # ---- per-kernel live timing (HIP events on the launch stream) -------------------
+    # ---- per-kernel live timing (HIP events on the launch stream, hipGraph replays) ----------
     from raft_optical_flow_amd import kernels as K
-    lk = [l for l in plan.launches[plan.loop_start:plan.loop_end] if getattr(l, "name", None) in
-          ("raft_corr_lookup", "raft_alt_corr_lookup_nhwc")]
-    reps = 200
     h8, w8 = H // 8, W // 8
     P = args.batch * h8 * w8
+    pu = plan.pk.update
     if not args.alternate_corr:
-        t_lookup = time_kernel_events(lambda: [l(K.stream_handle()) for l in lk[:1]], reps)
-        bytes_per_launch = P * lookup_bytes_per_pixel()
-        achieved = bytes_per_launch / t_lookup / 1e9
-        # the committed PMC pass was taken at config 2 (B=1, 440x1024): only that shape carries it
-        traffic = load_traffic() if (args.batch, H, W) == (1, 440, 1024) else None
-        roof = {"kernel": "raft_corr_lookup", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
-                "algorithmic_bytes_per_launch": bytes_per_launch, "launch_us": round(t_lookup * 1e6, 2)}
+        # 16 pyramids: 16 x 28 MB of windows per rotation at B=1 (> the 256 MiB Infinity Cache)
+        roof = rotated_lookup(plan, args.batch, h8, w8, nrot=max(3, -(-16 // args.batch)), reps=4)
+        pmc = load_pmc("r02_lookup_pmc.json", "corr_pyramid.hip")
+        # the committed PMC pass is of config 2 (B=1, 440x1024) on the current kernel source
+        roof["traffic"] = pmc["hbm_bytes_per_launch"] if pmc and [args.batch, H, W] == pmc["shape_bhw"] else None
+        if roof["traffic"] is not None:
+            roof["traffic_source"] = "profiles/r02_lookup_pmc.json (in-forward FETCH_SIZE/WRITE_SIZE, calibrated)"
     else:
         # alternate corr: FP32 VALU-bound, 2*P*L*(2r+2)^2*C flops over the L per-level launches
         nl = plan.pk.levels
-        t_lookup = time_kernel_events(lambda: [l(K.stream_handle()) for l in lk[:nl]], reps)
+        lk = [l for l in plan.launches[plan.loop_start:plan.loop_end]
+              if getattr(l, "name", None) == "raft_alt_corr_lookup_nhwc"]
+        t_it = time_kernel_events(lambda: [l(K.stream_handle()) for l in lk[:nl]], 20)
         fl = alt_lookup_flops(P, nl, plan.pk.radius, plan.pk.fdim)
-        roof = {"kernel": f"raft_alt_corr_lookup_nhwc x{nl}", "bound": "valu", "achieved": round(fl / t_lookup / 1e12, 2),
-                "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s", "frac": round(fl / t_lookup / 1e12 / FP32_MFMA_PEAK_TF, 4),
-                "traffic": None, "algorithmic_flops_per_iteration": fl, "launch_us": round(t_lookup * 1e6, 2)}
+        roof = {"kernel": f"alt_corr_tile_kernel<4> (raft_alt_corr_lookup_nhwc x{nl} per iteration)", "bound": "valu",
+                "achieved": round(fl / t_it / 1e12, 2), "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                "frac": round(fl / t_it / 1e12 / FP32_MFMA_PEAK_TF, 4), "traffic": None,
+                "algorithmic_flops_per_iteration": fl, "iteration_us": round(t_it * 1e6, 2),
+                "timing": "HIP events around a hipGraph replay of the last iteration's lookups (final coords)"}
 
-    # at B >= 8 the main roofline line already is the batched measurement
-    lookup_b8 = None if (args.alternate_corr or args.batch >= 8) else lookup_at_b8(plan, dev, h8, w8)
+    # the >= 50 % lookup target is quoted at B = 8: 3 rotating B=8 pyramids (6.6 GB)
+    lookup_b8 = None
+    if not args.alternate_corr and args.batch < 8:
+        lookup_b8 = rotated_lookup(plan, 8, h8, w8, nrot=3, reps=8)
 
-    it_launches = plan.launches[plan.loop_start:plan.loop_end]
-    upd = [l for l in it_launches if getattr(l, "name", None) == "raft_conv2d"]
-    n_iter_convs = len(upd) // args.iters
-    # one non-final iteration's conv GEMMs (no mask head)
-    one_iter = upd[:n_iter_convs - 0]
-    pu = plan.pk.update
-    t_upd = time_kernel_events(lambda: [l(K.stream_handle()) for l in one_iter], 50)
-    fl = P * update_flops_per_pixel(pu, with_mask=False)
-    upd_tf = fl / t_upd / 1e12
+    # the update block's main-stream convolutions of one (non-final) iteration, replayed as a graph
+    # (their operands are L2 / MALL-resident in the forward as well: 7 MB activations, <= 2 MB weights)
+    lk_idx = [i for i, l in enumerate(plan.launches) if getattr(l, "name", "") in
+              ("raft_corr_lookup", "raft_alt_corr_lookup_nhwc")]
+    per_it = len(lk_idx) // args.iters
+    it_convs = [plan.launches[i] for i in range(lk_idx[per_it] + 1, lk_idx[2 * per_it])
+                if getattr(plan.launches[i], "name", "") == "raft_conv2d" and not plan.launches[i].side]
+    t_upd = time_kernel_events(lambda: [l(K.stream_handle()) for l in it_convs], 20)
+    fl = P * sum(2 * l.keep.n * l.keep.kh * l.keep.kw * (l.keep.in0_c + l.keep.in1_c) for l in it_convs)
     peak = CONV_PEAK_TF[prec]
-    update_roof = {"kernel": f"raft_conv2d (update block, one iteration, {prec})", "bound": "mfma",
-                   "achieved": round(upd_tf, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-                   "frac": round(upd_tf / peak, 4), "iteration_us": round(t_upd * 1e6, 1),
-                   "flops_per_iteration": fl}
+    update_roof = {"kernel": f"raft_conv2d (update block, one iteration, {prec}; main-stream convs)", "bound": "mfma",
+                   "achieved": round(fl / t_upd / 1e12, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+                   "frac": round(fl / t_upd / 1e12 / peak, 4), "convs_us": round(t_upd * 1e6, 1),
+                   "flops_per_iteration": fl,
+                   "timing": "HIP events around a hipGraph of 20 replays of one iteration's conv launches"}
+
+    # the dominant kernel of the step: conv_halo_kernel<3,3,64> (the update block's 3x3 convs with
+    # N >= 192 at B=1: convc2 and the flow head's conv1), flops 2*M*N*K per launch
+    dom = [l for l in it_convs if l.keep.kh == 3 and l.keep.kw == 3 and l.keep.n > 4 and l.keep.precision != 0
+           and halo_bn(l.keep.n, args.batch, h8, w8) == 64]
+    dominant = None
+    if dom:
+        dfl = sum(2 * P * l.keep.n * 9 * (l.keep.in0_c + l.keep.in1_c) for l in dom)
+        dt = time_kernel_events(lambda: [l(K.stream_handle()) for l in dom], 50)
+        dominant = {"kernel": "conv_halo_kernel<3,3,64> (convc2 and the flow-head conv1 of one iteration)",
+                    "bound": "mfma", "achieved": round(dfl / dt / 1e12, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+                    "frac": round(dfl / dt / 1e12 / peak, 4), "launches": len(dom),
+                    "launch_us": round(dt / len(dom) * 1e6, 2), "flops_per_launch": dfl // len(dom),
+                    "timing": "HIP events around a hipGraph of 50 replays of those launches"}
+        hpmc = load_pmc("r02_halo_pmc.json", "conv_halo.hip")
+        if hpmc:
+            dominant["mfma_busy"] = hpmc.get("conv_halo_kernel<3, 3, 64, 1>", {}).get("mfma_busy")
 
     exact = None
     if prec != "fp32" and world == 1 and not args.no_fp32_exact:
@@ -308,6 +353,7 @@ def main():
             "roofline": roof,
             "lookup_b8": lookup_b8,
             "update_gemm": update_roof,
+            "dominant_kernel": dominant,
             "fp32_exact": exact,
             "cpu_baseline": cpu,
         }

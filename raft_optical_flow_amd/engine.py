@@ -336,18 +336,22 @@ def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool
     flow slot of HX were filled by the lookup and plan_gru_context ran for this pair."""
     flow = Rows(ub.hx, ub.flow_off(pu), 2)
     # the flow branch (convf1 -> convf2) runs on the side stream beside the corr branch
+    # (RAFT_FLOW_SIDE=0: on the main stream, no fork / join)
+    side = os.environ.get("RAFT_FLOW_SIDE", "1") != "0"
     cf = Rows(ub.cf)
-    L.append(K.FORK)
+    if side:
+        L.append(K.FORK)
     if pu.small:
-        _conv(L, pu.convf1, flow, B, h, w, Rows(ub.flo1), epilogue=_lib.EPI_RELU, side=True)
-        _conv(L, pu.convf2, Rows(ub.flo1), B, h, w, cf.sub(96, 32), epilogue=_lib.EPI_RELU, side=True)
+        _conv(L, pu.convf1, flow, B, h, w, Rows(ub.flo1), epilogue=_lib.EPI_RELU, side=side)
+        _conv(L, pu.convf2, Rows(ub.flo1), B, h, w, cf.sub(96, 32), epilogue=_lib.EPI_RELU, side=side)
         _conv(L, pu.convc1, Rows(ub.corr), B, h, w, cf.sub(0, 96), epilogue=_lib.EPI_RELU)
     else:
-        _conv(L, pu.convf1, flow, B, h, w, Rows(ub.flo1), epilogue=_lib.EPI_RELU, side=True)
-        _conv(L, pu.convf2, Rows(ub.flo1), B, h, w, cf.sub(192, 64), epilogue=_lib.EPI_RELU, side=True)
+        _conv(L, pu.convf1, flow, B, h, w, Rows(ub.flo1), epilogue=_lib.EPI_RELU, side=side)
+        _conv(L, pu.convf2, Rows(ub.flo1), B, h, w, cf.sub(192, 64), epilogue=_lib.EPI_RELU, side=side)
         _conv(L, pu.convc1, Rows(ub.corr), B, h, w, Rows(ub.cor1), epilogue=_lib.EPI_RELU)
         _conv(L, pu.convc2, Rows(ub.cor1), B, h, w, cf.sub(0, 192), epilogue=_lib.EPI_RELU)
-    L.append(K.JOIN)
+    if side:
+        L.append(K.JOIN)
     _conv(L, pu.conv, cf, B, h, w, ub.motion(pu), epilogue=_lib.EPI_RELU)
     hd = pu.hdim
     hrows = ub.h(pu)
@@ -479,12 +483,26 @@ class RaftPlan:
         L.append(Launch("raft_flow_from_coords", ub.coords.data_ptr(), self.flow_low.data_ptr(), B, h, w))
         self.graph = None
         self.side_stream = None
+        self.runs = 0
 
     # -- execution --------------------------------------------------------
     def run(self):
         if self.side_stream is None:
             self.side_stream = torch.cuda.Stream(device=self.device)
         K.run(self.launches, self.side_stream)
+        self.runs += 1
+
+    def release(self):
+        """Drop the graph and every device buffer of the plan (it cannot run afterwards)."""
+        if self.graph is not None:
+            torch.cuda.synchronize(self.device)
+            self.graph.reset()
+            self.graph = None
+        self.launches = []
+        self.arena.bufs.clear()
+        for name in ("pyramid", "fmap", "f2levels", "ub", "img1", "img2", "flow_init", "flow_low", "flow_up"):
+            if hasattr(self, name):
+                setattr(self, name, None)
 
     def capture(self):
         """Record the whole launch list into a hipGraph (static buffers, no allocation)."""

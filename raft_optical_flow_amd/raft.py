@@ -11,10 +11,19 @@ list of `iters` upsampled flows.
 
 Execution is an engine.RaftPlan: every kernel is hand-written HIP (encoders,
 correlation build + pyramid, window lookup, update block, upsampling), the
-launch list is fixed per input shape, and with `model.hip_graph = True` the
-whole forward (including the 32-iteration loop) replays as one hipGraph.
+launch list is fixed per input shape.  The first forward of a shape runs the
+launch list eagerly; from the second one on the whole forward (including the
+32-iteration loop) is captured once and replays as one hipGraph, so unchanged
+callers (demo.py, evaluate.py) get graph replay without setting anything
+(`args.hip_graph = False`, `model.hip_graph = False` or RAFT_HIP_GRAPH=0 keep
+eager launches).  Plans live in a small LRU (RAFT_MAX_PLANS, default 2): a
+plan pins its correlation pyramid (275 MB at 440x1024) and buffers, so
+evaluate.py's many KITTI sizes do not accumulate device memory.
 """
 from __future__ import annotations
+
+import os
+from collections import OrderedDict
 
 import torch
 import torch.nn as nn
@@ -63,13 +72,14 @@ class RAFT(nn.Module):
             self.cnet = BasicEncoder(output_dim=hdim + cdim, norm_fn="batch", dropout=args.dropout)
             self.update_block = BasicUpdateBlock(self.args, hidden_dim=hdim)
         # execution state (not part of state_dict)
-        self.hip_graph = bool(getattr(args, "hip_graph", False))
+        self.hip_graph = bool(getattr(args, "hip_graph", os.environ.get("RAFT_HIP_GRAPH", "1") != "0"))
+        self.max_plans = int(os.environ.get("RAFT_MAX_PLANS", "2"))
         # conv arithmetic: "fp32" | "f16x3" | "f16"; args.mixed_precision (the
         # reference's fp16 autocast, core/raft.py:156) selects "f16"
         self.conv_precision = getattr(args, "conv_precision", None)
         self._packed = None
         self._packed_key = None
-        self._plans = {}
+        self._plans = OrderedDict()
 
     def freeze_bn(self):
         for m in self.modules():
@@ -115,7 +125,7 @@ class RAFT(nn.Module):
             with torch.no_grad():
                 self._packed = PackedRaft(self, device, _lib.PRECISIONS[prec])
             self._packed_key = key
-            self._plans = {}
+            self.release_plans()
         return self._packed
 
     def plan(self, batch, height, width, iters, test_mode=True, flow_init=False, device=None):
@@ -124,10 +134,20 @@ class RAFT(nn.Module):
         key = (batch, height, width, iters, bool(test_mode), bool(self.args.alternate_corr), bool(flow_init))
         pl = self._plans.get(key)
         if pl is None:
+            while len(self._plans) >= max(1, self.max_plans):
+                self._plans.popitem(last=False)[1].release()
             pl = RaftPlan(pk, batch, height, width, iters, test_mode=test_mode,
                           alternate=bool(self.args.alternate_corr), flow_init=flow_init, device=device)
             self._plans[key] = pl
+        else:
+            self._plans.move_to_end(key)
         return pl
+
+    def release_plans(self, keep=None):
+        """Free the cached plans' device memory and graphs (all but `keep`)."""
+        for k in list(self._plans):
+            if self._plans[k] is not keep:
+                self._plans.pop(k).release()
 
     def forward(self, image1, image2, iters=12, flow_init=None, upsample=True, test_mode=False):
         if self.training:
@@ -139,7 +159,7 @@ class RAFT(nn.Module):
         b, _, H, W = image1.shape
         pl = self.plan(b, H, W, iters, test_mode, flow_init is not None, image1.device)
         pl.set_inputs(image1, image2, flow_init)
-        if self.hip_graph:
+        if self.hip_graph and (pl.graph is not None or pl.runs > 0):
             pl.replay()
         else:
             pl.run()

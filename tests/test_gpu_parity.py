@@ -399,12 +399,31 @@ def test_raft_train_mode_output_list_and_graph_replay():
         preds = m(i1, i2, iters=12, test_mode=False)
         assert isinstance(preds, list) and len(preds) == 12
         assert maxabs(preds[-1], g["flow_up"]) < 1e-3
-        low0, up0 = m(i1, i2, iters=12, test_mode=True)
-        m.hip_graph = True
-        low1, up1 = m(i1, i2, iters=12, test_mode=True)
-        low2, up2 = m(i1, i2, iters=12, test_mode=True)
+        assert m.hip_graph  # the default: graph replay from a plan's second forward on
+        low0, up0 = m(i1, i2, iters=12, test_mode=True)   # first forward of the plan: eager
+        pl = m.plan(2, 128, 192, 12, True)
+        assert pl.graph is None and pl.runs == 1
+        low1, up1 = m(i1, i2, iters=12, test_mode=True)   # captured, replayed
+        assert pl.graph is not None
+        low2, up2 = m(i1, i2, iters=12, test_mode=True)   # replayed
     assert maxabs(low1, low0) == 0.0 and maxabs(up1, up0) == 0.0
     assert maxabs(up2, up0) == 0.0
+
+
+def test_plan_cache_is_a_bounded_lru():
+    """RAFT_MAX_PLANS (default 2) plans per model; the evicted plan's buffers and graph are freed."""
+    m, _ = make_model(False, 0)
+    x = torch.zeros(1, 3, 64, 96, device=DEV)
+    with torch.no_grad():
+        for _ in range(2):
+            m(x, x, iters=2, test_mode=True)
+        first = m.plan(1, 64, 96, 2, True)
+        assert first.graph is not None
+        m(x, x, iters=3, test_mode=True)
+        m(x, x, iters=4, test_mode=True)
+    assert len(m._plans) == 2 and first.graph is None and first.pyramid is None
+    m.release_plans()
+    assert len(m._plans) == 0
 
 
 def test_raft_flow_init_warm_start():

@@ -134,3 +134,14 @@ def test_raft_config4_shape_matches_reference():
     low, up = O.raft_forward(p, i1.numpy(), i2.numpy(), iters=32)
     assert maxabs(low, g["flow_low"]) < 1e-3
     assert maxabs(up[:, :, ::8], g["flow_up_rows8"]) < 1e-3
+
+
+def test_torch_cpu_baseline_matches_reference():
+    """oracle/torch_cpu.py (bench.py's CPU baseline) reproduces the reference's flow."""
+    import torch
+    from oracle import torch_cpu as T
+    g = load_golden("raft_full_rand_b1_128x192_i32.npz")
+    p = {k: torch.from_numpy(v) for k, v in params(False, int(g["seed"])).items()}
+    low, up = T.raft_forward(p, torch.from_numpy(g["image1"]), torch.from_numpy(g["image2"]), iters=int(g["iters"]))
+    assert maxabs(low.numpy(), g["flow_low"]) < 1e-4
+    assert maxabs(up.numpy(), g["flow_up"]) < 1e-4

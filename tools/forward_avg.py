@@ -1,0 +1,56 @@
+"""Per-dispatch averages of bench.py's roofline kernels from a rocprofv3 kernel trace of the same
+bench command, to check bench.py's live figures against rocprof:
+
+  * corr_lookup_kernel<4,4>, B=1 grid (1760 x 256 threads) and B=8 grid (14080 x 256), split into
+      - rotated: the dispatches of bench.py's cache-cold rotation graphs (runs of >= 16 consecutive
+        lookups with no other kernel between them)  -> compare with roofline / lookup_b8 launch_us
+      - in-forward: every other lookup dispatch (the 32 per forward of the timed graph replays)
+  * conv_halo_kernel<3,3,64,1> at B=1 (grids of 168 and 224 work-groups: convc2 and the flow-head
+    conv1), all dispatches                                  -> compare with dominant_kernel launch_us
+
+    python tools/forward_avg.py gpurun_out/prof_<tag>/run_kernel_trace.csv [out.json]
+"""
+import csv
+import json
+import statistics
+import sys
+
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+
+
+def dur(r):
+    return (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
+
+
+def is_lookup(r):
+    return "corr_lookup_kernel<4, 4>" in r["Kernel_Name"]
+
+
+# runs of consecutive lookup dispatches
+runs, cur = [], []
+for r in rows:
+    if is_lookup(r):
+        cur.append(r)
+    else:
+        if cur:
+            runs.append(cur)
+        cur = []
+if cur:
+    runs.append(cur)
+res = {}
+for grid, tag in ((1760 * 256, "B=1"), (14080 * 256, "B=8")):
+    rot = [dur(r) for run in runs if len(run) >= 16 for r in run if int(r["Grid_Size_X"]) == grid]
+    fwd = [dur(r) for run in runs if len(run) < 16 for r in run if int(r["Grid_Size_X"]) == grid]
+    for name, v in (("rotated", rot), ("in-forward", fwd)):
+        if v:
+            res[f"corr_lookup {tag} {name}"] = {"dispatches": len(v), "mean_us": round(statistics.mean(v), 3),
+                                                 "median_us": round(statistics.median(v), 3)}
+h = [dur(r) for r in rows if "conv_halo_kernel<3, 3, 64, 1>" in r["Kernel_Name"]
+     and int(r["Grid_Size_X"]) in (168 * 512, 224 * 512)]
+if h:
+    res["conv_halo_kernel<3,3,64,1> B=1 (convc2 + fh1)"] = {"dispatches": len(h), "mean_us": round(statistics.mean(h), 3),
+                                                           "median_us": round(statistics.median(h), 3)}
+for k, v in res.items():
+    print(f"{k:50s} {v['dispatches']:6d} dispatches  mean {v['mean_us']:8.2f} us  median {v['median_us']:8.2f} us")
+if len(sys.argv) > 2:
+    json.dump(res, open(sys.argv[2], "w"), indent=1)
