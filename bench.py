@@ -122,7 +122,7 @@ def rotated_lookup(plan, batch, h8, w8, nrot, reps):
     def fn():
         for k in range(nrot):
             _lib.call("raft_corr_lookup", pyrs[k].data_ptr(), batch, h8, w8, L, r, coords.data_ptr(), 0,
-                      out.data_ptr(), ntap, 0, None, 0, K.stream_handle())
+                      out.data_ptr(), ntap, 0, None, 0, None, K.stream_handle())
 
     t = time_kernel_events(fn, reps) / nrot
     del pyrs

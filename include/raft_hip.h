@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RAFT_HIP_ABI_VERSION 4
+#define RAFT_HIP_ABI_VERSION 5
 
 /* Negative return codes (argument errors, raised before any launch). */
 #define RAFT_E_INVALID (-1)   /* bad size / null pointer / unsupported shape */
@@ -83,10 +83,12 @@ int raft_corr_pyramid_level(const float* pyramid, int B, int H, int W, int num_l
  * out: out_layout 0 = NHWC rows [B*H*W][out_ld], channel lvl*(2r+1)^2 + ix*(2r+1) + iy;
  *      out_layout 1 = NCHW [B][L*(2r+1)^2][H][W] (out_ld ignored).
  * flow_out (optional, may be NULL): NHWC rows [B*H*W][flow_ld] receive
- *      coords - coords_grid (the RAFT loop's `flow`, core/raft.py:222). */
+ *      coords - coords_grid (the RAFT loop's `flow`, core/raft.py:222).
+ * range_flag (optional, may be NULL): set to 1 when an output exceeds RAFT_RANGE_LIMIT in
+ *      magnitude (see the f16x3 range guard below). */
 int raft_corr_lookup(const float* pyramid, int B, int H, int W, int num_levels, int radius,
                      const float* coords, int coords_layout, float* out, int out_ld, int out_layout,
-                     float* flow_out, int flow_ld, raft_stream_t stream);
+                     float* flow_out, int flow_ld, int* range_flag, raft_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * On-the-fly ("alternate") correlation — the alt_cuda_corr plugin.
@@ -104,11 +106,12 @@ int raft_alt_corr_forward(const float* fmap1, const float* fmap2, const float* c
 
 /* Same computation, NHWC output: out rows [B*H1*W1][out_ld] at channel
  * offset already applied by the caller; coords_layout as raft_corr_lookup
- * (coordinates are divided by coord_div before use: 2**level in RAFT). */
+ * (coordinates are divided by coord_div before use: 2**level in RAFT);
+ * range_flag as raft_corr_lookup. */
 int raft_alt_corr_lookup_nhwc(const float* fmap1, const float* fmap2, const float* coords, int coords_layout,
                               float coord_div, float* out, int out_ld, int B, int H1, int W1, int H2, int W2,
                               int C, int radius, float scale_div, float* flow_out, int flow_ld,
-                              raft_stream_t stream);
+                              int* range_flag, raft_stream_t stream);
 
 /* Gradients of raft_alt_corr_forward (unscaled), like correlation_kernel.cu:122-256:
  * fmap1_grad is a deterministic gather; fmap2_grad is accumulated with float
@@ -192,7 +195,18 @@ typedef struct raft_conv2d_params {
                                                (a precomputed partial sum, e.g. the GRU's
                                                iteration-invariant context term) */
   int precision;                            /* RAFT_PREC_* (weight format follows it) */
+  int* range_flag;                          /* optional (NULL = off): set to 1 when an output
+                                               exceeds RAFT_RANGE_LIMIT in magnitude */
 } raft_conv2d_params;
+
+/* f16x3 range guard.  RAFT_PREC_F16X3 splits every activation x as hi = f16(x), which is
+ * only exact for |x| < 65504: a larger conv input would silently become inf.  Producers
+ * whose outputs feed a split-precision conv (conv epilogues, the correlation lookups) can
+ * raise a device flag when any output exceeds RAFT_RANGE_LIMIT = 2^15 (NaN does not raise
+ * it: a NaN input propagates as in fp32); the caller checks the flag after the forward and
+ * re-runs it with RAFT_PREC_FP32 (or raises).  InstanceNorm outputs are bounded by
+ * sqrt(H*W) and the prepared images by 1, so they need no flag. */
+#define RAFT_RANGE_LIMIT 32768.0f
 
 /* Packed weight geometry for a conv (n_pad, k_pad in floats per row). */
 int raft_conv2d_packed_shape(int mode, int n, int kh, int kw, int cin, int* n_pad, int* k_pad);

@@ -29,7 +29,8 @@ PREC_F16 = 2     # single f16 product (mixed precision)
 PREC_BF16 = 3    # single bf16 product on v_mfma_f32_32x32x16_bf16 (bf16 mixed precision)
 PRECISIONS = {"fp32": PREC_FP32, "f16x3": PREC_F16X3, "f16": PREC_F16, "bf16": PREC_BF16}
 
-ABI_VERSION = 4
+ABI_VERSION = 5
+RANGE_LIMIT = 32768.0  # RAFT_RANGE_LIMIT: |x| above it raises the f16x3 range guard
 
 EPI_LINEAR = 0
 EPI_RELU = 1
@@ -59,6 +60,7 @@ class ConvParams(ctypes.Structure):
         ("out1", P), ("out1_ld", c_int),
         ("add0", P), ("add0_ld", c_int),
         ("precision", c_int),
+        ("range_flag", P),
     ]
 
 
@@ -71,10 +73,10 @@ _PROTOS = {
     "raft_corr_build": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, P, P]),
     "raft_corr_build_prec": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, P, P]),
     "raft_corr_pyramid_level": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
-    "raft_corr_lookup": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, c_int, c_int, P, c_int, P]),
+    "raft_corr_lookup": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, c_int, c_int, P, c_int, P, P]),
     "raft_alt_corr_forward": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, P]),
     "raft_alt_corr_lookup_nhwc": (c_int, [P, P, P, c_int, c_float, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                                          c_int, c_float, P, c_int, P]),
+                                          c_int, c_float, P, c_int, P, P]),
     "raft_alt_corr_backward": (c_int, [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                        P, c_size_t, P]),
     "raft_alt_corr_backward_workspace_floats": (c_size_t, [c_int] * 8),

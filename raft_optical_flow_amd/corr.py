@@ -64,7 +64,7 @@ class CorrBlock:
         r = self.radius
         out = torch.empty(b, self.num_levels * (2 * r + 1) ** 2, h, w, device=coords.device)
         _lib.call("raft_corr_lookup", self.pyramid_flat.data_ptr(), b, h, w, self.num_levels, r, coords.data_ptr(), 1,
-                  out.data_ptr(), 0, 1, None, 0, K.stream_handle())
+                  out.data_ptr(), 0, 1, None, 0, None, K.stream_handle())
         return out
 
     @staticmethod
@@ -118,5 +118,5 @@ class AlternateCorrBlock:
         for i in range(self.num_levels):
             f2, hh, ww = self._f2[i]
             _lib.call("raft_alt_corr_lookup_nhwc", f1.data_ptr(), f2.data_ptr(), coords.data_ptr(), 1, float(2 ** i),
-                      out.data_ptr() + 4 * i * nb, out.shape[1], b, h, w, hh, ww, self.dim, r, div, None, 0, s)
+                      out.data_ptr() + 4 * i * nb, out.shape[1], b, h, w, hh, ww, self.dim, r, div, None, 0, None, s)
         return K.rows_to_nchw(K.Rows(out), b, h, w)

@@ -32,6 +32,7 @@ struct AltArgs {
   float scale_div;
   float* flow;
   int flow_ld;
+  int* range_flag;  // f16x3 range guard (raft_hip.h), or null
 };
 
 // Partial dot product of one tap: this lane's channel quads of fmap1[p] (registers)
@@ -195,6 +196,7 @@ __device__ __forceinline__ void alt_pixel(const AltArgs& a, long gid, bool valid
     val += s10 * (dy * (1.f - dx));
     val += s11 * (dy * dx);
     val = val / a.scale_div;
+    if (a.range_flag && fabsf(val) > RAFT_RANGE_LIMIT) *a.range_flag = 1;
     if (a.out_layout == 0)
       a.out[(bn * (rd * rd) + o) * P1 + p] = val;
     else
@@ -259,6 +261,7 @@ __device__ __forceinline__ void alt_bin_store(const AltArgs& a, long bn, int p, 
   val += s10 * (dy * (1.f - dx));
   val += s11 * (dy * dx);
   val = val / a.scale_div;
+  if (a.range_flag && fabsf(val) > RAFT_RANGE_LIMIT) *a.range_flag = 1;
   if (a.out_layout == 0)
     a.out[(bn * (rd * rd) + o) * P1 + p] = val;
   else
@@ -542,13 +545,14 @@ extern "C" int raft_alt_corr_forward(const float* fmap1, const float* fmap2, con
   a.scale_div = scale_div;
   a.flow = nullptr;
   a.flow_ld = 0;
+  a.range_flag = nullptr;
   return launch_alt(a, stream);
 }
 
 extern "C" int raft_alt_corr_lookup_nhwc(const float* fmap1, const float* fmap2, const float* coords,
                                          int coords_layout, float coord_div, float* out, int out_ld, int B, int H1,
                                          int W1, int H2, int W2, int C, int radius, float scale_div, float* flow_out,
-                                         int flow_ld, raft_stream_t stream) {
+                                         int flow_ld, int* range_flag, raft_stream_t stream) {
   int rc = alt_checks(fmap1, fmap2, coords, out, B, H1, W1, H2, W2, C, 1, radius);
   if (rc) return rc;
   RAFT_REQUIRE(coords_layout == 0 || coords_layout == 1, "raft_alt_corr_lookup_nhwc: bad coords_layout");
@@ -574,6 +578,7 @@ extern "C" int raft_alt_corr_lookup_nhwc(const float* fmap1, const float* fmap2,
   a.scale_div = scale_div;
   a.flow = flow_out;
   a.flow_ld = flow_ld;
+  a.range_flag = range_flag;
   return launch_alt(a, stream);
 }
 

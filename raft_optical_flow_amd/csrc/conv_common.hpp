@@ -164,6 +164,12 @@ __device__ __forceinline__ void tile_epilogue(const raft_conv2d_params& p, const
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] += t[r];
   }
+  if (p.range_flag) {  // f16x3 range guard (raft_hip.h): out-of-range outputs raise the flag
+    bool big = false;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) big |= ncol && rows[r] >= 0 && fabsf(v[r]) > RAFT_RANGE_LIMIT;
+    if (big) *p.range_flag = 1;
+  }
 #pragma unroll
   for (int r = 0; r < 16; ++r)
     if (ncol && rows[r] >= 0) dst[eidx(rows[r], ld, col)] = v[r];

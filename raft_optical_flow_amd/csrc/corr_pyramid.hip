@@ -263,6 +263,7 @@ struct LookupArgs {
   int out_ld, out_layout;
   float* flow;
   int flow_ld;
+  int* range_flag;  // f16x3 range guard (raft_hip.h), or null
   // per level: W-1, H-1 and their reciprocals, rounded on the host exactly as
   // the device's correctly rounded 1.0f / x would
   float wm1[LK_MAXL], hm1[LK_MAXL], rw[LK_MAXL], rh[LK_MAXL];
@@ -508,6 +509,12 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
     }
   }
   LK_STAMP(4);
+  if (a.range_flag && col) {  // f16x3 range guard: the output feeds the split-precision convc1
+    bool big = false;
+#pragma unroll
+    for (int iy = 0; iy < RD; ++iy) big |= fabsf(val[iy]) > RAFT_RANGE_LIMIT;
+    if (big) *a.range_flag = 1;
+  }
 #ifdef LK_ABL_NOSTORE  // timing ablation (dev builds only): no output stores
   if (val[0] != -12345.f) return;
 #endif
@@ -667,7 +674,7 @@ extern "C" int raft_corr_pyramid_level(const float* pyramid, int B, int H, int W
 
 extern "C" int raft_corr_lookup(const float* pyramid, int B, int H, int W, int L, int radius, const float* coords,
                                 int coords_layout, float* out, int out_ld, int out_layout, float* flow_out,
-                                int flow_ld, raft_stream_t stream) {
+                                int flow_ld, int* range_flag, raft_stream_t stream) {
   RAFT_REQUIRE(pyramid && coords && out, "raft_corr_lookup: null pointer");
   RAFT_REQUIRE(B > 0 && H > 0 && W > 0 && L >= 1 && L <= LK_MAXL, "raft_corr_lookup: bad sizes");
   RAFT_REQUIRE(radius >= 1 && radius <= 4, "raft_corr_lookup: radius must be 1..4 (got %d)", radius);
@@ -702,6 +709,7 @@ extern "C" int raft_corr_lookup(const float* pyramid, int B, int H, int W, int L
   a.out_layout = out_layout;
   a.flow = flow_out;
   a.flow_ld = flow_ld;
+  a.range_flag = range_flag;
   dim3 grid((unsigned)cdiv_l((long)B * H * W, 4));
   hipStream_t s = as_stream(stream);
   // the 4-level case (RAFT) gets a tight instantiation; other level counts use LMAX = 6

@@ -186,7 +186,13 @@ def _in_apply(L, A: Arena, x: Rows, st, n_img, hw, mode, resid: Rows | None = No
     return out
 
 
+# the f16x3 range guard's device flag of the plan being built (RaftPlan.__init__ sets it):
+# every conv whose output feeds a split-precision conv raises it on |x| > 2^15 (raft_hip.h)
+_GUARD = {"flag": None}
+
+
 def _conv(L, pc: PackedConv, src: Rows, n_img, h, w, out: Rows, side=False, **kw):
+    kw.setdefault("range_flag", _GUARD["flag"])
     L.append(conv_launch(conv_params(pc, src, n_img, h, w, out, **kw), side=side))
 
 
@@ -373,7 +379,9 @@ def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool
             _conv(L, pu.fh1, hrows, B, h, w, fh.sub(0, 256), epilogue=_lib.EPI_RELU)
         _conv(L, pu.fh2, fh.sub(0, 256), B, h, w, coords, epilogue=_lib.EPI_ADD_TO_OUT)
         if with_mask:
-            _conv(L, pu.mask2, fh.sub(256, 256), B, h, w, Rows(ub.mask), epilogue=_lib.EPI_LINEAR, alpha=0.25)
+            # the mask feeds only the fp32 softmax of the upsampling: no range guard
+            _conv(L, pu.mask2, fh.sub(256, 256), B, h, w, Rows(ub.mask), epilogue=_lib.EPI_LINEAR, alpha=0.25,
+                  range_flag=None)
 
 
 # ----------------------------------------------------------------------------
@@ -391,6 +399,20 @@ class RaftPlan:
         self.pk, self.B, self.H, self.W, self.iters = pk, B, H, W, iters
         self.test_mode, self.alternate = test_mode, alternate
         self.device = device
+        # f16x3 range guard flag (raft_hip.h): raised by the convs and lookups whose outputs
+        # feed split-precision convs; RAFT.forward checks it after the forward
+        self.guarded = pk.precision == _lib.PREC_F16X3
+        self.range_flag = torch.zeros(1, dtype=torch.int32, device=device)
+        _GUARD["flag"] = self.range_flag if self.guarded else None
+        try:
+            self._build(pk, B, H, W, iters, test_mode, alternate, flow_init, device)
+        finally:
+            _GUARD["flag"] = None
+        self.graph = None
+        self.side_stream = None
+        self.runs = 0
+
+    def _build(self, pk, B, H, W, iters, test_mode, alternate, flow_init, device):
         A = self.arena = Arena(device)
         L = self.launches = []
         h, w = H // 8, W // 8
@@ -458,17 +480,18 @@ class RaftPlan:
         self.loop_start = len(L)
         self.flow_up = [torch.empty(B, 2, H, W, device=device) for _ in range(1 if test_mode else iters)]
         flow_slot = ub.flow_off(pu)
+        gflag = self.range_flag.data_ptr() if self.guarded else None
         for it in range(iters):
             last = it == iters - 1
             if not alternate:
                 L.append(Launch("raft_corr_lookup", self.pyramid.data_ptr(), B, h, w, lv, r, ub.coords.data_ptr(), 0,
-                                ub.corr.data_ptr(), corr_ld, 0, ub.hx.data_ptr() + 4 * flow_slot, pu.ld))
+                                ub.corr.data_ptr(), corr_ld, 0, ub.hx.data_ptr() + 4 * flow_slot, pu.ld, gflag))
             else:
                 for i, (f2, hh, ww) in enumerate(self.f2levels):
                     fl = ub.hx.data_ptr() + 4 * flow_slot if i == 0 else None
                     L.append(Launch("raft_alt_corr_lookup_nhwc", fmap1.data_ptr(), f2.data_ptr(), ub.coords.data_ptr(),
                                     0, float(2 ** i), ub.corr.data_ptr() + 4 * i * (2 * r + 1) ** 2, corr_ld,
-                                    B, h, w, hh, ww, C, r, div, fl, pu.ld))
+                                    B, h, w, hh, ww, C, r, div, fl, pu.ld, gflag))
             want_up = last or not test_mode
             plan_update(L, pu, ub, B, h, w, with_mask=want_up and not pu.small)
             if want_up:
@@ -481,9 +504,6 @@ class RaftPlan:
         self.loop_end = len(L)
         self.flow_low = torch.empty(B, 2, h, w, device=device)
         L.append(Launch("raft_flow_from_coords", ub.coords.data_ptr(), self.flow_low.data_ptr(), B, h, w))
-        self.graph = None
-        self.side_stream = None
-        self.runs = 0
 
     # -- execution --------------------------------------------------------
     def run(self):
@@ -500,7 +520,8 @@ class RaftPlan:
             self.graph = None
         self.launches = []
         self.arena.bufs.clear()
-        for name in ("pyramid", "fmap", "f2levels", "ub", "img1", "img2", "flow_init", "flow_low", "flow_up"):
+        for name in ("pyramid", "fmap", "f2levels", "ub", "img1", "img2", "flow_init", "flow_low", "flow_up",
+                     "range_flag"):
             if hasattr(self, name):
                 setattr(self, name, None)
 

@@ -179,7 +179,7 @@ def fold_bn(weight, bias, bn: torch.nn.BatchNorm2d):
 def conv_params(pc: PackedConv, src0: Rows, batch: int, in_h: int, in_w: int, out: Rows,
                 epilogue=_lib.EPI_LINEAR, src1: Rows | None = None, alpha=1.0, split=0,
                 aux0: Rows | None = None, aux1: Rows | None = None, out1: Rows | None = None,
-                add0: Rows | None = None) -> ConvParams:
+                add0: Rows | None = None, range_flag: torch.Tensor | None = None) -> ConvParams:
     """Build (and validate shapes of) a raft_conv2d_params for one launch."""
     sh, sw = pc.stride
     ph, pw = pc.pad
@@ -215,6 +215,8 @@ def conv_params(pc: PackedConv, src0: Rows, batch: int, in_h: int, in_w: int, ou
         p.out1, p.out1_ld = out1.ptr, out1.ld
     if add0 is not None:
         p.add0, p.add0_ld = add0.ptr, add0.ld
+    if range_flag is not None and p.precision == _lib.PREC_F16X3:
+        p.range_flag = range_flag.data_ptr()
     return p
 
 

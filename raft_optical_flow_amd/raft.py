@@ -19,10 +19,17 @@ callers (demo.py, evaluate.py) get graph replay without setting anything
 eager launches).  Plans live in a small LRU (RAFT_MAX_PLANS, default 2): a
 plan pins its correlation pyramid (275 MB at 440x1024) and buffers, so
 evaluate.py's many KITTI sizes do not accumulate device memory.
+
+f16x3 range guard: the default fp32-accurate split arithmetic holds only while every
+conv input stays below 65504 in magnitude (include/raft_hip.h).  The convs and lookups
+whose outputs feed split convs raise a device flag above 2^15; forward() checks it and
+re-runs that forward on exact f32 MFMA with a warning (`model.range_guard = "raise"`
+raises FloatingPointError instead; "off" skips the check; env RAFT_RANGE_GUARD).
 """
 from __future__ import annotations
 
 import os
+import warnings
 from collections import OrderedDict
 
 import torch
@@ -74,11 +81,11 @@ class RAFT(nn.Module):
         # execution state (not part of state_dict)
         self.hip_graph = bool(getattr(args, "hip_graph", os.environ.get("RAFT_HIP_GRAPH", "1") != "0"))
         self.max_plans = int(os.environ.get("RAFT_MAX_PLANS", "2"))
+        self.range_guard = os.environ.get("RAFT_RANGE_GUARD", "fallback")
         # conv arithmetic: "fp32" | "f16x3" | "f16"; args.mixed_precision (the
         # reference's fp16 autocast, core/raft.py:156) selects "f16"
         self.conv_precision = getattr(args, "conv_precision", None)
-        self._packed = None
-        self._packed_key = None
+        self._packed = {}           # precision -> (weights key, PackedRaft)
         self._plans = OrderedDict()
 
     def freeze_bn(self):
@@ -117,21 +124,26 @@ class RAFT(nn.Module):
             raise ValueError(f"conv_precision must be one of {sorted(_lib.PRECISIONS)}, got {prec!r}")
         return prec
 
-    def packed(self, device):
+    def packed(self, device, prec=None):
         from . import _lib
-        prec = self.resolved_precision()
-        key = (self._weights_key(), str(device), prec)
-        if self._packed is None or self._packed_key != key:
+        prec = prec or self.resolved_precision()
+        key = (self._weights_key(), str(device))
+        got = self._packed.get(prec)
+        if got is None or got[0] != key:
+            if got is not None or any(k != key for k, _ in self._packed.values()):
+                # new weights (or device): every packed form and plan is stale
+                self._packed.clear()
+                self.release_plans()
             with torch.no_grad():
-                self._packed = PackedRaft(self, device, _lib.PRECISIONS[prec])
-            self._packed_key = key
-            self.release_plans()
-        return self._packed
+                got = (key, PackedRaft(self, device, _lib.PRECISIONS[prec]))
+            self._packed[prec] = got
+        return got[1]
 
-    def plan(self, batch, height, width, iters, test_mode=True, flow_init=False, device=None):
+    def plan(self, batch, height, width, iters, test_mode=True, flow_init=False, device=None, prec=None):
         device = device or next(self.parameters()).device
-        pk = self.packed(device)
-        key = (batch, height, width, iters, bool(test_mode), bool(self.args.alternate_corr), bool(flow_init))
+        prec = prec or self.resolved_precision()
+        pk = self.packed(device, prec)
+        key = (batch, height, width, iters, bool(test_mode), bool(self.args.alternate_corr), bool(flow_init), prec)
         pl = self._plans.get(key)
         if pl is None:
             while len(self._plans) >= max(1, self.max_plans):
@@ -149,7 +161,7 @@ class RAFT(nn.Module):
             if self._plans[k] is not keep:
                 self._plans.pop(k).release()
 
-    def forward(self, image1, image2, iters=12, flow_init=None, upsample=True, test_mode=False):
+    def forward(self, image1, image2, iters=12, flow_init=None, upsample=True, test_mode=False, _prec=None):
         if self.training:
             raise NotImplementedError("raft_optical_flow_amd.RAFT is an inference path: call model.eval() "
                                       "(training / BatchNorm batch statistics are out of scope)")
@@ -157,10 +169,20 @@ class RAFT(nn.Module):
         if image1.shape != image2.shape or image1.dim() != 4 or image1.shape[1] != 3:
             raise ValueError(f"images must both be [N, 3, H, W], got {tuple(image1.shape)} / {tuple(image2.shape)}")
         b, _, H, W = image1.shape
-        pl = self.plan(b, H, W, iters, test_mode, flow_init is not None, image1.device)
+        pl = self.plan(b, H, W, iters, test_mode, flow_init is not None, image1.device, prec=_prec)
         pl.set_inputs(image1, image2, flow_init)
+        guard = pl.guarded and self.range_guard != "off"
+        if guard:
+            pl.range_flag.zero_()
         if self.hip_graph and (pl.graph is not None or pl.runs > 0):
             pl.replay()
         else:
             pl.run()
+        if guard and int(pl.range_flag.item()):
+            msg = ("f16x3 range guard: an activation exceeded 2^15 in magnitude, outside the exact range "
+                   "of the split-f16 conv arithmetic")
+            if self.range_guard == "raise":
+                raise FloatingPointError(msg)
+            warnings.warn(msg + "; this forward was re-run with exact f32 MFMA convs", RuntimeWarning)
+            return self.forward(image1, image2, iters, flow_init, upsample, test_mode, _prec="fp32")
         return pl.outputs(clone=True)

@@ -147,7 +147,7 @@ def test_config3_alt_kernel_on_run_coords_vs_oracle(sigma):
     for lvl, (f2_dev, hh, ww) in enumerate(pl.f2levels):
         out = torch.empty(B * h * w, nb, device=DEV)
         _lib.call("raft_alt_corr_lookup_nhwc", f1_dev.data_ptr(), f2_dev.data_ptr(), ct.data_ptr(), 0,
-                  float(2 ** lvl), out.data_ptr(), nb, B, h, w, hh, ww, C, r, 1.0, None, 0, K.stream_handle())
+                  float(2 ** lvl), out.data_ptr(), nb, B, h, w, hh, ww, C, r, 1.0, None, 0, None, K.stream_handle())
         torch.cuda.synchronize()
         got = out.cpu().numpy().reshape(B, h * w, nb)
         f2 = f2_dev.cpu().numpy().reshape(B, hh, ww, C)

@@ -185,7 +185,7 @@ def test_alt_corr_tiled_vs_oracle(layout):
         out = torch.empty(B * H1 * W1, 81, device=DEV)
         f1t, f2t, ct = t(f1), t(f2), t(coords)
         _lib.call("raft_alt_corr_lookup_nhwc", f1t.data_ptr(), f2t.data_ptr(), ct.data_ptr(), 0, 1.0, out.data_ptr(),
-                  81, B, H1, W1, H2, W2, C, r, 8.0, None, 0, K.stream_handle())
+                  81, B, H1, W1, H2, W2, C, r, 8.0, None, 0, None, K.stream_handle())
         torch.cuda.synchronize()
         got = out.reshape(B, H1, W1, 81).permute(0, 3, 1, 2).cpu().numpy()
         assert maxabs(got, ref[:, 0] / 8.0) < 2e-5
@@ -490,3 +490,47 @@ def test_raft_small_demo_frames_golden():
         low, up = m(i1, i2, iters=12, test_mode=True)
     assert maxabs(low, g["flow_low"]) < 1e-3
     assert maxabs(up[:, :, ::4], g["flow_up_rows4"]) < 1e-3
+
+
+def test_f16x3_range_guard_falls_back_to_fp32():
+    """Activations beyond f16's range (fnet head scaled so |fmap| ~ 1e5 > 65504): the split-f16
+    arithmetic alone would turn them into inf; the range guard (raft_hip.h, RAFT_RANGE_LIMIT) is
+    raised by the fnet head's epilogue and the lookups, and RAFT.forward re-runs the forward on
+    exact f32 MFMA (same result as conv_precision="fp32"), raises with range_guard="raise", and
+    with the guard off shows the hole it closes."""
+    import warnings
+    g = load_golden("raft_full_rand_b1_128x192_i32.npz")
+    m, _ = make_model(False, 0)
+    with torch.no_grad():
+        m.fnet.conv2.weight.mul_(20000.0)
+        m.fnet.conv2.bias.mul_(20000.0)
+    i1, i2 = t(g["image1"]), t(g["image2"])
+    ref_m, _ = make_model(False, 0, precision="fp32")
+    ref_m.load_state_dict(m.state_dict())
+    with torch.no_grad():
+        fm = ref_m.fnet(i1)
+        assert float(fm.abs().max()) > 65504.0
+        rlow, rup = ref_m(i1, i2, iters=4, test_mode=True)
+        with pytest.warns(RuntimeWarning, match="range guard"):
+            low, up = m(i1, i2, iters=4, test_mode=True)
+        assert maxabs(low, rlow) == 0.0 and maxabs(up, rup) == 0.0
+        m.range_guard = "raise"
+        with pytest.raises(FloatingPointError):
+            m(i1, i2, iters=4, test_mode=True)
+        m.range_guard = "off"
+        with warnings.catch_warnings():
+            warnings.simplefilter("error")
+            low_off, up_off = m(i1, i2, iters=4, test_mode=True)
+    assert not bool(torch.isfinite(up_off).all()) or maxabs(up_off, rup) > 1e-3
+
+
+def test_range_guard_quiet_in_range():
+    """In range (the random-init model, |x| < 2^15 everywhere) the flag stays clear: no warning."""
+    import warnings
+    g = load_golden("raft_full_rand_b1_128x192_i32.npz")
+    m, _ = make_model(False, 0)
+    with torch.no_grad(), warnings.catch_warnings():
+        warnings.simplefilter("error")
+        m(t(g["image1"]), t(g["image2"]), iters=4, test_mode=True)
+    pl = m.plan(1, 128, 192, 4, True)
+    assert pl.guarded and int(pl.range_flag.item()) == 0

@@ -32,7 +32,7 @@ def run():
     s = K.stream_handle()
     for l in range(L):
         _lib.call("raft_alt_corr_lookup_nhwc", f1.data_ptr(), f2s[l].data_ptr(), coords.data_ptr(), 0, float(2 ** l),
-                  out.data_ptr() + 4 * l * 81, ntap, B, h, w, h >> l, w >> l, C, r, 16.0, None, 0, s)
+                  out.data_ptr() + 4 * l * 81, ntap, B, h, w, h >> l, w >> l, C, r, 16.0, None, 0, None, s)
 
 
 run()

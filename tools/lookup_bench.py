@@ -30,7 +30,7 @@ flow = torch.empty(B * h * w, 2, device=dev)
 
 def lookup():
     _lib.call("raft_corr_lookup", pyr.data_ptr(), B, h, w, L, r, coords.data_ptr(), 0, out.data_ptr(), L * 81, 0,
-              flow.data_ptr(), 2, s)
+              flow.data_ptr(), 2, None, s)
 
 
 calib_src = torch.randn(64 * 1024 * 1024 // 4, device=dev)  # 64 MiB, read once per launch
