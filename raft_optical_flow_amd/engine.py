@@ -48,30 +48,38 @@ def _conv_bn(conv, bn, device, **kw):
     return pack_conv(w, b, conv.stride, conv.padding, device=device, **kw)
 
 
+def check_norm(norm):
+    if norm not in ("instance", "batch", "none"):
+        raise NotImplementedError(f"norm_fn={norm!r} is not on the RAFT inference path")
+
+
+def pack_block(blk, norm, small, device) -> dict:
+    """One ResidualBlock (core/extractor.py:6-56) / BottleneckBlock (:60-116), eval BatchNorm folded."""
+    bn = (lambda m: m) if norm == "batch" else (lambda m: None)
+    d = {"stride": blk.conv1.stride[0] if not small else blk.conv2.stride[0]}
+    d["conv1"] = _conv_bn(blk.conv1, bn(blk.norm1), device)
+    d["conv2"] = _conv_bn(blk.conv2, bn(blk.norm2), device)
+    if small:
+        d["conv3"] = _conv_bn(blk.conv3, bn(blk.norm3), device)
+        dsn = getattr(blk, "norm4", None)
+    else:
+        dsn = getattr(blk, "norm3", None)
+    d["ds"] = None if blk.downsample is None else _conv_bn(blk.downsample[0], bn(dsn), device)
+    d["planes"] = d["conv3" if small else "conv2"].n
+    return d
+
+
 class PackedEncoder:
     """BasicEncoder (core/extractor.py:118-192) / SmallEncoder (:195-267) weights, packed."""
 
     def __init__(self, enc, device):
         self.norm = enc.norm_fn
-        if self.norm not in ("instance", "batch", "none"):
-            raise NotImplementedError(f"norm_fn={self.norm!r} is not on the RAFT inference path")
+        check_norm(self.norm)
         self.small = enc.__class__.__name__ == "SmallEncoder"
         bn = (lambda m: m) if self.norm == "batch" else (lambda m: None)
         self.stem = _conv_bn(enc.conv1, bn(enc.norm1), device, mode=_lib.RAFT_CONV_GATHER)
-        self.blocks = []
-        for layer in (enc.layer1, enc.layer2, enc.layer3):
-            for blk in layer:
-                d = {"stride": blk.conv1.stride[0] if not self.small else blk.conv2.stride[0]}
-                d["conv1"] = _conv_bn(blk.conv1, bn(blk.norm1), device)
-                d["conv2"] = _conv_bn(blk.conv2, bn(blk.norm2), device)
-                if self.small:
-                    d["conv3"] = _conv_bn(blk.conv3, bn(blk.norm3), device)
-                    dsn = getattr(blk, "norm4", None)
-                else:
-                    dsn = getattr(blk, "norm3", None)
-                d["ds"] = None if blk.downsample is None else _conv_bn(blk.downsample[0], bn(dsn), device)
-                d["planes"] = d["conv3" if self.small else "conv2"].n
-                self.blocks.append(d)
+        self.blocks = [pack_block(blk, self.norm, self.small, device)
+                       for layer in (enc.layer1, enc.layer2, enc.layer3) for blk in layer]
         self.head = pack_conv(enc.conv2.weight, enc.conv2.bias, 1, 0, device=device)
 
 

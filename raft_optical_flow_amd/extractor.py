@@ -28,9 +28,34 @@ def _norm(norm_fn, planes, groups=None):
     raise ValueError(norm_fn)
 
 
-class ResidualBlock(nn.Module):
+class _BlockBase(nn.Module):
+    """Shared forward of ResidualBlock / BottleneckBlock on the HIP path (engine._plan_residual /
+    _plan_bottleneck: the encoders' own launch sequence, BatchNorm folded, InstanceNorm as
+    stats + apply kernels)."""
+    _small = False
+
+    def forward(self, x):
+        from types import SimpleNamespace
+
+        from .engine import Arena, _plan_bottleneck, _plan_residual, check_norm, pack_block
+        if self.training and isinstance(self.norm1, nn.BatchNorm2d):
+            raise NotImplementedError("raft_optical_flow_amd blocks are inference-only: call .eval()")
+        check_norm(self.norm_fn)
+        K.require_device(x)
+        n, c, h, w = x.shape
+        d = K.cached_pack(self, x.device, lambda: pack_block(self, self.norm_fn, self._small, x.device))
+        pe = SimpleNamespace(norm=self.norm_fn, small=self._small)
+        L, A = [], Arena(x.device)
+        plan = _plan_bottleneck if self._small else _plan_residual
+        y, ho, wo = plan(L, A, pe, d, Rows(K.nchw_to_rows(x)), n, h, w)
+        K.run(L)
+        return K.rows_to_nchw(y, n, ho, wo)
+
+
+class ResidualBlock(_BlockBase):
     def __init__(self, in_planes, planes, norm_fn="group", stride=1):
         super().__init__()
+        self.norm_fn = norm_fn
         self.conv1 = nn.Conv2d(in_planes, planes, kernel_size=3, padding=1, stride=stride)
         self.conv2 = nn.Conv2d(planes, planes, kernel_size=3, padding=1)
         self.relu = nn.ReLU(inplace=True)
@@ -43,9 +68,12 @@ class ResidualBlock(nn.Module):
             nn.Conv2d(in_planes, planes, kernel_size=1, stride=stride), self.norm3)
 
 
-class BottleneckBlock(nn.Module):
+class BottleneckBlock(_BlockBase):
+    _small = True
+
     def __init__(self, in_planes, planes, norm_fn="group", stride=1):
         super().__init__()
+        self.norm_fn = norm_fn
         self.conv1 = nn.Conv2d(in_planes, planes // 4, kernel_size=1, padding=0)
         self.conv2 = nn.Conv2d(planes // 4, planes // 4, kernel_size=3, padding=1, stride=stride)
         self.conv3 = nn.Conv2d(planes // 4, planes, kernel_size=1, padding=0)
@@ -73,7 +101,7 @@ class _EncoderBase(nn.Module):
             x = torch.cat(x, dim=0)
         K.require_device(x)
         n, c, h, w = x.shape
-        pe = PackedEncoder(self, x.device)
+        pe = K.cached_pack(self, x.device, lambda: PackedEncoder(self, x.device))
         A = Arena(x.device)
         L = []
         src = Rows(K.nchw_to_rows(x))

@@ -273,6 +273,31 @@ def run(launches, side_stream: torch.cuda.Stream | None = None):
 # ----------------------------------------------------------------------------
 
 
+def module_precision(mod) -> str:
+    """Conv arithmetic of a block-level call: `mod.conv_precision` if set, else exact fp32."""
+    prec = getattr(mod, "conv_precision", None) or "fp32"
+    if prec not in _lib.PRECISIONS:
+        raise ValueError(f"conv_precision must be one of {sorted(_lib.PRECISIONS)}, got {prec!r}")
+    return prec
+
+
+def cached_pack(mod, device, build):
+    """The packed weights of `mod` for a block-level forward, rebuilt only when a parameter or
+    buffer changes (data_ptr / version), the device or the conv precision changes; kept on the
+    module outside its state_dict."""
+    prec = module_precision(mod)
+    key = (tuple((p.data_ptr(), p._version) for p in mod.parameters()) +
+           tuple((b.data_ptr(), b._version) for b in mod.buffers()), str(device), prec)
+    hit = mod.__dict__.get("_hip_pack")
+    if hit is None or hit[0] != key:
+        with torch.no_grad():
+            obj = build()
+        set_precision(obj, _lib.PRECISIONS[prec])
+        hit = (key, obj)
+        mod.__dict__["_hip_pack"] = hit
+    return hit[1]
+
+
 def conv2d_rows(pc: PackedConv, src0: Rows, batch, in_h, in_w, out: Rows, **kw):
     conv_launch(conv_params(pc, src0, batch, in_h, in_w, out, **kw))(stream_handle())
 

@@ -7,10 +7,14 @@ SmallUpdateBlock (`:218-263`), BasicUpdateBlock (`:265-325`).
 
 `BasicUpdateBlock(args, hidden_dim)(net, inp, corr, flow) -> (net, mask, delta)`
 runs one update step on the HIP path (engine.plan_update): NHWC implicit-GEMM
-convs on fp32 MFMA with the concatenations elided (virtual-concat inputs and
+convs on MFMA with the concatenations elided (virtual-concat inputs and
 channel-offset outputs), the z/r gates of each GRU half-step as one GEMM with a
 sigmoid / r*h epilogue, and the candidate conv's epilogue doing tanh and the
-GRU blend in place.
+GRU blend in place.  Every sub-module keeps the reference's forward as well
+(FlowHead(x), ConvGRU / SepConvGRU(h, x), the motion encoders (flow, corr)), on
+the same kernels.  Block-level calls compute in exact fp32 MFMA unless the
+module's `conv_precision` says otherwise; their packed weights are cached on
+the module until a parameter changes.
 """
 from __future__ import annotations
 
@@ -19,6 +23,21 @@ import torch.nn as nn
 
 from . import _lib
 from . import kernels as K
+from .kernels import Rows
+
+
+def _pk(conv, **kw):
+    """pack_conv of an nn.Conv2d (its own stride / padding)."""
+    return K.pack_conv(conv.weight, conv.bias, conv.stride, conv.padding, device=conv.weight.device, **kw)
+
+
+def _rows(x: torch.Tensor, ld=None) -> torch.Tensor:
+    K.require_device(x)
+    return K.nchw_to_rows(x.contiguous(), ld)
+
+
+def _pad4(c):
+    return -(-c // 4) * 4
 
 
 class FlowHead(nn.Module):
@@ -28,6 +47,55 @@ class FlowHead(nn.Module):
         self.conv2 = nn.Conv2d(hidden_dim, 2, 3, padding=1)
         self.relu = nn.ReLU(inplace=True)
 
+    def forward(self, x):
+        """conv2(relu(conv1(x))) (core/update.py:6-28)."""
+        c1, c2 = K.cached_pack(self, x.device, lambda: (_pk(self.conv1), _pk(self.conv2)))
+        b, _, h, w = x.shape
+        hid = Rows(torch.empty(b * h * w, c1.n, device=x.device))
+        out = Rows(torch.empty(b * h * w, 4, device=x.device), 0, 2)
+        K.conv2d_rows(c1, Rows(_rows(x)), b, h, w, hid, epilogue=_lib.EPI_RELU)
+        K.conv2d_rows(c2, hid, b, h, w, out)
+        return K.rows_to_nchw(out, b, h, w)
+
+
+class _GRUHalf:
+    """One GRU half-step as two GEMMs: z|r (sigmoid, r*h epilogue) over [h | x], then q over
+    [r*h | x] with the tanh + (1-z)h + zq blend in its epilogue, h updated in place."""
+
+    def __init__(self, cz, cr, cq, hd, xd):
+        xp = _pad4(xd)
+        w = torch.cat([cz.weight, cr.weight], 0)
+        self.zr = K.pack_conv(w, torch.cat([cz.bias, cr.bias]), 1, cz.padding, seg_real=[hd + xd],
+                              seg_decl=[hd + xp], device=w.device)
+        self.q = K.pack_conv(cq.weight, cq.bias, 1, cq.padding, seg_real=[hd, xd], seg_decl=[hd, xp],
+                             device=w.device)
+
+    def run(self, hx: torch.Tensor, hd, xp, z, rh, b, h, w):
+        hrows = Rows(hx, 0, hd)
+        K.conv2d_rows(self.zr, Rows(hx), b, h, w, Rows(z), epilogue=_lib.EPI_GRU_ZR, split=hd, aux0=hrows,
+                      out1=Rows(rh))
+        K.conv2d_rows(self.q, Rows(rh), b, h, w, hrows, src1=Rows(hx, hd, xp), epilogue=_lib.EPI_GRU_Q,
+                      aux0=hrows, aux1=Rows(z))
+
+
+def _gru_forward(mod, steps, h, x):
+    """Shared ConvGRU / SepConvGRU forward on NHWC rows [h | x | zero pad]."""
+    K.require_device(h, x)
+    b, hd, hh, ww = h.shape
+    xd = x.shape[1]
+    xp = _pad4(xd)
+    halves = K.cached_pack(mod, h.device, lambda: [_GRUHalf(*s, hd, xd) for s in steps])
+    hx = torch.zeros(b * hh * ww, hd + xp, device=h.device)
+    s = K.stream_handle()
+    for t, off in ((h, 0), (x, hd)):
+        t = t.contiguous()
+        _lib.call("raft_nchw_to_nhwc", t.data_ptr(), hx.data_ptr() + 4 * off, hx.shape[1], b, t.shape[1], hh, ww, s)
+    z = torch.empty(b * hh * ww, hd, device=h.device)
+    rh = torch.empty_like(z)
+    for half in halves:
+        half.run(hx, hd, xp, z, rh, b, hh, ww)
+    return K.rows_to_nchw(Rows(hx, 0, hd), b, hh, ww)
+
 
 class ConvGRU(nn.Module):
     def __init__(self, hidden_dim=128, input_dim=192 + 128):
@@ -35,6 +103,10 @@ class ConvGRU(nn.Module):
         self.convz = nn.Conv2d(hidden_dim + input_dim, hidden_dim, 3, padding=1)
         self.convr = nn.Conv2d(hidden_dim + input_dim, hidden_dim, 3, padding=1)
         self.convq = nn.Conv2d(hidden_dim + input_dim, hidden_dim, 3, padding=1)
+
+    def forward(self, h, x):
+        """h <- (1-z) h + z tanh(convq([r h, x])), z, r = sigmoid(convz / convr([h, x])) (core/update.py:52-72)."""
+        return _gru_forward(self, [(self.convz, self.convr, self.convq)], h, x)
 
 
 class SepConvGRU(nn.Module):
@@ -47,6 +119,47 @@ class SepConvGRU(nn.Module):
         self.convr2 = nn.Conv2d(hidden_dim + input_dim, hidden_dim, (5, 1), padding=(2, 0))
         self.convq2 = nn.Conv2d(hidden_dim + input_dim, hidden_dim, (5, 1), padding=(2, 0))
 
+    def forward(self, h, x):
+        """The 1x5 half-step, then the 5x1 half-step (core/update.py:99-121)."""
+        return _gru_forward(self, [(self.convz1, self.convr1, self.convq1), (self.convz2, self.convr2, self.convq2)],
+                            h, x)
+
+
+def _motion_forward(mod, flow, corr, small):
+    """BasicMotionEncoder / SmallMotionEncoder forward (core/update.py:145-167, :193-216):
+    cor = relu(convc1(corr)) [-> relu(convc2)], flo = relu(convf2(relu(convf1(flow)))),
+    out = relu(conv([cor, flo])); returns [out, flow]."""
+    K.require_device(flow, corr)
+    b, _, h, w = flow.shape
+    dev = flow.device
+
+    def build():
+        return {n: _pk(getattr(mod, n), **({"mode": _lib.RAFT_CONV_GATHER} if n == "convf1" else {}))
+                for n in ("convc1", "convc2", "convf1", "convf2", "conv") if hasattr(mod, n)}
+
+    pc = K.cached_pack(mod, dev, build)
+    P = b * h * w
+    cor_c, flo_c = (96, 32) if small else (192, 64)
+    out_c = pc["conv"].n
+    fl = Rows(_rows(flow))
+    cr = Rows(_rows(corr, _pad4(corr.shape[1])), 0, corr.shape[1])
+    cf = Rows(torch.empty(P, cor_c + flo_c, device=dev))
+    if small:
+        K.conv2d_rows(pc["convc1"], cr, b, h, w, cf.sub(0, cor_c), epilogue=_lib.EPI_RELU)
+    else:
+        cor1 = Rows(torch.empty(P, pc["convc1"].n, device=dev))
+        K.conv2d_rows(pc["convc1"], cr, b, h, w, cor1, epilogue=_lib.EPI_RELU)
+        K.conv2d_rows(pc["convc2"], cor1, b, h, w, cf.sub(0, cor_c), epilogue=_lib.EPI_RELU)
+    flo1 = Rows(torch.empty(P, pc["convf1"].n, device=dev))
+    K.conv2d_rows(pc["convf1"], fl, b, h, w, flo1, epilogue=_lib.EPI_RELU)
+    K.conv2d_rows(pc["convf2"], flo1, b, h, w, cf.sub(cor_c, flo_c), epilogue=_lib.EPI_RELU)
+    out = torch.empty(P, _pad4(out_c + 2), device=dev)
+    K.conv2d_rows(pc["conv"], cf, b, h, w, Rows(out, 0, out_c), epilogue=_lib.EPI_RELU)
+    # cat([out, flow]): the flow lands in the last two channels of the output rows
+    _lib.call("raft_nchw_to_nhwc", flow.contiguous().data_ptr(), out.data_ptr() + 4 * out_c, out.shape[1], b, 2, h, w,
+              K.stream_handle())
+    return K.rows_to_nchw(Rows(out, 0, out_c + 2), b, h, w)
+
 
 class SmallMotionEncoder(nn.Module):
     def __init__(self, args):
@@ -56,6 +169,9 @@ class SmallMotionEncoder(nn.Module):
         self.convf1 = nn.Conv2d(2, 64, 7, padding=3)
         self.convf2 = nn.Conv2d(64, 32, 3, padding=1)
         self.conv = nn.Conv2d(128, 80, 3, padding=1)
+
+    def forward(self, flow, corr):
+        return _motion_forward(self, flow, corr, small=True)
 
 
 class BasicMotionEncoder(nn.Module):
@@ -68,6 +184,9 @@ class BasicMotionEncoder(nn.Module):
         self.convf2 = nn.Conv2d(128, 64, 3, padding=1)
         self.conv = nn.Conv2d(64 + 192, 128 - 2, 3, padding=1)
 
+    def forward(self, flow, corr):
+        return _motion_forward(self, flow, corr, small=False)
+
 
 class _UpdateBase(nn.Module):
     _small = False
@@ -77,7 +196,7 @@ class _UpdateBase(nn.Module):
         K.require_device(net, inp, corr, flow)
         b, _, h, w = net.shape
         P = b * h * w
-        pu = PackedUpdate(self, self._small, net.device)
+        pu = K.cached_pack(self, net.device, lambda: PackedUpdate(self, self._small, net.device))
         if corr.shape[1] != pu.cor_planes:
             raise ValueError(f"corr has {corr.shape[1]} channels, expected {pu.cor_planes}")
         A = Arena(net.device)
