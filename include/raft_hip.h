@@ -28,6 +28,9 @@
  *   raft_upflow8            <- upflow8 (core/utils/utils.py:80-82)
  *   raft_prep_images        <- RAFT.forward normalisation 2*(x/255)-1 (core/raft.py:164-169)
  *   raft_avgpool2_nhwc      <- F.avg_pool2d(x, 2, stride=2) in AlternateCorrBlock (core/corr.py:157-161)
+ *   raft_pad_replicate      <- InputPadder.pad (core/utils/utils.py:7-24, F.pad mode='replicate')
+ *   raft_bilinear_sample    <- bilinear_sampler (core/utils/utils.py:57-71)
+ *   raft_forward_interpolate <- forward_interpolate (core/utils/utils.py:26-54; scipy griddata 'nearest')
  */
 #ifndef RAFT_HIP_H_
 #define RAFT_HIP_H_
@@ -38,7 +41,7 @@
 extern "C" {
 #endif
 
-#define RAFT_HIP_ABI_VERSION 5
+#define RAFT_HIP_ABI_VERSION 6
 
 /* Negative return codes (argument errors, raised before any launch). */
 #define RAFT_E_INVALID (-1)   /* bad size / null pointer / unsupported shape */
@@ -253,6 +256,22 @@ int raft_upflow8(const float* coords, float* flow_up, int B, int H, int W, raft_
 /* NCHW [B][C][H][W] <-> NHWC rows [B*H*W][ld] */
 int raft_nchw_to_nhwc(const float* in, float* out, int out_ld, int B, int C, int H, int W, raft_stream_t stream);
 int raft_nhwc_to_nchw(const float* in, int in_ld, float* out, int B, int C, int H, int W, raft_stream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Caller-side helpers (demo.py / evaluate.py around RAFT.forward), NCHW fp32
+ * --------------------------------------------------------------------------- */
+/* replicate padding: in [NC][H][W] -> out [NC][H+top+bottom][W+left+right] */
+int raft_pad_replicate(const float* in, float* out, int NC, int H, int W, int top, int bottom, int left, int right,
+                       raft_stream_t stream);
+/* bilinear_sampler: img [N][C][H][W], coords [N][Ho][Wo][2] pixel (x, y) -> out [N][C][Ho][Wo]
+ * (grid_sample, align_corners=True, zero padding; a non-finite position gives NaN, as the
+ * reference on a 1-px axis); mask (optional) [N][Ho][Wo] = 1 where -1 < grid < 1 on both axes. */
+int raft_bilinear_sample(const float* img, const float* coords, float* out, float* mask, int N, int C, int H, int W,
+                         int Ho, int Wo, raft_stream_t stream);
+/* forward_interpolate: flow [B][2][H][W] -> out [B][2][H][W]; every grid point takes the flow of
+ * the nearest (fp64 Euclidean) forward-moved point (x + dx, y + dy) strictly inside
+ * (0, W) x (0, H); ties -> the lowest source index; no valid point -> 0. */
+int raft_forward_interpolate(const float* flow, float* out, int B, int H, int W, raft_stream_t stream);
 
 #ifdef __cplusplus
 }

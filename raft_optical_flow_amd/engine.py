@@ -481,7 +481,8 @@ class RaftPlan:
         plan_gru_context(L, pu, ub, B, h, w)
         if ctx_side:
             for l in L[n_ctx:]:
-                l.side = True
+                if isinstance(l, Launch):  # FORK / JOIN markers are plain strings
+                    l.side = True
             L.append(K.JOIN)
         L.append(Launch("raft_init_coords", ub.coords.data_ptr(),
                         self.flow_init.data_ptr() if self.flow_init is not None else None, B, h, w))

@@ -143,7 +143,10 @@ class RAFT(nn.Module):
         device = device or next(self.parameters()).device
         prec = prec or self.resolved_precision()
         pk = self.packed(device, prec)
-        key = (batch, height, width, iters, bool(test_mode), bool(self.args.alternate_corr), bool(flow_init), prec)
+        # the stream layout knobs are read when a plan is built, so they are part of its key
+        knobs = (os.environ.get("RAFT_CTX_SIDE", "1"), os.environ.get("RAFT_FLOW_SIDE", "1"))
+        key = (batch, height, width, iters, bool(test_mode), bool(self.args.alternate_corr), bool(flow_init), prec,
+               knobs)
         pl = self._plans.get(key)
         if pl is None:
             while len(self._plans) >= max(1, self.max_plans):

@@ -1,86 +1,123 @@
-"""Tensor utilities — drop-in for core/utils/utils.py.
+"""Caller-side tensor helpers — drop-in for core/utils/utils.py, on the GPU.
 
-InputPadder (`core/utils/utils.py:7-24`), coords_grid (`:74-77`),
-bilinear_sampler (`:57-71`) and forward_interpolate (`:26-54`) keep the
-reference's torch/scipy semantics (they are caller-side helpers, not kernels of
-the accelerated path).  upflow8 (`:80-82`) runs the HIP kernel on GPU tensors.
+  InputPadder          core/utils/utils.py:7-24   replicate padding to multiples of 8
+                                                   (raft_pad_replicate for GPU tensors)
+  forward_interpolate  :26-54                      Sintel warm start: nearest forward-splatted
+                                                   flow (raft_forward_interpolate, fp64 search)
+  bilinear_sampler     :57-71                      grid_sample(align_corners=True) in pixel
+                                                   coordinates (raft_bilinear_sample)
+  coords_grid          :74-77                      (x, y) pixel grid
+  upflow8              :80-82                      8 * bilinear x8 upsampling (raft_upflow8)
+
+Every helper computes on the GPU through the HIP kernels of libraft_hip.so; a CPU tensor is
+copied to the current GPU and the result copied back (there is no host computation path).
 """
 from __future__ import annotations
 
-import numpy as np
 import torch
-import torch.nn.functional as F
+
+
+def _lib():
+    from .. import _lib as L
+    return L
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _on_gpu(x: torch.Tensor) -> torch.Tensor:
+    if x.is_cuda:
+        return x
+    if not torch.cuda.is_available():
+        raise RuntimeError("raft_optical_flow_amd helpers run on a ROCm GPU only (no CPU path)")
+    return x.cuda()
 
 
 class InputPadder:
-    """Pads images such that dimensions are divisible by 8."""
+    """Replicate-pad NCHW images so H and W become multiples of 8: centred ('sintel', the
+    default) or all rows at the bottom (any other mode, e.g. 'kitti'); `unpad` crops back.
+    `_pad` = [left, right, top, bottom] (F.pad order), as the reference keeps it."""
 
     def __init__(self, dims, mode="sintel"):
-        self.ht, self.wd = dims[-2:]
-        pad_ht = (((self.ht // 8) + 1) * 8 - self.ht) % 8
-        pad_wd = (((self.wd // 8) + 1) * 8 - self.wd) % 8
-        if mode == "sintel":
-            self._pad = [pad_wd // 2, pad_wd - pad_wd // 2, pad_ht // 2, pad_ht - pad_ht // 2]
-        else:
-            self._pad = [pad_wd // 2, pad_wd - pad_wd // 2, 0, pad_ht]
+        self.ht, self.wd = int(dims[-2]), int(dims[-1])
+        ph, pw = -self.ht % 8, -self.wd % 8
+        top = ph // 2 if mode == "sintel" else 0
+        self._pad = [pw // 2, pw - pw // 2, top, ph - top]
+
+    def _pad_one(self, x: torch.Tensor) -> torch.Tensor:
+        left, right, top, bottom = self._pad
+        src = x
+        x = _on_gpu(x).float().contiguous()
+        h, w = x.shape[-2:]
+        out = torch.empty(*x.shape[:-2], h + top + bottom, w + left + right, device=x.device)
+        nc = x.numel() // (h * w)
+        _lib().call("raft_pad_replicate", x.data_ptr(), out.data_ptr(), nc, h, w, top, bottom, left, right, _stream())
+        return out.to(device=src.device, dtype=src.dtype)
 
     def pad(self, *inputs):
-        return [F.pad(x, self._pad, mode="replicate") for x in inputs]
+        return [self._pad_one(x) for x in inputs]
 
     def unpad(self, x):
-        ht, wd = x.shape[-2:]
-        c = [self._pad[2], ht - self._pad[3], self._pad[0], wd - self._pad[1]]
-        return x[..., c[0]:c[1], c[2]:c[3]]
+        left, right, top, bottom = self._pad
+        h, w = x.shape[-2:]
+        return x[..., top:h - bottom, left:w - right]
 
 
 def forward_interpolate(flow):
-    """Warm-start flow for the next frame (scipy nearest-neighbour griddata on the host)."""
-    from scipy import interpolate
-    flow = flow.detach().cpu().numpy()
-    dx, dy = flow[0], flow[1]
-    ht, wd = dx.shape
-    x0, y0 = np.meshgrid(np.arange(wd), np.arange(ht))
-    x1 = (x0 + dx).reshape(-1)
-    y1 = (y0 + dy).reshape(-1)
-    dx = dx.reshape(-1)
-    dy = dy.reshape(-1)
-    valid = (x1 > 0) & (x1 < wd) & (y1 > 0) & (y1 < ht)
-    x1, y1, dx, dy = x1[valid], y1[valid], dx[valid], dy[valid]
-    flow_x = interpolate.griddata((x1, y1), dx, (x0, y0), method="nearest", fill_value=0)
-    flow_y = interpolate.griddata((x1, y1), dy, (x0, y0), method="nearest", fill_value=0)
-    return torch.from_numpy(np.stack([flow_x, flow_y], axis=0)).float()
+    """Warm-start flow for the next frame pair (evaluate.py:37-41): each pixel takes the flow of
+    the nearest point the flow moves a pixel to, over the points that land strictly inside the
+    frame (scipy griddata 'nearest' in the reference; 0 where none lands).  flow [2, H, W] (or
+    [B, 2, H, W]) -> float32, same shape, same device."""
+    f = _on_gpu(flow.detach()).float().contiguous()
+    batched = f.dim() == 4
+    if not batched:
+        f = f[None]
+    b, c, h, w = f.shape
+    if c != 2:
+        raise ValueError(f"flow must be [2, H, W] or [B, 2, H, W], got {tuple(flow.shape)}")
+    out = torch.empty_like(f)
+    _lib().call("raft_forward_interpolate", f.data_ptr(), out.data_ptr(), b, h, w, _stream())
+    out = out if batched else out[0]
+    return out.to(flow.device)
 
 
 def bilinear_sampler(img, coords, mode="bilinear", mask=False):
-    """Wrapper for grid_sample, uses pixel coordinates."""
-    H, W = img.shape[-2:]
-    xgrid, ygrid = coords.split([1, 1], dim=-1)
-    xgrid = 2 * xgrid / (W - 1) - 1
-    ygrid = 2 * ygrid / (H - 1) - 1
-    grid = torch.cat([xgrid, ygrid], dim=-1)
-    img = F.grid_sample(img, grid, align_corners=True)
-    if mask:
-        m = (xgrid > -1) & (ygrid > -1) & (xgrid < 1) & (ygrid < 1)
-        return img, m.float()
-    return img
+    """Sample img [N, C, H, W] at pixel coordinates coords [N, Ho, Wo, 2] (x, y): bilinear,
+    corners outside the image read 0 (grid_sample align_corners=True).  With mask=True also
+    returns the in-range mask [N, Ho, Wo, 1] as float."""
+    if mode != "bilinear":
+        raise NotImplementedError("bilinear_sampler: only mode='bilinear' is on the RAFT path")
+    from .. import kernels as K
+    K.require_device(img, coords)
+    img = img.contiguous()
+    coords = coords.contiguous()
+    n, c, h, w = img.shape
+    ho, wo = coords.shape[1:3]
+    out = torch.empty(n, c, ho, wo, device=img.device)
+    m = torch.empty(n, ho, wo, 1, device=img.device) if mask else None
+    _lib().call("raft_bilinear_sample", img.data_ptr(), coords.data_ptr(), out.data_ptr(),
+                m.data_ptr() if mask else None, n, c, h, w, ho, wo, _stream())
+    return (out, m) if mask else out
 
 
 def coords_grid(batch, ht, wd, device):
-    ys, xs = torch.meshgrid(torch.arange(ht, device=device), torch.arange(wd, device=device), indexing="ij")
-    coords = torch.stack([xs, ys], dim=0).float()
-    return coords[None].repeat(batch, 1, 1, 1)
+    """[batch, 2, ht, wd] float grid: channel 0 = x (column index), channel 1 = y (row index)."""
+    x = torch.arange(wd, device=device, dtype=torch.float32).view(1, wd).expand(ht, wd)
+    y = torch.arange(ht, device=device, dtype=torch.float32).view(ht, 1).expand(ht, wd)
+    return torch.stack([x, y], 0)[None].repeat(batch, 1, 1, 1)
 
 
 def upflow8(flow, mode="bilinear"):
-    """8 * bilinear(align_corners=True) x8 upsampling; HIP kernel for GPU tensors."""
-    from .. import _lib
+    """8 * bilinear(align_corners=True) x8 upsampling (raft_upflow8)."""
     from .. import kernels as K
-    if mode != "bilinear" or not flow.is_cuda:
-        new_size = (8 * flow.shape[2], 8 * flow.shape[3])
-        return 8 * F.interpolate(flow, size=new_size, mode=mode, align_corners=True)
+    if mode != "bilinear":
+        raise NotImplementedError("upflow8: only mode='bilinear' is on the RAFT path")
+    src = flow
+    flow = _on_gpu(flow).float()
     n, _, h, w = flow.shape
     coords = (coords_grid(n, h, w, flow.device) + flow).contiguous()
     crow = K.nchw_to_rows(coords)
     out = torch.empty(n, 2, 8 * h, 8 * w, device=flow.device)
-    _lib.call("raft_upflow8", crow.data_ptr(), out.data_ptr(), n, h, w, K.stream_handle())
-    return out
+    _lib().call("raft_upflow8", crow.data_ptr(), out.data_ptr(), n, h, w, K.stream_handle())
+    return out.to(src.device)

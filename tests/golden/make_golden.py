@@ -158,6 +158,34 @@ def gen_raft_e2e(full_size: bool):
 
 
 @torch.no_grad()
+def gen_caller():
+    """Caller-side helpers of core/utils/utils.py: InputPadder pads (both modes, many sizes) and a
+    padded tensor, forward_interpolate (scipy griddata 'nearest') on smooth / leaving / zero flows,
+    bilinear_sampler with its mask."""
+    _, _, _, rutils = ref_modules()
+    g = torch.Generator().manual_seed(21)
+    dims = [(436, 1024), (540, 960), (1080, 1920), (375, 1242), (370, 1226), (100, 100), (8, 8), (13, 21)]
+    pads = np.array([[rutils.InputPadder((1, 3, h, w), mode=m)._pad for (h, w) in dims] for m in ("sintel", "kitti")])
+    x = torch.rand(2, 3, 13, 21, generator=g) * 255
+    out = {"dims": np.array(dims), "pads": pads, "pad_in": x,
+           "pad_sintel": rutils.InputPadder(x.shape).pad(x)[0],
+           "pad_kitti": rutils.InputPadder(x.shape, mode="kitti").pad(x)[0]}
+    ys, xs = torch.meshgrid(torch.arange(55).float(), torch.arange(128).float(), indexing="ij")
+    smooth = torch.stack([4 * torch.sin(xs / 17 + ys / 23) + 1.3, 3 * torch.cos(ys / 11 - xs / 29) - 0.7])
+    leaving = smooth * 6 + torch.randn(2, 55, 128, generator=g) * 2
+    zero = torch.zeros(2, 16, 24)
+    for name, f in (("fi_smooth", smooth), ("fi_leaving", leaving), ("fi_zero", zero)):
+        out[name + "_in"] = f
+        out[name + "_out"] = rutils.forward_interpolate(f)
+    img = torch.randn(2, 3, 9, 11, generator=g)
+    coords = torch.rand(2, 5, 7, 2, generator=g) * torch.tensor([14.0, 12.0]) - torch.tensor([2.0, 1.5])
+    coords[0, 0, 0] = torch.tensor([4.0, 3.0])     # exact integers
+    smp, msk = rutils.bilinear_sampler(img, coords, mask=True)
+    out.update(bs_img=img, bs_coords=coords, bs_out=smp, bs_mask=msk)
+    save("caller_utils.npz", **out)
+
+
+@torch.no_grad()
 def gen_config4():
     """Config 4 shape: 540x960 frames padded (InputPadder 'sintel') to 544x960, B=1, iters=32."""
     i1, i2 = seeded_images(1, 544, 960, seed=2)
@@ -222,7 +250,7 @@ if __name__ == "__main__":
     a = ap.parse_args()
     jobs = {"lookup": gen_lookup, "update": gen_update_and_upsample, "enc": gen_encoders,
             "e2e": lambda: gen_raft_e2e(a.full_size), "demo": gen_raft_small_demo,
-            "config4": gen_config4, "bf16": gen_bf16}
+            "config4": gen_config4, "bf16": gen_bf16, "caller": gen_caller}
     for k, f in jobs.items():
         if not a.only or k in a.only.split(","):
             f()

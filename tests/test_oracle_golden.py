@@ -145,3 +145,24 @@ def test_torch_cpu_baseline_matches_reference():
     low, up = T.raft_forward(p, torch.from_numpy(g["image1"]), torch.from_numpy(g["image2"]), iters=int(g["iters"]))
     assert maxabs(low.numpy(), g["flow_low"]) < 1e-4
     assert maxabs(up.numpy(), g["flow_up"]) < 1e-4
+
+
+def test_caller_helpers_match_reference():
+    """InputPadder pads (both modes), replicate padding, forward_interpolate, bilinear_sampler."""
+    g = load_golden("caller_utils.npz")
+    for mi, mode in enumerate(("sintel", "kitti")):
+        for (h, w), pad in zip(g["dims"], g["pads"][mi]):
+            assert O.InputPadder((1, 3, int(h), int(w)), mode=mode)._pad == list(pad)
+    assert maxabs(O.InputPadder(g["pad_in"].shape).pad(g["pad_in"])[0], g["pad_sintel"]) == 0.0
+    for name in ("fi_smooth", "fi_leaving", "fi_zero"):
+        assert maxabs(O.forward_interpolate(g[name + "_in"]), g[name + "_out"]) == 0.0
+    assert maxabs(O.bilinear_sampler(g["bs_img"], g["bs_coords"]), g["bs_out"]) < 1e-6
+
+
+def test_host_padder_matches_reference_pads():
+    """raft_optical_flow_amd.InputPadder computes the reference's pads (no GPU needed)."""
+    g = load_golden("caller_utils.npz")
+    from raft_optical_flow_amd import InputPadder
+    for mi, mode in enumerate(("sintel", "kitti")):
+        for (h, w), pad in zip(g["dims"], g["pads"][mi]):
+            assert InputPadder((1, 3, int(h), int(w)), mode=mode)._pad == list(pad)
