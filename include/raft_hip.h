@@ -116,10 +116,14 @@ int raft_alt_corr_lookup_nhwc(const float* fmap1, const float* fmap2, const floa
                               int C, int radius, float scale_div, float* flow_out, int flow_ld,
                               int* range_flag, raft_stream_t stream);
 
-/* Gradients of raft_alt_corr_forward (unscaled), like correlation_kernel.cu:122-256:
- * fmap1_grad is a deterministic gather; fmap2_grad is accumulated with float
- * atomics (order-dependent in the last bits, as the reference); coords_grad is
- * written with zeros, like the reference (correlation_kernel.cu:307 never fills it). */
+/* Gradients of raft_alt_corr_forward (unscaled), replacing correlation_kernel.cu:122-256:
+ * every output is written (no pre-zeroing) and bit-identical run to run.  fmap1_grad is
+ * a gather over each query's taps; fmap2_grad inverts the (query, tap) -> fmap2 pixel map
+ * (a stable sort of the queries by window origin, then a gather per fmap2 pixel) instead
+ * of the reference's float atomics; coords_grad is the true gradient through the bilinear
+ * weights (the reference leaves it zero, correlation_kernel.cu:307).  workspace: at least
+ * raft_alt_corr_backward_workspace_floats(...) floats, 256-byte aligned.  C % 4 == 0,
+ * C <= 1024, radius <= 4. */
 int raft_alt_corr_backward(const float* fmap1, const float* fmap2, const float* coords, const float* corr_grad,
                            float* fmap1_grad, float* fmap2_grad, float* coords_grad,
                            int B, int H1, int W1, int H2, int W2, int C, int N, int radius,

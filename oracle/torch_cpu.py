@@ -161,3 +161,30 @@ def raft_forward(p, image1, image2, iters=12, small=False):
         coords1 = coords1 + delta
         flow_up = upflow8(coords1 - coords0) if mask is None else upsample(coords1 - coords0, mask)
     return coords1 - coords0, flow_up
+
+
+def alt_corr_forward(f1, f2, coords, r):
+    """alt_cuda_corr/correlation_kernel.cu:18-119 (corr_forward_kernel) as differentiable torch
+    ops, for the gradient checks of the plugin's backward: f1 [B,H1,W1,C], f2 [B,H2,W2,C],
+    coords [B,N,H1,W1,2] -> [B,N,(2r+1)^2,H1,W1], unscaled, channel oy + (2r+1)*ox.  The taps sit
+    at floor(coords) - r + (0..2r+1) (piecewise constant: no gradient through the floor); the
+    bilinear weights carry the coordinate gradient."""
+    B, H1, W1, C = f1.shape
+    _, H2, W2, _ = f2.shape
+    N = coords.shape[1]
+    rd, wd = 2 * r + 1, 2 * r + 2
+    x, y = coords[..., 0], coords[..., 1]
+    fx, fy = torch.floor(x).detach(), torch.floor(y).detach()
+    dx, dy = x - fx, y - fy
+    ar = torch.arange(wd)
+    h2 = (fy.long() - r)[..., None, None] + ar.view(wd, 1)
+    w2 = (fx.long() - r)[..., None, None] + ar.view(1, wd)
+    ok = ((h2 >= 0) & (h2 < H2) & (w2 >= 0) & (w2 < W2)).to(f1.dtype)
+    idx = (h2.clamp(0, H2 - 1) * W2 + w2.clamp(0, W2 - 1)).reshape(B, -1)        # [B, N*H1*W1*wd*wd]
+    taps = torch.gather(f2.reshape(B, H2 * W2, C), 1, idx[..., None].expand(-1, -1, C))
+    taps = taps.reshape(B, N, H1, W1, wd, wd, C)
+    s = (f1[:, None, :, :, None, None, :] * taps).sum(-1) * ok                   # s[..., iy, ix]
+    ex, ey = dx[..., None, None], dy[..., None, None]
+    o = (s[..., :rd, :rd] * ((1 - ey) * (1 - ex)) + s[..., :rd, 1:] * ((1 - ey) * ex)
+         + s[..., 1:, :rd] * (ey * (1 - ex)) + s[..., 1:, 1:] * (ey * ex))        # o[..., oy, ox]
+    return o.permute(0, 1, 5, 4, 2, 3).reshape(B, N, rd * rd, H1, W1)

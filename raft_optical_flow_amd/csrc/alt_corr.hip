@@ -437,52 +437,6 @@ int launch_alt(const AltArgs& a, raft_stream_t stream) {
 // fmap1_grad[p] = sum_tap g * fmap2[tap] (gather, deterministic);
 // fmap2_grad[q] += g * fmap1[p] (float atomics, as the reference).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void alt_corr_bwd_kernel(const float* f1, const float* f2, const float* coords,
-                                                         const float* cg, float* f1g, float* f2g, int B, int H1,
-                                                         int W1, int H2, int W2, int C, int N, int r) {
-  const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
-  const int P1 = H1 * W1;
-  const long gid = (long)blockIdx.x * 4 + wv;  // b*P1 + p
-  if (gid >= (long)B * P1) return;
-  const int b = (int)(gid / P1);
-  const int p = (int)(gid - (long)b * P1);
-  const int rd = 2 * r + 1, wd = 2 * r + 2;
-  for (int c0 = lane * 4; c0 < C; c0 += 256) {
-    f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
-    const f32x4 a1 = *reinterpret_cast<const f32x4*>(f1 + gid * C + c0);
-    for (int n = 0; n < N; ++n) {
-      const long bn = (long)b * N + n;
-      const float x = coords[2 * (bn * P1 + p)], y = coords[2 * (bn * P1 + p) + 1];
-      const float fx = floorf(x), fy = floorf(y);
-      const float dx = x - fx, dy = y - fy;
-      const int x0 = (int)fx - r, y0 = (int)fy - r;
-      const float* g = cg + bn * rd * rd * P1 + p;
-      for (int iy = 0; iy < wd; ++iy) {
-        for (int ix = 0; ix < wd; ++ix) {
-          const int h2 = y0 + iy, w2 = x0 + ix;
-          if (h2 < 0 || h2 >= H2 || w2 < 0 || w2 >= W2) continue;
-          float gt = 0.f;
-          if (iy > 0 && ix > 0) gt += g[(long)((iy - 1) + rd * (ix - 1)) * P1] * dy * dx;
-          if (iy > 0 && ix < rd) gt += g[(long)((iy - 1) + rd * ix) * P1] * dy * (1.f - dx);
-          if (iy < rd && ix > 0) gt += g[(long)(iy + rd * (ix - 1)) * P1] * (1.f - dy) * dx;
-          if (iy < rd && ix < rd) gt += g[(long)(iy + rd * ix) * P1] * (1.f - dy) * (1.f - dx);
-          float* q2 = f2g + (((long)b * H2 + h2) * W2 + w2) * C + c0;
-          const f32x4 b2 = *reinterpret_cast<const f32x4*>(f2 + (((long)b * H2 + h2) * W2 + w2) * C + c0);
-          acc1 += gt * b2;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) atomicAdd(q2 + j, gt * a1[j]);
-        }
-      }
-    }
-    *reinterpret_cast<f32x4*>(f1g + gid * C + c0) = acc1;
-  }
-}
-
-__global__ void zero_kernel(float* p, long n) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) p[i] = 0.f;
-}
-
 __global__ void avgpool2_nhwc_kernel(const float* in, float* out, int B, int H, int W, int C, int Ho, int Wo) {
   const long total = (long)B * Ho * Wo * C;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -580,25 +534,6 @@ extern "C" int raft_alt_corr_lookup_nhwc(const float* fmap1, const float* fmap2,
   a.flow_ld = flow_ld;
   a.range_flag = range_flag;
   return launch_alt(a, stream);
-}
-
-extern "C" size_t raft_alt_corr_backward_workspace_floats(int, int, int, int, int, int, int, int) { return 0; }
-
-extern "C" int raft_alt_corr_backward(const float* fmap1, const float* fmap2, const float* coords,
-                                      const float* corr_grad, float* fmap1_grad, float* fmap2_grad,
-                                      float* coords_grad, int B, int H1, int W1, int H2, int W2, int C, int N,
-                                      int radius, float*, size_t, raft_stream_t stream) {
-  int rc = alt_checks(fmap1, fmap2, coords, corr_grad, B, H1, W1, H2, W2, C, N, radius);
-  if (rc) return rc;
-  RAFT_REQUIRE(fmap1_grad && fmap2_grad && coords_grad, "raft_alt_corr_backward: null gradient pointer");
-  hipStream_t s = as_stream(stream);
-  const long n2 = (long)B * H2 * W2 * C;
-  const long nc = (long)B * N * H1 * W1 * 2;
-  hipLaunchKernelGGL(zero_kernel, dim3(grid_for(n2)), dim3(256), 0, s, fmap2_grad, n2);
-  hipLaunchKernelGGL(zero_kernel, dim3(grid_for(nc)), dim3(256), 0, s, coords_grad, nc);
-  hipLaunchKernelGGL(alt_corr_bwd_kernel, dim3((unsigned)cdiv_l((long)B * H1 * W1, 4)), dim3(256), 0, s, fmap1,
-                     fmap2, coords, corr_grad, fmap1_grad, fmap2_grad, B, H1, W1, H2, W2, C, N, radius);
-  return check_launch("raft_alt_corr_backward");
 }
 
 extern "C" int raft_avgpool2_nhwc(const float* in, float* out, int B, int H, int W, int C, raft_stream_t stream) {

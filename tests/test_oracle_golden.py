@@ -166,3 +166,21 @@ def test_host_padder_matches_reference_pads():
     for mi, mode in enumerate(("sintel", "kitti")):
         for (h, w), pad in zip(g["dims"], g["pads"][mi]):
             assert InputPadder((1, 3, int(h), int(w)), mode=mode)._pad == list(pad)
+
+
+def test_alt_corr_torch_restatement_and_its_gradient():
+    """oracle/torch_cpu.alt_corr_forward (the gradient oracle of the plugin's backward) equals the
+    numpy restatement of correlation_kernel.cu:18-119, and its autograd passes gradcheck
+    (coordinates kept off the integer grid, where the taps' floor is constant)."""
+    import torch
+    from oracle import torch_cpu as T
+    rng = np.random.default_rng(0)
+    f1 = rng.standard_normal((2, 5, 6, 16))
+    f2 = rng.standard_normal((2, 7, 8, 16))
+    c = rng.uniform(-3, 10, (2, 2, 5, 6, 2))
+    got = T.alt_corr_forward(torch.tensor(f1), torch.tensor(f2), torch.tensor(c), 2).numpy()
+    assert maxabs(got, O.alt_corr_forward(f1, f2, c, 2)) < 1e-12
+    a = torch.tensor(f1[:1, :3, :4, :4], requires_grad=True)
+    b = torch.tensor(f2[:1, :5, :5, :4], requires_grad=True)
+    cc = torch.tensor(np.floor(c[:1, :1, :3, :4]) + rng.uniform(0.1, 0.9, (1, 1, 3, 4, 2)), requires_grad=True)
+    assert torch.autograd.gradcheck(lambda x, y, z: T.alt_corr_forward(x, y, z, 1), (a, b, cc))
