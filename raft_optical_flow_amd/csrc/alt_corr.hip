@@ -411,8 +411,81 @@ __global__ __launch_bounds__(256) void alt_corr_tile_kernel(AltArgs a) {
   }
 }
 
+// Any radius (the reference's CorrBlock / AlternateCorrBlock take any r; RAFT uses 3 and 4,
+// which the kernels above serve): one wave per query, the (2r+2)^2 tap sums in dynamic LDS
+// (one row of ALT_GEN_ROW floats per wave), then the bilinear binning.
+__global__ __launch_bounds__(256) void alt_corr_generic_kernel(AltArgs a, int row) {
+  extern __shared__ float gts[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int P1 = a.H1 * a.W1;
+  const long gid = (long)blockIdx.x * 4 + wv;
+  if (gid >= (long)a.B * a.N * P1) return;
+  const long bn = gid / P1;
+  const int p = (int)(gid - bn * P1);
+  const int b = (int)(bn / a.N);
+  const int rd = 2 * a.r + 1, wd = 2 * a.r + 2;
+  float* ts = gts + wv * row;
+  float x, y;
+  if (a.coords_layout == 0) {
+    x = a.coords[2 * gid];
+    y = a.coords[2 * gid + 1];
+  } else {
+    x = a.coords[((long)b * 2) * P1 + p];
+    y = a.coords[((long)b * 2 + 1) * P1 + p];
+  }
+  x = x / a.coord_div;
+  y = y / a.coord_div;
+  const bool fin = isfinite(x) && isfinite(y) && fabsf(x) < 1e8f && fabsf(y) < 1e8f;
+  const int x0 = fin ? (int)floorf(x) - a.r : 0, y0 = fin ? (int)floorf(y) - a.r : 0;
+  const float* f1row = a.f1 + ((long)b * P1 + p) * a.C;
+  const float* f2b = a.f2 + (long)b * a.H2 * a.W2 * a.C;
+  for (int t = 0; t < wd * wd; ++t) {
+    const int h2 = y0 + t / wd, w2 = x0 + t % wd;
+    float v = 0.f;
+    if ((unsigned)h2 < (unsigned)a.H2 && (unsigned)w2 < (unsigned)a.W2) {
+      const float* r2 = f2b + ((long)h2 * a.W2 + w2) * a.C;
+      for (int c = 4 * lane; c < a.C; c += 256) {
+        const f32x4 u = *reinterpret_cast<const f32x4*>(r2 + c);
+        const f32x4 f = *reinterpret_cast<const f32x4*>(f1row + c);
+        v += f[0] * u[0] + f[1] * u[1] + f[2] * u[2] + f[3] * u[3];
+      }
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+    if (lane == 0) ts[t] = v;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const float dx = x - floorf(x), dy = y - floorf(y);
+  for (int o = lane; o < rd * rd; o += 64) {
+    const int ox = o / rd, oy = o - ox * rd;  // channel = oy + rd*ox
+    float val = ts[oy * wd + ox] * ((1.f - dy) * (1.f - dx));
+    val += ts[oy * wd + ox + 1] * ((1.f - dy) * dx);
+    val += ts[(oy + 1) * wd + ox] * (dy * (1.f - dx));
+    val += ts[(oy + 1) * wd + ox + 1] * (dy * dx);
+    val = val / a.scale_div;
+    if (a.range_flag && fabsf(val) > RAFT_RANGE_LIMIT) *a.range_flag = 1;
+    if (a.out_layout == 0)
+      a.out[(bn * (rd * rd) + o) * P1 + p] = val;
+    else
+      a.out[((long)b * P1 + p) * a.out_ld + o] = val;
+  }
+  if (a.flow && lane < 2) {
+    const float gx = lane == 0 ? (float)(p % a.W1) : (float)(p / a.W1);
+    a.flow[((long)b * P1 + p) * a.flow_ld + lane] = (lane == 0 ? x : y) * a.coord_div - gx;
+  }
+}
+
 int launch_alt(const AltArgs& a, raft_stream_t stream) {
   hipStream_t s = as_stream(stream);
+  if (a.r > 4) {  // any radius: the generic kernel
+    const int wd = 2 * a.r + 2, row = wd * wd;
+    const long waves = (long)a.B * a.N * a.H1 * a.W1;
+    hipLaunchKernelGGL(alt_corr_generic_kernel, dim3((unsigned)cdiv_l(waves, 4)), dim3(256),
+                       (size_t)(4 * row * sizeof(float)), s, a, row);
+    return check_launch("raft_alt_corr(generic radius)");
+  }
 #ifndef ALT_NO_TILE  // dev builds: the per-pixel kernel at every size
   if (a.r == 4 && a.C % ACC == 0 && a.C <= 256) {
     const long tiles = (long)a.B * a.N * cdiv_l(a.H1, AT) * cdiv_l(a.W1, AT);
@@ -431,12 +504,6 @@ int launch_alt(const AltArgs& a, raft_stream_t stream) {
   return check_launch("raft_alt_corr");
 }
 
-// ---------------------------------------------------------------------------
-// alt backward (training path, correlation_kernel.cu:122-256):
-// g(tap) = sum of the corr_grad bins the tap fed, weighted as in forward;
-// fmap1_grad[p] = sum_tap g * fmap2[tap] (gather, deterministic);
-// fmap2_grad[q] += g * fmap1[p] (float atomics, as the reference).
-// ---------------------------------------------------------------------------
 __global__ void avgpool2_nhwc_kernel(const float* in, float* out, int B, int H, int W, int C, int Ho, int Wo) {
   const long total = (long)B * Ho * Wo * C;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -468,7 +535,7 @@ static int alt_checks(const float* f1, const float* f2, const float* coords, con
   RAFT_REQUIRE(f1 && f2 && coords && out, "raft_alt_corr: null pointer");
   RAFT_REQUIRE(B > 0 && H1 > 0 && W1 > 0 && H2 > 0 && W2 > 0 && C > 0 && N > 0, "raft_alt_corr: bad sizes");
   RAFT_REQUIRE(C % 4 == 0 && C <= 1024, "raft_alt_corr: C must be a multiple of 4 and <= 1024 (got %d)", C);
-  RAFT_REQUIRE(r >= 0 && (2 * r + 2) * (2 * r + 2) <= 128, "raft_alt_corr: radius must be 0..4 (got %d)", r);
+  RAFT_REQUIRE(r >= 0 && r <= 32, "raft_alt_corr: radius must be 0..32 (got %d)", r);
   RAFT_REQUIRE((((uintptr_t)f1 | (uintptr_t)f2) & 15) == 0, "raft_alt_corr: fmaps must be 16-byte aligned");
   RAFT_REQUIRE((long)H2 * W2 * C * 4 < (1L << 31), "raft_alt_corr: one fmap2 exceeds 2 GiB");
   return 0;

@@ -565,6 +565,53 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
 }
 
 
+// Any radius / level count (the reference's CorrBlock takes any r; RAFT's r = 3, 4 use the
+// kernel above): one thread per (query pixel, level, output channel), the same per-axis
+// arithmetic as axis_entry, corners read from the tiled maps (zeros off the map; NaN where
+// the position is not finite, as the reference on a 1-px level).
+__global__ void corr_lookup_generic_kernel(LookupArgs a) {
+#pragma clang fp contract(off)
+  const int r = a.r, rd = 2 * r + 1, ntap = a.L * rd * rd;
+  const int P = a.H * a.W;
+  const long total = (long)a.B * P * ntap;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int ch = (int)(i % ntap);
+    const long gp = i / ntap;
+    const int b = (int)(gp / P), p = (int)(gp - (long)b * P);
+    const int l = ch / (rd * rd), k = ch - l * rd * rd;
+    const int ix = k / rd, iy = k - ix * rd;  // channel lvl*rd^2 + ix*rd + iy, ix moves x
+    float x, y;
+    load_coords(a.coords, a.coords_layout, b, p, P, x, y);
+    const float s = 1.0f / (float)(1 << l);
+    const float m1x = a.wm1[l], m1y = a.hm1[l];
+    const float X = x * s + (float)(ix - r), Y = y * s + (float)(iy - r);
+    const float ux = (div_rn(2.0f * X, m1x, a.rw[l]) - 1.0f + 1.0f) * (m1x * 0.5f);
+    const float uy = (div_rn(2.0f * Y, m1y, a.rh[l]) - 1.0f + 1.0f) * (m1y * 0.5f);
+    float v;
+    if (!isfinite(ux) || !isfinite(uy)) {
+      v = __builtin_nanf("");
+    } else {
+      const float fx = floorf(ux), fy = floorf(uy);
+      const float tx = ux - fx, ty = uy - fy;
+      const int x0 = (int)fx, y0 = (int)fy;
+      const Level& lv = a.lv[l];
+      const float* m = a.pyr + lv.off + gp * lv.mapsz;
+      auto at = [&](int yy, int xx) {
+        return ((unsigned)yy < (unsigned)lv.h && (unsigned)xx < (unsigned)lv.w) ? m[tiled_index(yy, xx, lv.tw)] : 0.f;
+      };
+      const float ex = 1.0f - tx, sS = 1.0f - ty;
+      v = at(y0, x0) * (sS * ex) + at(y0, x0 + 1) * (sS * tx) + at(y0 + 1, x0) * (ty * ex) +
+          at(y0 + 1, x0 + 1) * (ty * tx);
+    }
+    if (a.range_flag && fabsf(v) > RAFT_RANGE_LIMIT) *a.range_flag = 1;
+    if (a.out_layout == 0)
+      a.out[gp * a.out_ld + ch] = v;
+    else
+      a.out[((long)b * ntap + ch) * P + p] = v;
+    if (a.flow && ch < 2) a.flow[gp * a.flow_ld + ch] = (ch == 0 ? x : y) - (ch == 0 ? (float)(p % a.W) : (float)(p / a.W));
+  }
+}
+
 int grid_for(long n, int block = 256) {
   long g = (n + block - 1) / block;
   if (g > 65536) g = 65536;
@@ -677,7 +724,7 @@ extern "C" int raft_corr_lookup(const float* pyramid, int B, int H, int W, int L
                                 int flow_ld, int* range_flag, raft_stream_t stream) {
   RAFT_REQUIRE(pyramid && coords && out, "raft_corr_lookup: null pointer");
   RAFT_REQUIRE(B > 0 && H > 0 && W > 0 && L >= 1 && L <= LK_MAXL, "raft_corr_lookup: bad sizes");
-  RAFT_REQUIRE(radius >= 1 && radius <= 4, "raft_corr_lookup: radius must be 1..4 (got %d)", radius);
+  RAFT_REQUIRE(radius >= 0 && radius <= 32, "raft_corr_lookup: radius must be 0..32 (got %d)", radius);
   RAFT_REQUIRE(coords_layout == 0 || coords_layout == 1, "raft_corr_lookup: bad coords_layout");
   RAFT_REQUIRE(out_layout == 0 || out_layout == 1, "raft_corr_lookup: bad out_layout");
   const int rd = 2 * radius + 1;
@@ -712,6 +759,10 @@ extern "C" int raft_corr_lookup(const float* pyramid, int B, int H, int W, int L
   a.range_flag = range_flag;
   dim3 grid((unsigned)cdiv_l((long)B * H * W, 4));
   hipStream_t s = as_stream(stream);
+  if (radius > 4 || radius < 1) {  // any other radius: the generic kernel
+    hipLaunchKernelGGL(corr_lookup_generic_kernel, dim3(grid_for((long)B * H * W * L * rd * rd)), dim3(256), 0, s, a);
+    return check_launch("raft_corr_lookup(generic radius)");
+  }
   // the 4-level case (RAFT) gets a tight instantiation; other level counts use LMAX = 6
 #define RAFT_LOOKUP_CASE(RR)                                                           \
   case RR:                                                                             \

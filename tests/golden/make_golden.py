@@ -158,6 +158,21 @@ def gen_raft_e2e(full_size: bool):
 
 
 @torch.no_grad()
+def gen_lookup_big_radius():
+    """CorrBlock / IterativeCorrBlock at radius 5 and 6 (the reference takes any r; RAFT uses 3, 4)
+    on the inputs of lookup_b2c64_16x20.npz."""
+    _, rcorr, _, _ = ref_modules()
+    from liteflownet3_correlation import IterativeCorrBlock
+    with np.load(os.path.join(HERE, "lookup_b2c64_16x20.npz")) as z:
+        f1, f2, coords = (torch.from_numpy(z[k]) for k in ("fmap1", "fmap2", "coords"))
+    out = {}
+    for r in (5, 6):
+        out[f"corr_r{r}"] = rcorr.CorrBlock(f1, f2, num_levels=4, radius=r)(coords)
+    out["iter_r6_err"] = (IterativeCorrBlock(f1, f2, radius=6, num_levels=4)(coords) - out["corr_r6"]).abs().max()
+    save("lookup_b2c64_16x20_r56.npz", **out)
+
+
+@torch.no_grad()
 def gen_caller():
     """Caller-side helpers of core/utils/utils.py: InputPadder pads (both modes, many sizes) and a
     padded tensor, forward_interpolate (scipy griddata 'nearest') on smooth / leaving / zero flows,
@@ -250,7 +265,7 @@ if __name__ == "__main__":
     a = ap.parse_args()
     jobs = {"lookup": gen_lookup, "update": gen_update_and_upsample, "enc": gen_encoders,
             "e2e": lambda: gen_raft_e2e(a.full_size), "demo": gen_raft_small_demo,
-            "config4": gen_config4, "bf16": gen_bf16, "caller": gen_caller}
+            "config4": gen_config4, "bf16": gen_bf16, "caller": gen_caller, "bigr": gen_lookup_big_radius}
     for k, f in jobs.items():
         if not a.only or k in a.only.split(","):
             f()

@@ -104,6 +104,34 @@ def test_lookup_golden(r):
     assert maxabs(out, g[f"corr_r{r}"]) < 1e-5
 
 
+@pytest.mark.parametrize("r", [5, 6])
+def test_lookup_any_radius_golden(r):
+    """Radius > 4 (the reference takes any r): the generic lookup kernels against the reference's
+    CorrBlock at r = 5, 6 (all-pairs and alternate paths)."""
+    from raft_optical_flow_amd import AlternateCorrBlock, CorrBlock
+    g = load_golden("lookup_b2c64_16x20.npz")
+    big = load_golden("lookup_b2c64_16x20_r56.npz")
+    cb = CorrBlock(t(g["fmap1"]), t(g["fmap2"]), num_levels=4, radius=r)
+    assert maxabs(cb(t(g["coords"])), big[f"corr_r{r}"]) < 1e-5
+    ab = AlternateCorrBlock(t(g["fmap1"]), t(g["fmap2"]), num_levels=4, radius=r)
+    assert maxabs(ab(t(g["coords"])), big[f"corr_r{r}"]) < 5e-5
+
+
+def test_lookup_radius_zero_and_alt_radius_seven_vs_oracle():
+    from raft_optical_flow_amd import CorrBlock, alt_cuda_corr
+    rng = np.random.default_rng(4)
+    f1 = rng.standard_normal((1, 32, 12, 15)).astype(np.float32)
+    f2 = rng.standard_normal((1, 32, 12, 15)).astype(np.float32)
+    coords = rng.uniform(-3, 17, (1, 2, 12, 15)).astype(np.float32)
+    ref = O.corr_lookup(O.corr_pyramid(f1, f2, 3), coords, 0)
+    assert maxabs(CorrBlock(t(f1), t(f2), num_levels=3, radius=0)(t(coords)), ref) < 1e-5
+    a1 = np.ascontiguousarray(f1.transpose(0, 2, 3, 1))
+    a2 = np.ascontiguousarray(f2.transpose(0, 2, 3, 1))
+    c5 = np.ascontiguousarray(coords.transpose(0, 2, 3, 1)[:, None])
+    corr, = alt_cuda_corr.forward(t(a1), t(a2), t(c5), 7)
+    assert maxabs(corr, O.alt_corr_forward(a1, a2, c5, 7)) < 1e-4
+
+
 def test_lookup_degenerate_level_nan():
     from raft_optical_flow_amd import CorrBlock
     g = load_golden("lookup_degenerate_6x8.npz")

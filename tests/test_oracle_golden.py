@@ -184,3 +184,11 @@ def test_alt_corr_torch_restatement_and_its_gradient():
     b = torch.tensor(f2[:1, :5, :5, :4], requires_grad=True)
     cc = torch.tensor(np.floor(c[:1, :1, :3, :4]) + rng.uniform(0.1, 0.9, (1, 1, 3, 4, 2)), requires_grad=True)
     assert torch.autograd.gradcheck(lambda x, y, z: T.alt_corr_forward(x, y, z, 1), (a, b, cc))
+
+
+@pytest.mark.parametrize("r", [5, 6])
+def test_lookup_big_radius_matches_reference(r):
+    g = load_golden("lookup_b2c64_16x20.npz")
+    big = load_golden("lookup_b2c64_16x20_r56.npz")
+    pyr = O.corr_pyramid(g["fmap1"], g["fmap2"], 4)
+    assert maxabs(O.corr_lookup(pyr, g["coords"], r), big[f"corr_r{r}"]) < 1e-5
