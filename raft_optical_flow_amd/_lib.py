@@ -11,7 +11,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("RAFT_HIP_LIB", os.path.join(_HERE, "libraft_hip.so"))
+LIB_PATH = os.environ.get("RAFT_HIP_LIB") or os.path.join(_HERE, "libraft_hip.so")
 
 c_int = ctypes.c_int
 c_float = ctypes.c_float

@@ -267,6 +267,8 @@ struct LookupArgs {
   // per level: W-1, H-1 and their reciprocals, rounded on the host exactly as
   // the device's correctly rounded 1.0f / x would
   float wm1[LK_MAXL], hm1[LK_MAXL], rw[LK_MAXL], rh[LK_MAXL];
+  // the same per level as {W-1, 1/(W-1), H-1, 1/(H-1)}: one 16-B per-lane load (lane-varying level)
+  f32x4 prm[LK_MAXL];
 };
 
 __device__ __forceinline__ void load_coords(const float* c, int layout, int b, int p, int P, float& x, float& y) {
@@ -351,7 +353,6 @@ __device__ __forceinline__ unsigned long long lk_clock(bool real) {
 
 template <int R, int LMAX>
 __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
-#pragma clang fp contract(off)  // the reference's bilinear is separate multiplies and adds
   constexpr int RD = 2 * R + 1;
   constexpr int WD = 2 * R + 2;  // integer window (<= 10 -> <= 4 tiles per axis)
   constexpr int RS = patch_rs<LMAX>();  // patch row stride (floats)
@@ -385,31 +386,46 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
   // all levels in flight together.  The window geometry is wave-uniform
   // (scalar); the pixel's map base too.
   const int ti = lane >> 4, tj = (lane >> 2) & 3, rr = lane & 3;
-  f32x4 v[LMAX];
-  bool ok[LMAX];
+  const int lrow = ti * 4 + rr;  // the lane's row of the 16-row patch
+  // phase 2's lane -> (level, offset) map and its level constants, loaded ahead of the tiles
+  // (so waiting for them leaves the tile loads in flight)
+  const int nlane = a.L * RD;
+  const bool col = lane < nlane;
+  // lane / RD by compares (3 VALU)
+  int lq = 0;
 #pragma unroll
-  for (int l = 0; l < LMAX; ++l) {
-    const float s = 1.0f / (float)(1 << l);  // coords / 2**l (exact power-of-two scaling)
+  for (int k = 1; k < LMAX; ++k) lq += lane >= k * RD ? 1 : 0;
+  const int l = col ? lq : 0;
+  const int ix = lane - l * RD;
+  const f32x4 prm = a.prm[l];
+  f32x4 v[LMAX];
+#pragma unroll
+  for (int k = 0; k < LMAX; ++k) {
+    const float s = 1.0f / (float)(1 << k);  // coords / 2**k (exact power-of-two scaling)
+    // the window geometry is wave-uniform: kept in SGPRs (SALU), not recomputed per lane.
+    // (The builtin, not an inline-asm v_readfirstlane: issued right behind the v_cvt that
+    // wrote its operand, the asm version read a stale value on gfx950 -- the hazard
+    // recognizer does not look into asm -- and fetched wrong tiles.)
     const int x0 = __builtin_amdgcn_readfirstlane((int)floorf(x * s)) - R;
     const int y0 = __builtin_amdgcn_readfirstlane((int)floorf(y * s)) - R;
     const int tyo = y0 >> 2, txo = x0 >> 2;  // arithmetic shift = floor division by 4 (negative too)
-    const int nty = ((y0 + WD - 1) >> 2) - tyo + 1;  // tiles the window needs (3 or 4)
-    const int ntx = ((x0 + WD - 1) >> 2) - txo + 1;
+    const int ntx = ((x0 + WD - 1) >> 2) - txo + 1;  // tile columns the window needs (3 or 4)
+    const Level& lv = a.lv[k];
     const int ty = tyo + ti, tx = txo + tj;
-    const Level& lv = a.lv[l];
-    // tile rows outside the window's WD rows are not fetched
-    ok[l] = (l < a.L) & valid & (ti < nty) & (tj < ntx) & ((unsigned)ty < (unsigned)lv.th) &
-            ((unsigned)tx < (unsigned)lv.tw) & ((unsigned)(ty * 4 + rr - y0) < (unsigned)WD);
-    // a raw buffer over this pixel's level map: lanes without a tile row to
-    // fetch pass an out-of-range offset and get zeros without a memory access
+    // only tile rows inside the window's WD rows are fetched (that also bounds the tile
+    // row count), only the window's tile columns, only tiles on the map
+    const bool ok = (k < a.L) & valid & (tj < ntx) & ((unsigned)(lrow + (tyo * 4 - y0)) < (unsigned)WD) &
+                    ((unsigned)ty < (unsigned)lv.th) & ((unsigned)tx < (unsigned)lv.tw);
+    // a raw buffer over this pixel's level map: lanes without a tile row to fetch pass an
+    // out-of-range offset and get zeros (the map's zero padding) without a memory access
     const float* mapb = a.pyr + lv.off + (long)gpc * lv.mapsz;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(mapb), (short)0, (int)(lv.mapsz * 4), 0x00020000);
-    const unsigned off = ok[l] ? (unsigned)((ty * lv.tw + tx) * 16 + rr * 4) * 4u : 0x80000000u;
+    const unsigned off = ok ? ((__umul24((unsigned)ty, (unsigned)lv.tw) + (unsigned)tx) * 64u + (unsigned)(rr * 16)) : 0x80000000u;
 #ifdef LK_ABL_NOLOAD  // timing ablation (dev builds only): no tile loads
-    v[l] = f32x4{(float)off, (float)(long)mapb, 0.f, 0.f};
+    v[k] = f32x4{(float)off, (float)(long)mapb, 0.f, 0.f};
 #else
-    v[l] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    v[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
 #endif
   }
 
@@ -419,33 +435,21 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
   // (shared through LDS) of level l, with the reference's arithmetic — offset
   // added to the centroid, bilinear_sampler's 2x/(W-1)-1, grid_sample's
   // (g+1)*((W-1)/2) — so corner indices and weights are the reference's
-  const int nlane = a.L * RD;
-  const bool col = lane < nlane;
-  const int l = col ? lane / RD : 0;
-  const int ix = lane - l * RD;
   int xw, xi, yw;
   float xt;
   {
-    float wm1 = a.wm1[0], hm1 = a.hm1[0], rw = a.rw[0], rh = a.rh[0], s = 1.0f;
-#pragma unroll
-    for (int k = 1; k < LMAX; ++k) {
-      const bool sel = l == k;
-      wm1 = sel ? a.wm1[k] : wm1;
-      hm1 = sel ? a.hm1[k] : hm1;
-      rw = sel ? a.rw[k] : rw;
-      rh = sel ? a.rh[k] : rh;
-      s = sel ? 1.0f / (float)(1 << k) : s;
-    }
+    const float wm1 = prm[0], rw = prm[1], hm1 = prm[2], rh = prm[3];
+    const float s = __builtin_ldexpf(1.0f, -l);
     axis_entry<R>(x * s, ix, wm1, rw, xw, xt, xi);
     int yi;
     float yt;
     axis_entry<R>(y * s, ix, hm1, rh, yw, yt, yi);
-    if (col) ytab[wv][lane] = int4{yw, __float_as_int(yt), __float_as_int(1.0f - yt), yi};
+    // .x: the row's float offset in the patch (row * RS), or the negative OFF_PATCH / NAN_POS code
+    if (col) ytab[wv][lane] = int4{yw >= 0 ? yw * RS : yw, __float_as_int(yt), __float_as_int(1.0f - yt), yi};
   }
-  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  // (lanes that fetched nothing hold zeros from the out-of-range buffer load)
 #pragma unroll
-  for (int k = 0; k < LMAX; ++k)
-    *reinterpret_cast<f32x4*>(&patch[wv][pidx<LMAX>(ti * 4 + rr, tj * 4, k)]) = ok[k] ? v[k] : zero;
+  for (int k = 0; k < LMAX; ++k) *reinterpret_cast<f32x4*>(&patch[wv][pidx<LMAX>(lrow, tj * 4, k)]) = v[k];
   LK_STAMP(3);
   // the patch and y-table are this wave's own: a wave-local barrier (the
   // block's four pixels never wait for each other)
@@ -455,7 +459,9 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
   if (!valid) return;
 
   // phase 3: lane (l, ix) walks its column iy = 0 .. 2r of output channels
-  // l*RD^2 + ix*RD + iy; the y-entries are LDS broadcasts
+  // l*RD^2 + ix*RD + iy; the y-entries are LDS broadcasts.  Bilinear as two horizontal
+  // interpolations and a vertical one, with fused multiply-adds (within 2 ulp of the
+  // reference's four products: the parity bound of the lookup is 1e-5 on O(1..10) values)
   const int ntap = a.L * RD * RD;
   const int cbase = l * RD * RD + ix * RD;
   const float ex = 1.0f - xt;
@@ -468,9 +474,11 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
 #pragma unroll
       for (int iy = 0; iy < RD; ++iy) {
         const int4 ye = ytab[wv][l * RD + iy];
-        const int ro = ye.x * RS;
+        const int ro = ye.x;
         const float ty = __int_as_float(ye.y), sS = __int_as_float(ye.z);
-        val[iy] = p0[ro] * (sS * ex) + p1[ro] * (sS * xt) + p0[ro + RS] * (ty * ex) + p1[ro + RS] * (ty * xt);
+        const float h0 = fmaf(p0[ro], ex, p1[ro] * xt);
+        const float h1 = fmaf(p0[ro + RS], ex, p1[ro + RS] * xt);
+        val[iy] = fmaf(sS, h0, ty * h1);
       }
     }
   } else if (col) {
@@ -478,11 +486,11 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
 #pragma unroll
     for (int iy = 0; iy < RD; ++iy) {
       const int4 ye = ytab[wv][l * RD + iy];
-      const int yw2 = ye.x;
+      const int yw2 = ye.x;  // row * RS, or a negative code
       const float ty = __int_as_float(ye.y), sS = __int_as_float(ye.z);
       const bool on = (xw | yw2) >= 0;
       const bool nan = xw == NAN_POS || yw2 == NAN_POS;
-      const int r0 = on ? yw2 : 0, c0 = on ? xw : 0;
+      const int r0 = on ? yw2 / RS : 0, c0 = on ? xw : 0;
       const float* pl = &patch[wv][0];
       const float v = pl[pidx<LMAX>(r0, c0, l)] * (sS * ex) + pl[pidx<LMAX>(r0, c0 + 1, l)] * (sS * xt) +
                       pl[pidx<LMAX>(r0 + 1, c0, l)] * (ty * ex) + pl[pidx<LMAX>(r0 + 1, c0 + 1, l)] * (ty * xt);
@@ -510,10 +518,10 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
   }
   LK_STAMP(4);
   if (a.range_flag && col) {  // f16x3 range guard: the output feeds the split-precision convc1
-    bool big = false;
+    float mx = fabsf(val[0]);
 #pragma unroll
-    for (int iy = 0; iy < RD; ++iy) big |= fabsf(val[iy]) > RAFT_RANGE_LIMIT;
-    if (big) *a.range_flag = 1;
+    for (int iy = 1; iy < RD; ++iy) mx = fmaxf(mx, fabsf(val[iy]));
+    if (mx > RAFT_RANGE_LIMIT) *a.range_flag = 1;
   }
 #ifdef LK_ABL_NOSTORE  // timing ablation (dev builds only): no output stores
   if (val[0] != -12345.f) return;
@@ -742,6 +750,7 @@ extern "C" int raft_corr_lookup(const float* pyramid, int B, int H, int W, int L
     volatile float one = 1.0f;  // host IEEE division, as the reference's 1 / (W - 1) path on the device
     a.rw[l] = one / a.wm1[l];
     a.rh[l] = one / a.hm1[l];
+    a.prm[l] = f32x4{a.wm1[l], a.rw[l], a.hm1[l], a.rh[l]};
   }
   a.pyr = pyramid;
   a.B = B;
