@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define RAFT_HIP_ABI_VERSION 6
+#define RAFT_HIP_ABI_VERSION 7
 
 /* Negative return codes (argument errors, raised before any launch). */
 #define RAFT_E_INVALID (-1)   /* bad size / null pointer / unsupported shape */
@@ -218,6 +218,13 @@ typedef struct raft_conv2d_params {
 /* Packed weight geometry for a conv (n_pad, k_pad in floats per row). */
 int raft_conv2d_packed_shape(int mode, int n, int kh, int kw, int cin, int* n_pad, int* k_pad);
 int raft_conv2d(const raft_conv2d_params* p, raft_stream_t stream);
+/* Two convs with no data dependence between them (core/update.py:276-285: convc2 of the corr
+ * branch beside convf2 of the flow branch), results identical to raft_conv2d(p0) then
+ * raft_conv2d(p1).  When both are halo-kernel convs of one shape class and precision, their
+ * tiles run side by side in ONE launch: the pair fills CUs that either alone leaves idle at
+ * one frame pair, with no second stream (a cross-stream fork/join costs a graph ~7 us per
+ * edge on ROCm).  Otherwise, or when one reads what the other writes, the two run in order. */
+int raft_conv2d_pair(const raft_conv2d_params* p0, const raft_conv2d_params* p1, raft_stream_t stream);
 /* fp32 packed weight [n_pad][k_pad] -> split form for RAFT_PREC_F16X3 / F16:
  * per row and 32-wide K-step, 32 f16 hi then 32 f16 lo (lo scaled by 2048);
  * out holds n_pad*k_pad*4 bytes, like the input. */

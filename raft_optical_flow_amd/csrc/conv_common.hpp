@@ -187,9 +187,17 @@ __device__ __forceinline__ f32x4 buf_load4(__amdgpu_buffer_rsrc_t r, unsigned vo
 
 }  // namespace
 
+// a validated conv with its packed-weight shape and operand byte sizes (raft_conv2d)
+struct HaloOperands {
+  raft_conv2d_params p;
+  int k_pad, n_pad;
+  unsigned w_bytes, in0_bytes, in1_bytes;
+};
+
 // conv_halo.hip: the halo-tiled LDS-DMA kernel for stride-1 "same" convs;
 // returns 1 (nothing launched) when the conv is not one it covers
-int conv_halo_launch(const raft_conv2d_params& p, int k_pad, int n_pad, unsigned w_bytes, unsigned in0_bytes,
-                     unsigned in1_bytes, hipStream_t s);
+int conv_halo_launch(const HaloOperands& o, hipStream_t s);
+// two independent convs of one shape class in one launch; 1 (nothing launched) if they do not qualify
+int conv_halo_launch_pair(const HaloOperands& o0, const HaloOperands& o1, hipStream_t s);
 
 }  // namespace raft

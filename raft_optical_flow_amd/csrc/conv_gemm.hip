@@ -736,7 +736,9 @@ extern "C" int raft_conv2d_packed_shape(int mode, int n, int kh, int kw, int cin
   return 0;
 }
 
-extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
+namespace {
+// raft_conv2d's argument checks and the GEMM view of the conv
+int conv_prepare(const raft_conv2d_params* pp, ConvArgs& a, HaloOperands& o) {
   RAFT_REQUIRE(pp != nullptr, "raft_conv2d: null params");
   const raft_conv2d_params& p = *pp;
   RAFT_REQUIRE(p.in0 && p.weight && p.out, "raft_conv2d: null in0/weight/out");
@@ -751,7 +753,6 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
   RAFT_REQUIRE(p.in0_ld >= p.in0_c && (p.in1_c == 0 || p.in1_ld >= p.in1_c) && p.out_ld >= 1,
                "raft_conv2d: leading dimension smaller than channel count");
   const int ctot = p.in0_c + p.in1_c;
-  ConvArgs a;
   a.p = p;
   a.M = p.batch * p.out_h * p.out_w;
   a.ctot = ctot;
@@ -815,6 +816,55 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
     default:
       return set_error(RAFT_E_INVALID, "raft_conv2d: unknown epilogue %d", p.epilogue);
   }
+  RAFT_REQUIRE(p.precision == RAFT_PREC_FP32 || p.precision == RAFT_PREC_F16X3 || p.precision == RAFT_PREC_F16 ||
+                   p.precision == RAFT_PREC_BF16,
+               "raft_conv2d: unknown precision %d", p.precision);
+  o.p = p;
+  o.k_pad = k_pad;
+  o.n_pad = n_pad;
+  o.w_bytes = a.w_bytes;
+  o.in0_bytes = a.in0_bytes;
+  o.in1_bytes = a.in1_bytes;
+  return 0;
+}
+
+bool small_n(const raft_conv2d_params& p) { return p.n <= 4 && p.mode == RAFT_CONV_VEC; }
+
+// byte range [lo, hi) of an NHWC row operand: rows x ld floats
+void row_range(const void* ptr, long rows, int ld, uintptr_t& lo, uintptr_t& hi) {
+  lo = (uintptr_t)ptr;
+  hi = lo + (uintptr_t)(rows * (long)ld * 4);
+}
+bool overlaps(const void* a, long ra, int lda, const void* b, long rb, int ldb) {
+  if (!a || !b) return false;
+  uintptr_t a0, a1, b0, b1;
+  row_range(a, ra, lda, a0, a1);
+  row_range(b, rb, ldb, b0, b1);
+  return a0 < b1 && b0 < a1;
+}
+// does conv y read anything conv x writes?
+bool reads_output_of(const raft_conv2d_params& y, const raft_conv2d_params& x) {
+  const long rin = (long)y.batch * y.in_h * y.in_w, rout = (long)x.batch * x.out_h * x.out_w;
+  const void* outs[2] = {x.out, x.out1};
+  const int olds[2] = {x.out_ld, x.out1_ld};
+  const void* ins[5] = {y.in0, y.in1, y.aux0, y.aux1, y.add0};
+  const int ilds[5] = {y.in0_ld, y.in1_ld, y.aux0_ld, y.aux1_ld, y.add0_ld};
+  const long irows[5] = {rin, rin, (long)y.batch * y.out_h * y.out_w, (long)y.batch * y.out_h * y.out_w,
+                         (long)y.batch * y.out_h * y.out_w};
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 5; ++j)
+      if (overlaps(outs[i], rout, olds[i], ins[j], irows[j], ilds[j])) return true;
+  return false;
+}
+}  // namespace
+
+extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
+  ConvArgs a;
+  HaloOperands o;
+  const int rc = conv_prepare(pp, a, o);
+  if (rc) return rc;
+  const raft_conv2d_params& p = *pp;
+  const int n_pad = o.n_pad;
   hipStream_t s = as_stream(stream);
   if (p.n <= 4 && p.mode == RAFT_CONV_VEC) {
     if (p.n <= 2 && p.kh == 3 && p.kw == 3 && p.stride_h == 1 && p.stride_w == 1 && p.pad_h == 1 &&
@@ -836,11 +886,7 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
       hipLaunchKernelGGL(conv_smalln_kernel<4>, grid, dim3(256), 0, s, a);
     return check_launch("raft_conv2d(small n)");
   }
-  RAFT_REQUIRE(p.precision == RAFT_PREC_FP32 || p.precision == RAFT_PREC_F16X3 || p.precision == RAFT_PREC_F16 ||
-                   p.precision == RAFT_PREC_BF16,
-               "raft_conv2d: unknown precision %d", p.precision);
-  if (p.mode == RAFT_CONV_VEC && conv_halo_launch(p, k_pad, n_pad, a.w_bytes, a.in0_bytes, a.in1_bytes, s) == 0)
-    return check_launch("raft_conv2d(halo)");
+  if (p.mode == RAFT_CONV_VEC && conv_halo_launch(o, s) == 0) return check_launch("raft_conv2d(halo)");
   a.gn = n_pad / BN;
   const long tiles = (long)cdiv(a.M, BM) * a.gn;
   RAFT_REQUIRE(tiles < (1L << 31), "raft_conv2d: too many tiles");
@@ -849,4 +895,20 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
   const bool two = tiles < 1024 && a.K / BK >= 4;
   launch_gemm(a, grid, two, s);
   return check_launch("raft_conv2d");
+}
+
+extern "C" int raft_conv2d_pair(const raft_conv2d_params* p0, const raft_conv2d_params* p1, raft_stream_t stream) {
+  ConvArgs a0, a1;
+  HaloOperands o0, o1;
+  int rc = conv_prepare(p0, a0, o0);
+  if (rc) return rc;
+  rc = conv_prepare(p1, a1, o1);
+  if (rc) return rc;
+  // one launch only when neither reads what the other writes (otherwise: in order, as two calls)
+  const bool independent = !reads_output_of(*p1, *p0) && !reads_output_of(*p0, *p1);
+  if (independent && !small_n(*p0) && !small_n(*p1) && conv_halo_launch_pair(o0, o1, as_stream(stream)) == 0)
+    return check_launch("raft_conv2d_pair(halo)");
+  rc = raft_conv2d(p0, stream);
+  if (rc) return rc;
+  return raft_conv2d(p1, stream);
 }

@@ -59,6 +59,13 @@ struct HaloArgs {
   unsigned w_bytes, in0_bytes, in1_bytes;
 };
 
+// One launch runs the tiles of one conv, or of two independent convs of the same shape
+// class (raft_conv2d_pair): tiles [0, tiles0) are a[0]'s, the rest a[1]'s.
+struct HaloLaunch {
+  HaloArgs a[2];
+  int tiles0;
+};
+
 // Smallest patch ring such that chunk c's patch never lands in the slot of a
 // chunk that is still read.  In super-steps of U K-steps: chunk c's patch is
 // part of load set cT/U, issued during super-step cT/U - D (the prologue's
@@ -84,15 +91,16 @@ template <int KH, int KW, int BNT>
 struct HaloCfg {
   static constexpr int T = KH * KW;
   static constexpr int U = (BNT == 32 && T > 1) ? 4 : 2;  // K-steps per super-step
+  static constexpr int LB = HALO_LDS;
   static constexpr int PH = HTH + KH - 1, PW = HTW + KW - 1, NPIX = PH * PW;
   static constexpr int PI = (NPIX + 7) / 8;  // 1-KiB DMA pieces per patch
   // load sets in flight ahead of the super-step: 3, or 2 where 3 does not fit
 #ifdef HALO_D  // dev builds: deeper load rings where they fit
-  static constexpr int D = halo_lds_bytes(T, U, HALO_D, BNT, PI) <= HALO_LDS   ? HALO_D
-                           : halo_lds_bytes(T, U, 3, BNT, PI) <= HALO_LDS ? 3
+  static constexpr int D = halo_lds_bytes(T, U, HALO_D, BNT, PI) <= LB   ? HALO_D
+                           : halo_lds_bytes(T, U, 3, BNT, PI) <= LB ? 3
                                                                           : 2;
 #else
-  static constexpr int D = halo_lds_bytes(T, U, 3, BNT, PI) <= HALO_LDS ? 3 : 2;
+  static constexpr int D = halo_lds_bytes(T, U, 3, BNT, PI) <= LB ? 3 : 2;
 #endif
   static constexpr int PA = patch_slots(T, U, D);
   static constexpr int SB = U * (D + 1);  // weight-block ring (K-steps)
@@ -192,7 +200,7 @@ __device__ __forceinline__ void split8(const f32x4 x0, const f32x4 x1, h8& hi, h
 }
 
 template <int KH, int KW, int BNT, int PREC>
-__global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
+__global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
   using C = HaloCfg<KH, KW, BNT>;
   constexpr int T = C::T, U = C::U, D = C::D, PW = C::PW, NPIX = C::NPIX, PI = C::PI, PA = C::PA, SB = C::SB;
   constexpr int NBI = BNT / 8;      // 1-KiB DMA pieces per weight block (one K-step)
@@ -205,7 +213,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
   // ready fragments; 1x1 convs (a patch per K-step, D = 2) keep fp32 patches
   // moved by LDS-DMA and split in the MFMA waves.
   constexpr bool LSPLIT = T > 1 && D == 3;
-  static_assert(D >= 2 && C::LDS_B + C::LDS_A <= HALO_LDS, "LDS budget");
+  static_assert(D >= 2 && C::LDS_B + C::LDS_A <= C::LB, "LDS budget");
   static_assert(NWP >= 1 && NBI % NWP == 0, "a wave's weight pieces lie in one K-step");
   static_assert(U % 2 == 0 && (T == 1 || T >= U), "fragment parity; at most one chunk start per load set");
   __shared__ __attribute__((aligned(1024))) char smem[C::LDS_B + C::LDS_A];
@@ -213,14 +221,17 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
 #ifdef STAMPS
   const unsigned long long r_entry = hstamp_real(), c_entry = hstamp_now();
 #endif
-  const raft_conv2d_params& p = a.p;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool loader = w >= 4;  // waves 4-7 move the operands, waves 0-3 compute
   const int lw = w & 3;
 
   // tile (N fastest: an output tile's N-tiles share its input patch in L2)
-  const int q = xcd_tile(blockIdx.x, gridDim.x);
+  int q = xcd_tile(blockIdx.x, gridDim.x);
+  const int prob = q >= hl.tiles0 ? 1 : 0;
+  q -= prob * hl.tiles0;
+  const HaloArgs& a = hl.a[prob];
+  const raft_conv2d_params& p = a.p;
   const int nt = q % a.gn, st = q / a.gn;
   const int per = a.tx_n * a.ty_n;
   const int b = st / per, sr = st - b * per;
@@ -659,20 +670,67 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloArgs a) {
 }
 
 template <int KH, int KW, int PREC>
-void launch_halo_p(const HaloArgs& a, int bn, dim3 grid, hipStream_t s) {
+void launch_halo_p(const HaloLaunch& l, int bn, dim3 grid, hipStream_t s) {
   if (bn == 64)
-    hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 64, PREC>), grid, dim3(512), 0, s, a);
+    hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 64, PREC>), grid, dim3(512), 0, s, l);
   else
-    hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 32, PREC>), grid, dim3(512), 0, s, a);
+    hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 32, PREC>), grid, dim3(512), 0, s, l);
 }
 template <int KH, int KW>
-void launch_halo_k(const HaloArgs& a, int bn, dim3 grid, hipStream_t s) {
-  if (a.p.precision == RAFT_PREC_F16X3)
-    launch_halo_p<KH, KW, RAFT_PREC_F16X3>(a, bn, grid, s);
-  else if (a.p.precision == RAFT_PREC_BF16)
-    launch_halo_p<KH, KW, RAFT_PREC_BF16>(a, bn, grid, s);
+void launch_halo_k(const HaloLaunch& l, int bn, dim3 grid, hipStream_t s) {
+  const int prec = l.a[0].p.precision;
+  if (prec == RAFT_PREC_F16X3)
+    launch_halo_p<KH, KW, RAFT_PREC_F16X3>(l, bn, grid, s);
+  else if (prec == RAFT_PREC_BF16)
+    launch_halo_p<KH, KW, RAFT_PREC_BF16>(l, bn, grid, s);
   else
-    launch_halo_p<KH, KW, RAFT_PREC_F16>(a, bn, grid, s);
+    launch_halo_p<KH, KW, RAFT_PREC_F16>(l, bn, grid, s);
+}
+
+bool halo_enabled() {
+  static const bool enabled = [] {
+    const char* e = getenv("RAFT_CONV_HALO");
+    return !(e && e[0] == '0');
+  }();
+  return enabled;
+}
+
+// The halo kernel's view of a conv it covers (stride 1, "same" padding, 1x1 / 3x3 / 1x5 /
+// 5x1, VEC mode, split-weight precisions), all but the N-tile width; false otherwise.
+bool halo_problem(const HaloOperands& o, HaloArgs& a) {
+  const raft_conv2d_params& p = o.p;
+  if (p.mode != RAFT_CONV_VEC || p.stride_h != 1 || p.stride_w != 1) return false;
+  if (p.precision != RAFT_PREC_F16X3 && p.precision != RAFT_PREC_F16 && p.precision != RAFT_PREC_BF16) return false;
+  const int kh = p.kh, kw = p.kw;
+  const bool shape = (kh == 1 && kw == 1) || (kh == 3 && kw == 3) || (kh == 1 && kw == 5) || (kh == 5 && kw == 1);
+  if (!shape || p.pad_h != (kh - 1) / 2 || p.pad_w != (kw - 1) / 2) return false;
+  if (p.out_h != p.in_h || p.out_w != p.in_w || p.n <= 4) return false;
+  a.p = p;
+  a.K = o.k_pad;
+  a.nch = o.k_pad / (kh * kw) / 32;
+  a.nk = a.nch * kh * kw;
+  a.tx_n = cdiv(p.out_w, HTW);
+  a.ty_n = cdiv(p.out_h, HTH);
+  a.w_bytes = o.w_bytes;
+  a.in0_bytes = o.in0_bytes;
+  a.in1_bytes = o.in1_bytes;
+  a.gn = 0;
+  return true;
+}
+
+long halo_spatial(const HaloArgs& a) { return (long)a.p.batch * a.tx_n * a.ty_n; }
+
+void launch_halo(const HaloLaunch& l, int bn, long tiles, hipStream_t s) {
+  const raft_conv2d_params& p = l.a[0].p;
+  dim3 grid((unsigned)tiles);
+  if (p.kh == 1 && p.kw == 1)
+    launch_halo_k<1, 1>(l, bn, grid, s);
+  else if (p.kh == 3)
+    launch_halo_k<3, 3>(l, bn, grid, s);
+  else if (p.kh == 1)
+    launch_halo_k<1, 5>(l, bn, grid, s);
+  else
+    launch_halo_k<5, 1>(l, bn, grid, s);
 }
 
 }  // namespace
@@ -683,49 +741,41 @@ extern "C" int raft_debug_hstamps(unsigned long long* host, int n) {
 }
 #endif
 
-// Launches the halo kernel when the conv is one it covers (stride 1, "same"
-// padding, 1x1 / 3x3 / 1x5 / 5x1, VEC mode, split-weight precisions);
-// returns 1 without launching otherwise.  Arguments are already validated by
-// raft_conv2d.
-int conv_halo_launch(const raft_conv2d_params& p, int k_pad, int n_pad, unsigned w_bytes, unsigned in0_bytes,
-                     unsigned in1_bytes, hipStream_t s) {
-  static const bool enabled = [] {
-    const char* e = getenv("RAFT_CONV_HALO");
-    return !(e && e[0] == '0');
-  }();
-  if (!enabled) return 1;
-  if (p.mode != RAFT_CONV_VEC || p.stride_h != 1 || p.stride_w != 1) return 1;
-  if (p.precision != RAFT_PREC_F16X3 && p.precision != RAFT_PREC_F16 && p.precision != RAFT_PREC_BF16) return 1;
-  const int kh = p.kh, kw = p.kw;
-  const bool shape = (kh == 1 && kw == 1) || (kh == 3 && kw == 3) || (kh == 1 && kw == 5) || (kh == 5 && kw == 1);
-  if (!shape || p.pad_h != (kh - 1) / 2 || p.pad_w != (kw - 1) / 2) return 1;
-  if (p.out_h != p.in_h || p.out_w != p.in_w || p.n <= 4) return 1;
-  HaloArgs a;
-  a.p = p;
-  a.K = k_pad;
-  a.nch = k_pad / (kh * kw) / 32;
-  a.nk = a.nch * kh * kw;
-  a.tx_n = cdiv(p.out_w, HTW);
-  a.ty_n = cdiv(p.out_h, HTH);
-  a.w_bytes = w_bytes;
-  a.in0_bytes = in0_bytes;
-  a.in1_bytes = in1_bytes;
-  const long spatial = (long)p.batch * a.tx_n * a.ty_n;
+// Launches the halo kernel when the conv is one it covers; returns 1 without launching
+// otherwise.  Arguments are already validated by raft_conv2d.
+int conv_halo_launch(const HaloOperands& o, hipStream_t s) {
+  HaloLaunch l;
+  if (!halo_enabled() || !halo_problem(o, l.a[0])) return 1;
+  const long spatial = halo_spatial(l.a[0]);
   // one work-group per CU (LDS): 64 output channels per work-group unless
   // 32 still fits the grid in one round of 256 CUs with half of them idle at 64
-  const int bn = spatial * (n_pad / 64) > 128 ? 64 : 32;
-  a.gn = n_pad / bn;
-  const long tiles = spatial * a.gn;
+  const int bn = spatial * (o.n_pad / 64) > 128 ? 64 : 32;
+  l.a[0].gn = o.n_pad / bn;
+  const long tiles = spatial * l.a[0].gn;
   if (tiles >= (1L << 31)) return 1;
-  dim3 grid((unsigned)tiles);
-  if (kh == 1 && kw == 1)
-    launch_halo_k<1, 1>(a, bn, grid, s);
-  else if (kh == 3)
-    launch_halo_k<3, 3>(a, bn, grid, s);
-  else if (kh == 1)
-    launch_halo_k<1, 5>(a, bn, grid, s);
-  else
-    launch_halo_k<5, 1>(a, bn, grid, s);
+  l.a[1] = l.a[0];
+  l.tiles0 = (int)tiles;
+  launch_halo(l, bn, tiles, s);
+  return 0;
+}
+
+// Two independent convs of one shape class and precision in one launch (their tiles side
+// by side in the grid, one N-tile width for both); returns 1 without launching when the
+// pair does not qualify.
+int conv_halo_launch_pair(const HaloOperands& o0, const HaloOperands& o1, hipStream_t s) {
+  HaloLaunch l;
+  if (!halo_enabled() || !halo_problem(o0, l.a[0]) || !halo_problem(o1, l.a[1])) return 1;
+  const raft_conv2d_params &p0 = o0.p, &p1 = o1.p;
+  if (p0.kh != p1.kh || p0.kw != p1.kw || p0.precision != p1.precision) return 1;
+  const long s0 = halo_spatial(l.a[0]), s1 = halo_spatial(l.a[1]);
+  const int bn = s0 * (o0.n_pad / 64) + s1 * (o1.n_pad / 64) > 128 ? 64 : 32;
+  if (o0.n_pad % bn || o1.n_pad % bn) return 1;
+  l.a[0].gn = o0.n_pad / bn;
+  l.a[1].gn = o1.n_pad / bn;
+  const long t0 = s0 * l.a[0].gn, tiles = t0 + s1 * l.a[1].gn;
+  if (tiles >= (1L << 31)) return 1;
+  l.tiles0 = (int)t0;
+  launch_halo(l, bn, tiles, s);
   return 0;
 }
 

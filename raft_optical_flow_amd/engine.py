@@ -349,16 +349,28 @@ def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool
     followed by coords1 += delta_flow (core/raft.py:232).  Assumes ub.corr and the
     flow slot of HX were filled by the lookup and plan_gru_context ran for this pair."""
     flow = Rows(ub.hx, ub.flow_off(pu), 2)
-    # the flow branch (convf1 -> convf2) runs on the side stream beside the corr branch
-    # (RAFT_FLOW_SIDE=0: on the main stream, no fork / join)
-    side = os.environ.get("RAFT_FLOW_SIDE", "1") != "0"
     cf = Rows(ub.cf)
+    # RAFT-full: one stream; convc2 (corr branch) and convf2 (flow branch) are two 3x3 halo
+    # convs with no data between them, run as ONE launch (raft_conv2d_pair: 168 + 56
+    # work-groups fill the CUs that convc2 alone leaves idle).  RAFT_CONV_PAIR=0: the flow
+    # branch on the side stream instead (a graph fork / join, as in round 1).
+    # RAFT-small (different conv shapes per branch): side stream unless RAFT_FLOW_SIDE=0.
+    pair = not pu.small and os.environ.get("RAFT_CONV_PAIR", "1") != "0"
+    side = not pair and os.environ.get("RAFT_FLOW_SIDE", "1") != "0"
     if side:
         L.append(K.FORK)
     if pu.small:
         _conv(L, pu.convf1, flow, B, h, w, Rows(ub.flo1), epilogue=_lib.EPI_RELU, side=side)
         _conv(L, pu.convf2, Rows(ub.flo1), B, h, w, cf.sub(96, 32), epilogue=_lib.EPI_RELU, side=side)
         _conv(L, pu.convc1, Rows(ub.corr), B, h, w, cf.sub(0, 96), epilogue=_lib.EPI_RELU)
+    elif pair:
+        _conv(L, pu.convf1, flow, B, h, w, Rows(ub.flo1), epilogue=_lib.EPI_RELU)
+        _conv(L, pu.convc1, Rows(ub.corr), B, h, w, Rows(ub.cor1), epilogue=_lib.EPI_RELU)
+        c2 = conv_params(pu.convc2, Rows(ub.cor1), B, h, w, cf.sub(0, 192), epilogue=_lib.EPI_RELU,
+                         range_flag=_GUARD["flag"])
+        f2 = conv_params(pu.convf2, Rows(ub.flo1), B, h, w, cf.sub(192, 64), epilogue=_lib.EPI_RELU,
+                         range_flag=_GUARD["flag"])
+        L.append(K.conv_pair_launch(c2, f2))
     else:
         _conv(L, pu.convf1, flow, B, h, w, Rows(ub.flo1), epilogue=_lib.EPI_RELU, side=side)
         _conv(L, pu.convf2, Rows(ub.flo1), B, h, w, cf.sub(192, 64), epilogue=_lib.EPI_RELU, side=side)

@@ -247,6 +247,11 @@ def conv_launch(params: ConvParams, side=False) -> Launch:
     return Launch("raft_conv2d", ctypes.byref(params), keep=params, side=side)
 
 
+def conv_pair_launch(p0: ConvParams, p1: ConvParams) -> Launch:
+    """Two independent convs as one launch where the halo kernel can take both (raft_conv2d_pair)."""
+    return Launch("raft_conv2d_pair", ctypes.byref(p0), ctypes.byref(p1), keep=(p0, p1))
+
+
 FORK = "fork"   # side stream waits for the main stream
 JOIN = "join"   # main stream waits for the side stream
 

@@ -144,7 +144,8 @@ class RAFT(nn.Module):
         prec = prec or self.resolved_precision()
         pk = self.packed(device, prec)
         # the stream layout knobs are read when a plan is built, so they are part of its key
-        knobs = (os.environ.get("RAFT_CTX_SIDE", "1"), os.environ.get("RAFT_FLOW_SIDE", "1"))
+        knobs = (os.environ.get("RAFT_CTX_SIDE", "1"), os.environ.get("RAFT_FLOW_SIDE", "1"),
+                 os.environ.get("RAFT_CONV_PAIR", "1"))
         key = (batch, height, width, iters, bool(test_mode), bool(self.args.alternate_corr), bool(flow_init), prec,
                knobs)
         pl = self._plans.get(key)

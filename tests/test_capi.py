@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_queries_without_gpu():
     lib = _lib.load()
-    assert lib.raft_hip_abi_version() == _lib.ABI_VERSION == 6
+    assert lib.raft_hip_abi_version() == _lib.ABI_VERSION == 7
     assert lib.raft_hip_arch() == b"gfx950"
     # size queries are pure host arithmetic
     assert lib.raft_corr_pyramid_floats(1, 55, 128, 4) == 7040 * 16 * (14 * 32 + 7 * 16 + 4 * 8 + 2 * 4)
@@ -55,3 +55,5 @@ def test_argument_errors_are_reported_without_launch():
     assert b"null" in lib.raft_hip_last_error()
     rc = lib.raft_corr_build(16, 16, 256, 1, 8, 8, 102, 4, 10.0, 16, None)  # C % 4 != 0
     assert rc == -1 and b"multiple of 4" in lib.raft_hip_last_error()
+    rc = lib.raft_conv2d_pair(None, None, None)
+    assert rc == -1 and b"null params" in lib.raft_hip_last_error()

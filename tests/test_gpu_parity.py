@@ -397,6 +397,56 @@ def test_conv2d_two_segments_and_gru_epilogues(prec):
     assert maxabs(hn, ref) < 1e-5
 
 
+@pytest.mark.parametrize("prec", ["f16x3", "bf16", "fp32"])
+@pytest.mark.parametrize("kh,kw,c0,n0,c1,n1,B,H,W", [
+    (3, 3, 256, 192, 128, 64, 1, 55, 128),   # convc2 | convf2 of RAFT-full at config 2 (one launch)
+    (3, 3, 64, 96, 32, 40, 2, 13, 21),       # ragged tiles, N padded, two images
+    (1, 5, 96, 128, 64, 64, 1, 9, 19),       # another shape class
+    (3, 3, 64, 64, 64, 64, 1, 8, 16),        # 3x3 beside 1x1 below: shapes differ -> two launches
+])
+def test_conv2d_pair_equals_two_convs(kh, kw, c0, n0, c1, n1, B, H, W, prec):
+    """raft_conv2d_pair == raft_conv2d twice (bit for bit: each tile runs the same K-walk)."""
+    from raft_optical_flow_amd import kernels as K
+    from raft_optical_flow_amd import _lib
+    g = torch.Generator().manual_seed(c0 + n1)
+    shapes = [(c0, n0, kh, kw), (c1, n1, kh, kw) if (c1, n1) != (64, 64) or kh == 1 else (c1, n1, 1, 1)]
+    xs, pcs, outs_pair, outs_seq = [], [], [], []
+    for cin, cout, a, b in shapes:
+        x = torch.randn(B, cin, H, W, generator=g)
+        w = torch.randn(cout, cin, a, b, generator=g) / np.sqrt(cin * a * b)
+        pc = K.pack_conv(w, torch.randn(cout, generator=g), 1, ((a - 1) // 2, (b - 1) // 2), device=DEV)
+        pc.precision = _lib.PRECISIONS[prec]
+        xs.append(K.Rows(K.nchw_to_rows(x.to(DEV))))
+        pcs.append(pc)
+        outs_pair.append(K.Rows(torch.full((B * H * W, cout), 7.0, device=DEV)))
+        outs_seq.append(K.Rows(torch.full((B * H * W, cout), 7.0, device=DEV)))
+    prm = [K.conv_params(pcs[i], xs[i], B, H, W, outs_pair[i], epilogue=_lib.EPI_RELU) for i in range(2)]
+    K.conv_pair_launch(prm[0], prm[1])(K.stream_handle())
+    for i in range(2):
+        K.conv2d_rows(pcs[i], xs[i], B, H, W, outs_seq[i], epilogue=_lib.EPI_RELU)
+    torch.cuda.synchronize()
+    for i in range(2):
+        assert torch.equal(outs_pair[i].t, outs_seq[i].t), (i, maxabs(outs_pair[i].t, outs_seq[i].t))
+
+
+def test_conv2d_pair_with_a_dependence_runs_in_order():
+    """The second conv reads the first one's output: the pair must not share a launch."""
+    from raft_optical_flow_amd import kernels as K
+    from raft_optical_flow_amd import _lib
+    g = torch.Generator().manual_seed(5)
+    B, H, W = 1, 16, 32
+    x = K.Rows(K.nchw_to_rows(torch.randn(B, 64, H, W, generator=g).to(DEV)))
+    pa = K.pack_conv(torch.randn(64, 64, 3, 3, generator=g) * 0.05, torch.zeros(64), 1, (1, 1), device=DEV)
+    pb = K.pack_conv(torch.randn(64, 64, 3, 3, generator=g) * 0.05, torch.zeros(64), 1, (1, 1), device=DEV)
+    mid, out, mid2, out2 = (K.Rows(torch.zeros(B * H * W, 64, device=DEV)) for _ in range(4))
+    K.conv_pair_launch(K.conv_params(pa, x, B, H, W, mid, epilogue=_lib.EPI_RELU),
+                       K.conv_params(pb, mid, B, H, W, out, epilogue=_lib.EPI_RELU))(K.stream_handle())
+    K.conv2d_rows(pa, x, B, H, W, mid2, epilogue=_lib.EPI_RELU)
+    K.conv2d_rows(pb, mid2, B, H, W, out2, epilogue=_lib.EPI_RELU)
+    torch.cuda.synchronize()
+    assert torch.equal(out.t, out2.t) and float(out.t.abs().max()) > 0
+
+
 # ----------------------------------------------------------------------------- blocks
 
 
