@@ -211,8 +211,10 @@ typedef struct raft_conv2d_params {
  * whose outputs feed a split-precision conv (conv epilogues, the correlation lookups) can
  * raise a device flag when any output exceeds RAFT_RANGE_LIMIT = 2^15 (NaN does not raise
  * it: a NaN input propagates as in fp32); the caller checks the flag after the forward and
- * re-runs it with RAFT_PREC_FP32 (or raises).  InstanceNorm outputs are bounded by
- * sqrt(H*W) and the prepared images by 1, so they need no flag. */
+ * re-runs it with RAFT_PREC_FP32 (or raises).  Producers with bounded outputs need no flag:
+ * InstanceNorm outputs (|x| <= sqrt(H*W)), the prepared images (|x| <= 1) and the GRU
+ * epilogues (sigmoid / tanh blends of |h| <= 1); neither do convs whose outputs only feed
+ * fp32 consumers (the raw convs of an InstanceNorm encoder, the flow head's first conv). */
 #define RAFT_RANGE_LIMIT 32768.0f
 
 /* Packed weight geometry for a conv (n_pad, k_pad in floats per row). */

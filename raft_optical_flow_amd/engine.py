@@ -208,8 +208,10 @@ def plan_encoder_trunk(L, A: Arena, pe: PackedEncoder, x: Rows, n_img, h, w):
     """Everything of the encoder but its final 1x1 conv.  Returns (rows, h, w)."""
     ho, wo = K.conv_out_hw(pe.stem, h, w)
     if pe.norm == "instance":
+        # (the raw conv outputs of an InstanceNorm encoder feed the fp32 statistics and the
+        # normalisation, whose outputs are bounded by sqrt(H*W): no range guard, raft_hip.h)
         t = Rows(A.rows(n_img * ho * wo, pe.stem.n))
-        _conv(L, pe.stem, x, n_img, h, w, t)
+        _conv(L, pe.stem, x, n_img, h, w, t, range_flag=None)
         st = _in_stats(L, A, t, n_img, ho * wo)
         x = _in_apply(L, A, t, st, n_img, ho * wo, 1)
     else:
@@ -232,14 +234,14 @@ def _plan_residual(L, A, pe, d, x: Rows, n, h, w):
     npx = n * ho * wo
     if pe.norm == "instance":
         t1 = Rows(A.rows(npx, c1.n))
-        _conv(L, c1, x, n, h, w, t1)
+        _conv(L, c1, x, n, h, w, t1, range_flag=None)
         y1 = _in_apply(L, A, t1, _in_stats(L, A, t1, n, ho * wo), n, ho * wo, 1)
         t2 = Rows(A.rows(npx, c2.n))
-        _conv(L, c2, y1, n, ho, wo, t2)
+        _conv(L, c2, y1, n, ho, wo, t2, range_flag=None)
         st2 = _in_stats(L, A, t2, n, ho * wo)
         if ds is not None:
             t3 = Rows(A.rows(npx, ds.n))
-            _conv(L, ds, x, n, h, w, t3)
+            _conv(L, ds, x, n, h, w, t3, range_flag=None)
             out = _in_apply(L, A, t2, st2, n, ho * wo, 2, resid=t3, rst=_in_stats(L, A, t3, n, ho * wo))
         else:
             out = _in_apply(L, A, t2, st2, n, ho * wo, 2, resid=x)
@@ -262,17 +264,17 @@ def _plan_bottleneck(L, A, pe, d, x: Rows, n, h, w):
     ho, wo = K.conv_out_hw(c2, h, w)
     if pe.norm == "instance":
         t1 = Rows(A.rows(n * h * w, c1.n))
-        _conv(L, c1, x, n, h, w, t1)
+        _conv(L, c1, x, n, h, w, t1, range_flag=None)
         y1 = _in_apply(L, A, t1, _in_stats(L, A, t1, n, h * w), n, h * w, 1)
         t2 = Rows(A.rows(n * ho * wo, c2.n))
-        _conv(L, c2, y1, n, h, w, t2)
+        _conv(L, c2, y1, n, h, w, t2, range_flag=None)
         y2 = _in_apply(L, A, t2, _in_stats(L, A, t2, n, ho * wo), n, ho * wo, 1)
         t3 = Rows(A.rows(n * ho * wo, c3.n))
-        _conv(L, c3, y2, n, ho, wo, t3)
+        _conv(L, c3, y2, n, ho, wo, t3, range_flag=None)
         st3 = _in_stats(L, A, t3, n, ho * wo)
         if ds is not None:
             t4 = Rows(A.rows(n * ho * wo, ds.n))
-            _conv(L, ds, x, n, h, w, t4)
+            _conv(L, ds, x, n, h, w, t4, range_flag=None)
             out = _in_apply(L, A, t3, st3, n, ho * wo, 2, resid=t4, rst=_in_stats(L, A, t4, n, ho * wo))
         else:
             out = _in_apply(L, A, t3, st3, n, ho * wo, 2, resid=x)
@@ -383,20 +385,21 @@ def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool
     hrows = ub.h(pu)
     for (zr, q, _), ctx in zip(pu.gru, ub.ctx):
         c = Rows(ctx)
+        # (z, r*h and the new h are sigmoid / tanh blends of |h| <= 1: no range guard)
         _conv(L, zr, ub.gru_in(pu), B, h, w, Rows(ub.z), epilogue=_lib.EPI_GRU_ZR, split=hd, aux0=hrows,
-              out1=Rows(ub.rh), add0=c.sub(0, 2 * hd))
+              out1=Rows(ub.rh), add0=c.sub(0, 2 * hd), range_flag=None)
         _conv(L, q, Rows(ub.rh), B, h, w, hrows, src1=ub.x_dyn(pu), epilogue=_lib.EPI_GRU_Q, aux0=hrows,
-              aux1=Rows(ub.z), add0=c.sub(2 * hd, hd))
+              aux1=Rows(ub.z), add0=c.sub(2 * hd, hd), range_flag=None)
     coords = Rows(ub.coords)
     if pu.small:
-        _conv(L, pu.fh1, hrows, B, h, w, Rows(ub.fh), epilogue=_lib.EPI_RELU)
+        _conv(L, pu.fh1, hrows, B, h, w, Rows(ub.fh), epilogue=_lib.EPI_RELU, range_flag=None)  # feeds fp32 fh2
         _conv(L, pu.fh2, Rows(ub.fh), B, h, w, coords, epilogue=_lib.EPI_ADD_TO_OUT)
     else:
         fh = Rows(ub.fh)
         if with_mask:
             _conv(L, pu.fh1_mask, hrows, B, h, w, fh, epilogue=_lib.EPI_RELU)
-        else:
-            _conv(L, pu.fh1, hrows, B, h, w, fh.sub(0, 256), epilogue=_lib.EPI_RELU)
+        else:  # (feeds only the fp32 flow-head conv2: no range guard)
+            _conv(L, pu.fh1, hrows, B, h, w, fh.sub(0, 256), epilogue=_lib.EPI_RELU, range_flag=None)
         _conv(L, pu.fh2, fh.sub(0, 256), B, h, w, coords, epilogue=_lib.EPI_ADD_TO_OUT)
         if with_mask:
             # the mask feeds only the fp32 softmax of the upsampling: no range guard
@@ -413,7 +416,7 @@ class RaftPlan:
     """RAFT.forward (core/raft.py:145-251, eval mode) as a fixed launch list."""
 
     def __init__(self, pk: PackedRaft, B, H, W, iters, test_mode=True, alternate=False, flow_init=False,
-                 device=None):
+                 device=None, range_guard=True):
         if H % 8 or W % 8:
             raise ValueError(f"image size {H}x{W} must be a multiple of 8 (pad with InputPadder)")
         self.pk, self.B, self.H, self.W, self.iters = pk, B, H, W, iters
@@ -421,7 +424,7 @@ class RaftPlan:
         self.device = device
         # f16x3 range guard flag (raft_hip.h): raised by the convs and lookups whose outputs
         # feed split-precision convs; RAFT.forward checks it after the forward
-        self.guarded = pk.precision == _lib.PREC_F16X3
+        self.guarded = range_guard and pk.precision == _lib.PREC_F16X3
         self.range_flag = torch.zeros(1, dtype=torch.int32, device=device)
         _GUARD["flag"] = self.range_flag if self.guarded else None
         try:

@@ -146,14 +146,16 @@ class RAFT(nn.Module):
         # the stream layout knobs are read when a plan is built, so they are part of its key
         knobs = (os.environ.get("RAFT_CTX_SIDE", "1"), os.environ.get("RAFT_FLOW_SIDE", "1"),
                  os.environ.get("RAFT_CONV_PAIR", "1"))
+        guard = self.range_guard != "off"  # "off": no device-side checks either
         key = (batch, height, width, iters, bool(test_mode), bool(self.args.alternate_corr), bool(flow_init), prec,
-               knobs)
+               knobs, guard)
         pl = self._plans.get(key)
         if pl is None:
             while len(self._plans) >= max(1, self.max_plans):
                 self._plans.popitem(last=False)[1].release()
             pl = RaftPlan(pk, batch, height, width, iters, test_mode=test_mode,
-                          alternate=bool(self.args.alternate_corr), flow_init=flow_init, device=device)
+                          alternate=bool(self.args.alternate_corr), flow_init=flow_init, device=device,
+                          range_guard=guard)
             self._plans[key] = pl
         else:
             self._plans.move_to_end(key)

@@ -15,6 +15,7 @@ run() {
 }
 run --batch 8 --alternate-corr                                   # config 3
 run --batch 8 --height 540 --width 960                           # config 4 (per GPU)
-run --batch 1 --height 1080 --width 1920 --precision f16         # config 5 (mixed precision)
-run --batch 4 --height 1080 --width 1920 --precision f16         # config 5, 4 pairs per GPU
+run --batch 1 --height 1080 --width 1920 --precision bf16        # config 5 (bf16 mixed precision)
+run --batch 4 --height 1080 --width 1920 --precision bf16        # config 5, 4 pairs per GPU
+run --batch 1 --height 1080 --width 1920 --precision f16         # config 5 geometry, the reference's fp16 autocast
 run --batch 1 --height 1080 --width 1920                         # config 5 geometry, fp32-accurate convs
