@@ -35,12 +35,6 @@ struct AltArgs {
   int* range_flag;  // f16x3 range guard (raft_hip.h), or null
 };
 
-// Partial dot product of one tap: this lane's channel quads of fmap1[p] (registers)
-// and of the tap's fmap2 row, read through a raw buffer over the batch's fmap2.
-// An out-of-map (or beyond-C) read passes an out-of-range offset and returns
-// zeros without a memory access, so every tap's load is issued unconditionally
-// (no exec-masked branch per tap: the loads of a tap group go out back to back
-// instead of one L2 round trip per tap).
 // One tap's fmap2 row slice for this lane's channel quads, read through a raw
 // buffer over the batch's fmap2.  An out-of-map (or beyond-C) read passes an
 // out-of-range offset and returns zeros without a memory access, so every
