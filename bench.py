@@ -92,11 +92,17 @@ def time_kernel_events(fn, reps):
     return start.elapsed_time(end) / reps * 1e-3  # seconds
 
 
-def halo_bn(pc_n, batch, h, w):
-    """The N tile conv_halo_launch picks (csrc/conv_halo.hip): 64 unless 32 keeps more CUs busy."""
+def halo_bn(ns, batch, h, w):
+    """The N tile conv_halo_launch / conv_halo_launch_pair picks (csrc/conv_halo.hip) for a launch
+    of the convs with output channels `ns` (one, or a raft_conv2d_pair): 64 unless 32 keeps more
+    CUs busy."""
     spatial = batch * -(-h // 8) * -(-w // 16)
-    n_pad = -(-pc_n // 64) * 64
-    return 64 if spatial * (n_pad // 64) > 128 else 32
+    return 64 if sum(spatial * (-(-n // 64)) for n in ns) > 128 else 32
+
+
+def launch_convs(l):
+    """The raft_conv2d_params of a conv launch: one, or the two of a raft_conv2d_pair."""
+    return l.keep if isinstance(l.keep, tuple) else (l.keep,)
 
 
 def rotated_lookup(plan, batch, h8, w8, nrot, reps):
@@ -299,9 +305,10 @@ def main():
               ("raft_corr_lookup", "raft_alt_corr_lookup_nhwc")]
     per_it = len(lk_idx) // args.iters
     it_convs = [plan.launches[i] for i in range(lk_idx[per_it] + 1, lk_idx[2 * per_it])
-                if getattr(plan.launches[i], "name", "") == "raft_conv2d" and not plan.launches[i].side]
+                if getattr(plan.launches[i], "name", "") in ("raft_conv2d", "raft_conv2d_pair")
+                and not plan.launches[i].side]
     t_upd = time_kernel_events(lambda: [l(K.stream_handle()) for l in it_convs], 20)
-    fl = P * sum(2 * l.keep.n * l.keep.kh * l.keep.kw * (l.keep.in0_c + l.keep.in1_c) for l in it_convs)
+    fl = P * sum(2 * c.n * c.kh * c.kw * (c.in0_c + c.in1_c) for l in it_convs for c in launch_convs(l))
     peak = CONV_PEAK_TF[prec]
     update_roof = {"kernel": f"raft_conv2d (update block, one iteration, {prec}; main-stream convs)", "bound": "mfma",
                    "achieved": round(fl / t_upd / 1e12, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
@@ -309,15 +316,17 @@ def main():
                    "flops_per_iteration": fl,
                    "timing": "HIP events around a hipGraph of 20 replays of one iteration's conv launches"}
 
-    # the dominant kernel of the step: conv_halo_kernel<3,3,64> (the update block's 3x3 convs with
-    # N >= 192 at B=1: convc2 and the flow head's conv1), flops 2*M*N*K per launch
-    dom = [l for l in it_convs if l.keep.kh == 3 and l.keep.kw == 3 and l.keep.n > 4 and l.keep.precision != 0
-           and halo_bn(l.keep.n, args.batch, h8, w8) == 64]
+    # the dominant kernel of the step: conv_halo_kernel<3,3,64> (the update block's 3x3 launches with
+    # N-tile 64 at B=1: the convc2 | convf2 pair and the flow head's conv1), flops 2*M*N*K per conv
+    dom = [l for l in it_convs
+           if all(c.kh == 3 and c.kw == 3 and c.n > 4 and c.precision != 0 for c in launch_convs(l))
+           and halo_bn([c.n for c in launch_convs(l)], args.batch, h8, w8) == 64]
     dominant = None
     if dom:
-        dfl = sum(2 * P * l.keep.n * 9 * (l.keep.in0_c + l.keep.in1_c) for l in dom)
+        dfl = sum(2 * P * c.n * 9 * (c.in0_c + c.in1_c) for l in dom for c in launch_convs(l))
         dt = time_kernel_events(lambda: [l(K.stream_handle()) for l in dom], 50)
-        dominant = {"kernel": "conv_halo_kernel<3,3,64> (convc2 and the flow-head conv1 of one iteration)",
+        dominant = {"kernel": "conv_halo_kernel<3,3,64> (the convc2 | convf2 pair and the flow-head conv1 of one "
+                              "iteration)",
                     "bound": "mfma", "achieved": round(dfl / dt / 1e12, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
                     "frac": round(dfl / dt / 1e12 / peak, 4), "launches": len(dom),
                     "launch_us": round(dt / len(dom) * 1e6, 2), "flops_per_launch": dfl // len(dom),
