@@ -288,9 +288,15 @@ def main():
               if getattr(l, "name", None) == "raft_alt_corr_lookup_nhwc"]
         t_it = time_kernel_events(lambda: [l(K.stream_handle()) for l in lk[:nl]], 20)
         fl = alt_lookup_flops(P, nl, plan.pk.radius, plan.pk.fdim)
-        roof = {"kernel": f"alt_corr_tile_kernel<4> (raft_alt_corr_lookup_nhwc x{nl} per iteration)", "bound": "valu",
-                "achieved": round(fl / t_it / 1e12, 2), "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                "frac": round(fl / t_it / 1e12 / FP32_MFMA_PEAK_TF, 4), "traffic": None,
+        # RAFT (r = 4, C = 256) runs the MFMA tile kernel (csrc/alt_corr.hip, f16x3 box GEMM) unless
+        # RAFT_ALT_MFMA=0 selects the fp32 VALU tile kernel; the peak is that arithmetic's
+        mfma = os.environ.get("RAFT_ALT_MFMA", "1") != "0" and plan.pk.radius == 4 and plan.pk.fdim % 32 == 0 \
+            and plan.pk.fdim <= 256
+        kname, bound, pk_tf = (("alt_corr_mfma_kernel<4>", "mfma (f16x3 box GEMM)", CONV_PEAK_TF["f16x3"]) if mfma
+                               else ("alt_corr_tile_kernel<4>", "valu", FP32_MFMA_PEAK_TF))
+        roof = {"kernel": f"{kname} (raft_alt_corr_lookup_nhwc x{nl} per iteration)", "bound": bound,
+                "achieved": round(fl / t_it / 1e12, 2), "peak": round(pk_tf, 1), "unit": "TFLOP/s",
+                "frac": round(fl / t_it / 1e12 / pk_tf, 4), "traffic": None,
                 "algorithmic_flops_per_iteration": fl, "iteration_us": round(t_it * 1e6, 2),
                 "timing": "HIP events around a hipGraph replay of the last iteration's lookups (final coords)"}
 

@@ -5,6 +5,9 @@
 namespace raft {
 namespace {
 
+using h4 = __attribute__((ext_vector_type(4))) _Float16;
+using h8 = __attribute__((ext_vector_type(8))) _Float16;
+
 // ============================================================================
 // K3: on-the-fly correlation (alt_cuda_corr forward, correlation_kernel.cu:18-119)
 //
@@ -405,6 +408,235 @@ __global__ __launch_bounds__(256) void alt_corr_tile_kernel(AltArgs a) {
   }
 }
 
+// ============================================================================
+// K3m: the tile kernel's tap sums on MFMA (RAFT: C = 256, r = 4).
+//
+// The tap sums of an 8x8 query tile are dot products of its 64 fmap1 rows with
+// the fmap2 pixels of the tile's window box: a GEMM S = F1 * F2box^T (M = 64
+// queries, N = box pixels, K = C) of which each query keeps its (2r+2)^2 window
+// entries.  The VALU tile kernel reads LDS once per (query, tap, 8 channels);
+// here the box (up to 96 x 96 fmap2 pixels, where the VALU kernel stops at 28 x 28)
+// is consumed in bands of whole box rows (96 / box width of them, N padded to 96) on v_mfma_f32_32x32x16_f16 in the fp32-accurate split (hi*hi + lo*hi +
+// hi*lo, the corr_build arithmetic), and the band's 64 x 64 product goes through
+// LDS where every query picks the taps of its window that lie in the band.
+//   LDS: F1 tile, all K, split (64 x C/32 x 128 B = 64 KB) | band rows of F2
+//   (96 px x C/32 x 128 B, reused for the band's S) -> 160 KB, one work-group
+//   per CU; 8 waves load, waves 0-5 own one 32x32 S subtile each, all 8 pick taps.
+// The next band's fmap2 loads are issued before the current band's MFMAs.
+// ============================================================================
+constexpr int AM_KS = 8;                 // 32-channel K-steps (C <= 256)
+constexpr int AM_ROW = 128;              // bytes per (row, K-step): 32 hi | 32 lo halves, 16-B chunks
+                                         // XOR-swizzled by row & 7 (conflict-free fragment reads)
+constexpr int AM_NB = 96;                // band pixels (>= 3 box rows of ATB)
+constexpr int AM_SLD = AM_NB + 4;        // S row stride (floats)
+constexpr int AM_PER = AM_NB * AM_KS * 32 / 4 / 512;  // 16-B loads per thread per band (C = 256): 12
+
+// byte offset of logical 16-B chunk c of LDS row `row`
+__device__ __forceinline__ int am_chunk(int row, int c) { return ((c ^ (row & 7)) << 4); }
+
+// 4 floats (channels 4*quad .. +3 of a K-step) -> f16 hi in chunk quad/2, lo = f16(x - hi) in
+// chunk 4 + quad/2 (the corr_build split, unscaled lo)
+__device__ __forceinline__ void am_split_store(char* base, int row, int quad, f32x4 v) {
+  h4 hi, lo;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const _Float16 h = (_Float16)v[e];
+    hi[e] = h;
+    lo[e] = (_Float16)(v[e] - (float)h);
+  }
+  char* r = base + row * AM_ROW + (quad & 1) * 8;
+  *reinterpret_cast<h4*>(r + am_chunk(row, quad >> 1)) = hi;
+  *reinterpret_cast<h4*>(r + am_chunk(row, 4 + (quad >> 1))) = lo;
+}
+
+template <int R>
+__global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a) {
+  constexpr int WD = 2 * R + 2, NT = WD * WD, RD = 2 * R + 1;
+  constexpr int TPT = (NT + 7) / 8;  // taps per thread (8 waves)
+  constexpr int ABYTES = AT * AT * AM_KS * AM_ROW, BBYTES = AM_NB * AM_KS * AM_ROW;
+  static_assert(AM_NB * AM_SLD * 4 <= BBYTES && AT * AT * (NT + 1) * 4 <= ABYTES, "S and ts fit their regions");
+  __shared__ __attribute__((aligned(16))) char smem[ABYTES + BBYTES];
+  char* const As = smem;
+  char* const Bs = smem + ABYTES;
+  float* const S = reinterpret_cast<float*>(Bs);
+  const int lane = threadIdx.x & 63;
+  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave 0..7
+  const int P1 = a.H1 * a.W1;
+  const int tiles_x = (a.W1 + AT - 1) / AT, tiles_y = (a.H1 + AT - 1) / AT;
+  const int per = tiles_x * tiles_y;
+  const long bn = blockIdx.x / per;
+  const int tr = (int)(blockIdx.x - bn * per);
+  const int b = (int)(bn / a.N);
+  // every wave holds the tile's 64 queries, one per lane (the box is computed per wave)
+  const int qy = (tr / tiles_x) * AT + (lane >> 3), qx = (tr % tiles_x) * AT + (lane & 7);
+  const bool valid = qy < a.H1 && qx < a.W1;
+  const int p = valid ? qy * a.W1 + qx : 0;
+  const long gid = bn * P1 + p;
+  float x = 0.f, y = 0.f;
+  if (valid) {
+    if (a.coords_layout == 0) {
+      x = a.coords[2 * gid];
+      y = a.coords[2 * gid + 1];
+    } else {
+      x = a.coords[((long)b * 2) * P1 + p];
+      y = a.coords[((long)b * 2 + 1) * P1 + p];
+    }
+    x = x / a.coord_div;
+    y = y / a.coord_div;
+  }
+  const bool fin = isfinite(x) && isfinite(y) && fabsf(x) < 1e8f && fabsf(y) < 1e8f;
+  const int x0 = fin ? (int)floorf(x) - R : 0, y0 = fin ? (int)floorf(y) - R : 0;
+  int mnx = valid ? x0 : (1 << 30), mny = valid ? y0 : (1 << 30);
+  int mxx = valid ? x0 : -(1 << 30), mxy = valid ? y0 : -(1 << 30);
+  int bad = valid && !fin;
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    mnx = min(mnx, __shfl_xor(mnx, m));
+    mny = min(mny, __shfl_xor(mny, m));
+    mxx = max(mxx, __shfl_xor(mxx, m));
+    mxy = max(mxy, __shfl_xor(mxy, m));
+    bad |= __shfl_xor(bad, m);
+  }
+  const int bx0 = __builtin_amdgcn_readfirstlane(mnx), by0 = __builtin_amdgcn_readfirstlane(mny);
+  const int bw = __builtin_amdgcn_readfirstlane(mxx) - bx0 + WD, bh = __builtin_amdgcn_readfirstlane(mxy) - by0 + WD;
+  // any box up to AM_NB wide is consumed band by band (a tall box only costs more bands)
+  const bool fits = !__builtin_amdgcn_readfirstlane(bad) && bw <= AM_NB && bh <= AM_NB;
+  if (!fits) {
+    // wave g finishes pixels 8g .. 8g + 7 of the tile one at a time (per-pixel path)
+    float* ts = reinterpret_cast<float*>(smem) + g * 128;
+    for (int i = 0; i < 8; ++i) {
+      const int q = 8 * g + i;
+      const int pq = __shfl(p, q), vq = __shfl((int)valid, q);
+      alt_pixel<1>(a, bn * P1 + pq, vq != 0, lane, ts);
+    }
+    return;
+  }
+  const int ks = a.C / 32;  // K-steps (host-checked: C % 32 == 0, C <= 256)
+  const int tid = threadIdx.x;
+  const int br = AM_NB / bw;  // box rows per band: as many whole rows as fit 96 pixels (>= 1)
+  // ---- fmap2 band loads: thread = (band pixel, quad), AM_PER per thread; zeros off the map / band
+  const float* f2b = a.f2 + (long)b * a.H2 * a.W2 * a.C;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(f2b), (short)0, (int)((long)a.H2 * a.W2 * a.C * 4), 0x00020000);
+  f32x4 bv[AM_PER];
+  auto load_band = [&](int r0) {
+#pragma unroll
+    for (int k = 0; k < AM_PER; ++k) {
+      const int i = tid + 512 * k;  // (pixel j, quad) with 64 quads per pixel (C = 256 max)
+      const int j = i >> 6, qd = i & 63;
+      const int rr = j / bw, xx = j - rr * bw;
+      const int h2 = by0 + r0 + rr, w2 = bx0 + xx;
+      const bool in = rr < br && r0 + rr < bh && 4 * qd < a.C && (unsigned)h2 < (unsigned)a.H2 &&
+                      (unsigned)w2 < (unsigned)a.W2;
+      const unsigned off = in ? (unsigned)((h2 * a.W2 + w2) * a.C + 4 * qd) * 4u : 0x80000000u;
+      bv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    }
+  };
+  auto store_band = [&]() {
+#pragma unroll
+    for (int k = 0; k < AM_PER; ++k) {
+      const int i = tid + 512 * k;
+      const int j = i >> 6, qd = i & 63, s = qd >> 3;
+      if (s < ks) am_split_store(Bs, s * AM_NB + j, qd & 7, bv[k]);
+    }
+  };
+  load_band(0);  // in flight with the F1 loads
+  // ---- F1 tile -> LDS (split), all K: thread = (query, 16-B quad), 16 quads per 2 K-steps
+  {
+    // thread = (query q, 16-B quad qd of the row): 64 quads per query, all loads in flight together
+    constexpr int AQ = AT * AT * AM_KS * 8 / 512;
+    const float* f1b = a.f1 + (long)b * P1 * a.C;
+    f32x4 av[AQ];
+#pragma unroll
+    for (int k = 0; k < AQ; ++k) {
+      const int i = tid + 512 * k, q = i >> 6, qd = i & 63;
+      const int qyy = (tr / tiles_x) * AT + (q >> 3), qxx = (tr % tiles_x) * AT + (q & 7);
+      const bool v = qyy < a.H1 && qxx < a.W1 && 4 * qd < a.C;
+      av[k] = v ? *reinterpret_cast<const f32x4*>(f1b + ((long)qyy * a.W1 + qxx) * a.C + 4 * qd)
+                : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < AQ; ++k) {
+      const int i = tid + 512 * k, q = i >> 6, qd = i & 63, s = qd >> 3;
+      if (s < ks) am_split_store(As, s * (AT * AT) + q, qd & 7, av[k]);
+    }
+  }
+  // box-relative window origin of this lane's query; taps t = g + 8j
+  const int ox0 = valid ? x0 - bx0 : 0, oy0 = valid ? y0 - by0 : 0;
+  float tap[TPT];
+#pragma unroll
+  for (int j = 0; j < TPT; ++j) tap[j] = 0.f;
+  const int mi = g & 1, ni = g >> 1;  // S subtile of MFMA waves 0-5
+  const int m = lane & 31, h = lane >> 5;
+  for (int r0 = 0; r0 < bh; r0 += br) {
+    store_band();
+    __syncthreads();  // band r0 (and, first time round, the F1 tile) in LDS
+    if (r0 + br < bh) load_band(r0 + br);  // in flight under the MFMAs
+    f32x16 acc = {}, acc2 = {}, acc3 = {};
+    if (g < 6) {
+      for (int s = 0; s < ks; ++s) {
+        const int ar = s * (AT * AT) + 32 * mi + m, brow = s * AM_NB + 32 * ni + m;
+        const char* Ar = As + ar * AM_ROW;
+        const char* Br = Bs + brow * AM_ROW;
+#pragma unroll
+        for (int qq = 0; qq < 2; ++qq) {
+          const int c = 2 * qq + h;  // the lane's 8 halves of this K-half: logical chunk c (hi), 4 + c (lo)
+          const h8 xh = *reinterpret_cast<const h8*>(Ar + am_chunk(ar, c));
+          const h8 xl = *reinterpret_cast<const h8*>(Ar + am_chunk(ar, 4 + c));
+          const h8 yh = *reinterpret_cast<const h8*>(Br + am_chunk(brow, c));
+          const h8 yl = *reinterpret_cast<const h8*>(Br + am_chunk(brow, 4 + c));
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, yh, acc, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, yh, acc2, 0, 0, 0);
+          acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, yl, acc3, 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();  // every MFMA wave has read the band: its region takes S
+    if (g < 6) {
+      // register r holds S[query 32mi + (r&3) + 8(r>>2) + 4h][band pixel 32ni + m]
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        S[(32 * mi + (r & 3) + 8 * (r >> 2) + 4 * h) * AM_SLD + 32 * ni + m] = acc[r] + acc2[r] + acc3[r];
+    }
+    __syncthreads();
+    // every lane (query) picks the taps of its window in box rows r0 .. r0 + br - 1
+#pragma unroll
+    for (int j = 0; j < TPT; ++j) {
+      const int t = g + 8 * j;
+      if (t < NT) {
+        const int iy = t / WD, ix = t - (t / WD) * WD;
+        const int rr = oy0 + iy - r0;
+        if ((unsigned)rr < (unsigned)br) tap[j] = S[lane * AM_SLD + rr * bw + ox0 + ix];
+      }
+    }
+    __syncthreads();  // S read: the region takes the next band
+  }
+  // ---- tap sums -> LDS ts[q][t] (over the F1 region), then the tile kernel's binning
+  float* ts = reinterpret_cast<float*>(As);
+#pragma unroll
+  for (int j = 0; j < TPT; ++j) {
+    const int t = g + 8 * j;
+    if (t < NT) ts[lane * (NT + 1) + t] = tap[j];
+  }
+  __syncthreads();
+  if (a.out_layout == 1) {
+    for (int q = g; q < AT * AT; q += 8) {
+      const float xq = __shfl(x, q), yq = __shfl(y, q);
+      const int pq = __shfl(p, q), vq = __shfl((int)valid, q);
+      if (!vq) continue;
+      for (int o = lane; o < RD * RD; o += 64) alt_bin_store(a, bn, pq, xq, yq, ts + q * (NT + 1), o);
+    }
+    if (!valid) return;
+  } else {
+    if (!valid) return;
+    for (int o = g; o < RD * RD; o += 8) alt_bin_store(a, bn, p, x, y, ts + lane * (NT + 1), o);
+  }
+  if (a.flow && g == 0) {
+    a.flow[((long)b * P1 + p) * a.flow_ld + 0] = x * a.coord_div - (float)(p % a.W1);
+    a.flow[((long)b * P1 + p) * a.flow_ld + 1] = y * a.coord_div - (float)(p / a.W1);
+  }
+}
+
 // Any radius (the reference's CorrBlock / AlternateCorrBlock take any r; RAFT uses 3 and 4,
 // which the kernels above serve): one wave per query, the (2r+2)^2 tap sums in dynamic LDS
 // (one row of ALT_GEN_ROW floats per wave), then the bilinear binning.
@@ -481,6 +713,15 @@ int launch_alt(const AltArgs& a, raft_stream_t stream) {
     return check_launch("raft_alt_corr(generic radius)");
   }
 #ifndef ALT_NO_TILE  // dev builds: the per-pixel kernel at every size
+  static const bool mfma = [] {
+    const char* e = getenv("RAFT_ALT_MFMA");
+    return !(e && e[0] == '0');
+  }();
+  if (mfma && a.r == 4 && a.C % 32 == 0 && a.C <= 256) {
+    const long tiles = (long)a.B * a.N * cdiv_l(a.H1, AT) * cdiv_l(a.W1, AT);
+    hipLaunchKernelGGL(alt_corr_mfma_kernel<4>, dim3((unsigned)tiles), dim3(512), 0, s, a);
+    return check_launch("raft_alt_corr(mfma)");
+  }
   if (a.r == 4 && a.C % ACC == 0 && a.C <= 256) {
     const long tiles = (long)a.B * a.N * cdiv_l(a.H1, AT) * cdiv_l(a.W1, AT);
     hipLaunchKernelGGL(alt_corr_tile_kernel<4>, dim3((unsigned)tiles), dim3(256), 0, s, a);
