@@ -285,8 +285,8 @@ def main():
         # alternate corr: FP32 VALU-bound, 2*P*L*(2r+2)^2*C flops over the L per-level launches
         nl = plan.pk.levels
         lk = [l for l in plan.launches[plan.loop_start:plan.loop_end]
-              if getattr(l, "name", None) == "raft_alt_corr_lookup_nhwc"]
-        t_it = time_kernel_events(lambda: [l(K.stream_handle()) for l in lk[:nl]], 20)
+              if getattr(l, "name", None) == "raft_alt_corr_lookup_levels"]
+        t_it = time_kernel_events(lambda: lk[0](K.stream_handle()), 20)
         fl = alt_lookup_flops(P, nl, plan.pk.radius, plan.pk.fdim)
         # RAFT (r = 4, C = 256) runs the MFMA tile kernel (csrc/alt_corr.hip, f16x3 box GEMM) unless
         # RAFT_ALT_MFMA=0 selects the fp32 VALU tile kernel; the peak is that arithmetic's
@@ -294,7 +294,8 @@ def main():
             and plan.pk.fdim <= 256
         kname, bound, pk_tf = (("alt_corr_mfma_kernel<4>", "mfma (f16x3 box GEMM)", CONV_PEAK_TF["f16x3"]) if mfma
                                else ("alt_corr_tile_kernel<4>", "valu", FP32_MFMA_PEAK_TF))
-        roof = {"kernel": f"{kname} (raft_alt_corr_lookup_nhwc x{nl} per iteration)", "bound": bound,
+        roof = {"kernel": f"{kname} (raft_alt_corr_lookup_levels: {nl} levels, one launch per iteration)",
+                "bound": bound,
                 "achieved": round(fl / t_it / 1e12, 2), "peak": round(pk_tf, 1), "unit": "TFLOP/s",
                 "frac": round(fl / t_it / 1e12 / pk_tf, 4), "traffic": None,
                 "algorithmic_flops_per_iteration": fl, "iteration_us": round(t_it * 1e6, 2),
@@ -308,7 +309,7 @@ def main():
     # the update block's main-stream convolutions of one (non-final) iteration, replayed as a graph
     # (their operands are L2 / MALL-resident in the forward as well: 7 MB activations, <= 2 MB weights)
     lk_idx = [i for i, l in enumerate(plan.launches) if getattr(l, "name", "") in
-              ("raft_corr_lookup", "raft_alt_corr_lookup_nhwc")]
+              ("raft_corr_lookup", "raft_alt_corr_lookup_levels")]
     per_it = len(lk_idx) // args.iters
     it_convs = [plan.launches[i] for i in range(lk_idx[per_it] + 1, lk_idx[2 * per_it])
                 if getattr(plan.launches[i], "name", "") in ("raft_conv2d", "raft_conv2d_pair")

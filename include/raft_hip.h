@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define RAFT_HIP_ABI_VERSION 7
+#define RAFT_HIP_ABI_VERSION 8
 
 /* Negative return codes (argument errors, raised before any launch). */
 #define RAFT_E_INVALID (-1)   /* bad size / null pointer / unsupported shape */
@@ -115,6 +115,17 @@ int raft_alt_corr_lookup_nhwc(const float* fmap1, const float* fmap2, const floa
                               float coord_div, float* out, int out_ld, int B, int H1, int W1, int H2, int W2,
                               int C, int radius, float scale_div, float* flow_out, int flow_ld,
                               int* range_flag, raft_stream_t stream);
+/* All L levels of AlternateCorrBlock.__call__ (core/corr.py:163-198, the L calls of
+ * alt_cuda_corr.forward of :176-186) as one call: level l reads fmap2_levels[l] (NHWC,
+ * h2s[l] x w2s[l]) with the coordinates divided by 2^l and writes output channels
+ * l*(2r+1)^2 .. of each NHWC row; flow_out as raft_alt_corr_lookup_nhwc (written once).  RAFT's
+ * case (r = 4, C % 32 == 0, C <= 256) is ONE launch whose work-groups stage their fmap1 tile
+ * once for every level; otherwise L launches of raft_alt_corr_lookup_nhwc.  Results equal the
+ * L separate calls.  The pointer / size arrays are read on the host during the call. */
+int raft_alt_corr_lookup_levels(const float* fmap1, const float* const* fmap2_levels, const int* h2s,
+                                const int* w2s, int L, const float* coords, int coords_layout, float* out,
+                                int out_ld, int B, int H1, int W1, int C, int radius, float scale_div,
+                                float* flow_out, int flow_ld, int* range_flag, raft_stream_t stream);
 
 /* Gradients of raft_alt_corr_forward (unscaled), replacing correlation_kernel.cu:122-256:
  * every output is written (no pre-zeroing) and bit-identical run to run.  fmap1_grad is

@@ -115,8 +115,8 @@ class AlternateCorrBlock:
         out = torch.empty(b * h * w, self.num_levels * nb, device=coords.device)
         s = K.stream_handle()
         div = K.sqrt_c(self.dim)
-        for i in range(self.num_levels):
-            f2, hh, ww = self._f2[i]
-            _lib.call("raft_alt_corr_lookup_nhwc", f1.data_ptr(), f2.data_ptr(), coords.data_ptr(), 1, float(2 ** i),
-                      out.data_ptr() + 4 * i * nb, out.shape[1], b, h, w, hh, ww, self.dim, r, div, None, 0, None, s)
+        levels = list(self._f2[: self.num_levels])
+        ptrs, hs, ws = K.alt_levels_args(levels)
+        _lib.call("raft_alt_corr_lookup_levels", f1.data_ptr(), ptrs, hs, ws, len(levels), coords.data_ptr(), 1,
+                  out.data_ptr(), out.shape[1], b, h, w, self.dim, r, div, None, 0, None, s)
         return K.rows_to_nchw(K.Rows(out), b, h, w)

@@ -449,110 +449,62 @@ __device__ __forceinline__ void am_split_store(char* base, int row, int quad, f3
   *reinterpret_cast<h4*>(r + am_chunk(row, 4 + (quad >> 1))) = lo;
 }
 
+// the per-level operands of one launch over all levels (raft_alt_corr_lookup_levels)
+constexpr int AM_MAXL = 6;
+struct AltLevels {
+  const float* f2[AM_MAXL];
+  float* out[AM_MAXL];
+  int H2[AM_MAXL], W2[AM_MAXL];
+  float div[AM_MAXL];
+  int n;
+};
+
 template <int R>
-__global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a) {
+__global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevels lvs) {
   constexpr int WD = 2 * R + 2, NT = WD * WD, RD = 2 * R + 1;
   constexpr int TPT = (NT + 7) / 8;  // taps per thread (8 waves)
   constexpr int ABYTES = AT * AT * AM_KS * AM_ROW, BBYTES = AM_NB * AM_KS * AM_ROW;
-  static_assert(AM_NB * AM_SLD * 4 <= BBYTES && AT * AT * (NT + 1) * 4 <= ABYTES, "S and ts fit their regions");
+  static_assert(AM_NB * AM_SLD * 4 <= BBYTES && AT * AT * (NT + 1) * 4 <= BBYTES, "S and ts fit the band region");
   __shared__ __attribute__((aligned(16))) char smem[ABYTES + BBYTES];
-  char* const As = smem;
-  char* const Bs = smem + ABYTES;
+  char* const As = smem;                // the F1 tile: resident over all levels
+  char* const Bs = smem + ABYTES;       // band rows, then the band's S, then the tap sums
   float* const S = reinterpret_cast<float*>(Bs);
   const int lane = threadIdx.x & 63;
   const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave 0..7
-  const int P1 = a.H1 * a.W1;
-  const int tiles_x = (a.W1 + AT - 1) / AT, tiles_y = (a.H1 + AT - 1) / AT;
+  const int tid = threadIdx.x;
+  const int P1 = a0.H1 * a0.W1;
+  const int tiles_x = (a0.W1 + AT - 1) / AT, tiles_y = (a0.H1 + AT - 1) / AT;
   const int per = tiles_x * tiles_y;
   const long bn = blockIdx.x / per;
   const int tr = (int)(blockIdx.x - bn * per);
-  const int b = (int)(bn / a.N);
+  const int b = (int)(bn / a0.N);
   // every wave holds the tile's 64 queries, one per lane (the box is computed per wave)
   const int qy = (tr / tiles_x) * AT + (lane >> 3), qx = (tr % tiles_x) * AT + (lane & 7);
-  const bool valid = qy < a.H1 && qx < a.W1;
-  const int p = valid ? qy * a.W1 + qx : 0;
+  const bool valid = qy < a0.H1 && qx < a0.W1;
+  const int p = valid ? qy * a0.W1 + qx : 0;
   const long gid = bn * P1 + p;
-  float x = 0.f, y = 0.f;
+  float xr = 0.f, yr = 0.f;  // level-0 coordinates
   if (valid) {
-    if (a.coords_layout == 0) {
-      x = a.coords[2 * gid];
-      y = a.coords[2 * gid + 1];
+    if (a0.coords_layout == 0) {
+      xr = a0.coords[2 * gid];
+      yr = a0.coords[2 * gid + 1];
     } else {
-      x = a.coords[((long)b * 2) * P1 + p];
-      y = a.coords[((long)b * 2 + 1) * P1 + p];
+      xr = a0.coords[((long)b * 2) * P1 + p];
+      yr = a0.coords[((long)b * 2 + 1) * P1 + p];
     }
-    x = x / a.coord_div;
-    y = y / a.coord_div;
   }
-  const bool fin = isfinite(x) && isfinite(y) && fabsf(x) < 1e8f && fabsf(y) < 1e8f;
-  const int x0 = fin ? (int)floorf(x) - R : 0, y0 = fin ? (int)floorf(y) - R : 0;
-  int mnx = valid ? x0 : (1 << 30), mny = valid ? y0 : (1 << 30);
-  int mxx = valid ? x0 : -(1 << 30), mxy = valid ? y0 : -(1 << 30);
-  int bad = valid && !fin;
-#pragma unroll
-  for (int m = 1; m < 64; m <<= 1) {
-    mnx = min(mnx, __shfl_xor(mnx, m));
-    mny = min(mny, __shfl_xor(mny, m));
-    mxx = max(mxx, __shfl_xor(mxx, m));
-    mxy = max(mxy, __shfl_xor(mxy, m));
-    bad |= __shfl_xor(bad, m);
-  }
-  const int bx0 = __builtin_amdgcn_readfirstlane(mnx), by0 = __builtin_amdgcn_readfirstlane(mny);
-  const int bw = __builtin_amdgcn_readfirstlane(mxx) - bx0 + WD, bh = __builtin_amdgcn_readfirstlane(mxy) - by0 + WD;
-  // any box up to AM_NB wide is consumed band by band (a tall box only costs more bands)
-  const bool fits = !__builtin_amdgcn_readfirstlane(bad) && bw <= AM_NB && bh <= AM_NB;
-  if (!fits) {
-    // wave g finishes pixels 8g .. 8g + 7 of the tile one at a time (per-pixel path)
-    float* ts = reinterpret_cast<float*>(smem) + g * 128;
-    for (int i = 0; i < 8; ++i) {
-      const int q = 8 * g + i;
-      const int pq = __shfl(p, q), vq = __shfl((int)valid, q);
-      alt_pixel<1>(a, bn * P1 + pq, vq != 0, lane, ts);
-    }
-    return;
-  }
-  const int ks = a.C / 32;  // K-steps (host-checked: C % 32 == 0, C <= 256)
-  const int tid = threadIdx.x;
-  const int br = AM_NB / bw;  // box rows per band: as many whole rows as fit 96 pixels (>= 1)
-  // ---- fmap2 band loads: thread = (band pixel, quad), AM_PER per thread; zeros off the map / band
-  const float* f2b = a.f2 + (long)b * a.H2 * a.W2 * a.C;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(f2b), (short)0, (int)((long)a.H2 * a.W2 * a.C * 4), 0x00020000);
-  f32x4 bv[AM_PER];
-  auto load_band = [&](int r0) {
-#pragma unroll
-    for (int k = 0; k < AM_PER; ++k) {
-      const int i = tid + 512 * k;  // (pixel j, quad) with 64 quads per pixel (C = 256 max)
-      const int j = i >> 6, qd = i & 63;
-      const int rr = j / bw, xx = j - rr * bw;
-      const int h2 = by0 + r0 + rr, w2 = bx0 + xx;
-      const bool in = rr < br && r0 + rr < bh && 4 * qd < a.C && (unsigned)h2 < (unsigned)a.H2 &&
-                      (unsigned)w2 < (unsigned)a.W2;
-      const unsigned off = in ? (unsigned)((h2 * a.W2 + w2) * a.C + 4 * qd) * 4u : 0x80000000u;
-      bv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-    }
-  };
-  auto store_band = [&]() {
-#pragma unroll
-    for (int k = 0; k < AM_PER; ++k) {
-      const int i = tid + 512 * k;
-      const int j = i >> 6, qd = i & 63, s = qd >> 3;
-      if (s < ks) am_split_store(Bs, s * AM_NB + j, qd & 7, bv[k]);
-    }
-  };
-  load_band(0);  // in flight with the F1 loads
-  // ---- F1 tile -> LDS (split), all K: thread = (query, 16-B quad), 16 quads per 2 K-steps
+  const int ks = a0.C / 32;  // K-steps (host-checked: C % 32 == 0, C <= 256)
+  // ---- F1 tile -> LDS (split), all K, once for every level: thread = (query q, 16-B quad qd)
   {
-    // thread = (query q, 16-B quad qd of the row): 64 quads per query, all loads in flight together
     constexpr int AQ = AT * AT * AM_KS * 8 / 512;
-    const float* f1b = a.f1 + (long)b * P1 * a.C;
+    const float* f1b = a0.f1 + (long)b * P1 * a0.C;
     f32x4 av[AQ];
 #pragma unroll
     for (int k = 0; k < AQ; ++k) {
       const int i = tid + 512 * k, q = i >> 6, qd = i & 63;
       const int qyy = (tr / tiles_x) * AT + (q >> 3), qxx = (tr % tiles_x) * AT + (q & 7);
-      const bool v = qyy < a.H1 && qxx < a.W1 && 4 * qd < a.C;
-      av[k] = v ? *reinterpret_cast<const f32x4*>(f1b + ((long)qyy * a.W1 + qxx) * a.C + 4 * qd)
+      const bool v = qyy < a0.H1 && qxx < a0.W1 && 4 * qd < a0.C;
+      av[k] = v ? *reinterpret_cast<const f32x4*>(f1b + ((long)qyy * a0.W1 + qxx) * a0.C + 4 * qd)
                 : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
@@ -561,79 +513,145 @@ __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a) {
       if (s < ks) am_split_store(As, s * (AT * AT) + q, qd & 7, av[k]);
     }
   }
-  // box-relative window origin of this lane's query; taps t = g + 8j
-  const int ox0 = valid ? x0 - bx0 : 0, oy0 = valid ? y0 - by0 : 0;
-  float tap[TPT];
-#pragma unroll
-  for (int j = 0; j < TPT; ++j) tap[j] = 0.f;
   const int mi = g & 1, ni = g >> 1;  // S subtile of MFMA waves 0-5
   const int m = lane & 31, h = lane >> 5;
-  for (int r0 = 0; r0 < bh; r0 += br) {
-    store_band();
-    __syncthreads();  // band r0 (and, first time round, the F1 tile) in LDS
-    if (r0 + br < bh) load_band(r0 + br);  // in flight under the MFMAs
-    f32x16 acc = {}, acc2 = {}, acc3 = {};
-    if (g < 6) {
-      for (int s = 0; s < ks; ++s) {
-        const int ar = s * (AT * AT) + 32 * mi + m, brow = s * AM_NB + 32 * ni + m;
-        const char* Ar = As + ar * AM_ROW;
-        const char* Br = Bs + brow * AM_ROW;
+  for (int l = 0; l < lvs.n; ++l) {
+    AltArgs a = a0;
+    a.f2 = lvs.f2[l];
+    a.H2 = lvs.H2[l];
+    a.W2 = lvs.W2[l];
+    a.coord_div = lvs.div[l];
+    a.out = lvs.out[l];
+    a.flow = l == 0 ? a0.flow : nullptr;
+    const float x = valid ? xr / a.coord_div : 0.f, y = valid ? yr / a.coord_div : 0.f;
+    const bool fin = isfinite(x) && isfinite(y) && fabsf(x) < 1e8f && fabsf(y) < 1e8f;
+    const int x0 = fin ? (int)floorf(x) - R : 0, y0 = fin ? (int)floorf(y) - R : 0;
+    int mnx = valid ? x0 : (1 << 30), mny = valid ? y0 : (1 << 30);
+    int mxx = valid ? x0 : -(1 << 30), mxy = valid ? y0 : -(1 << 30);
+    int bad = valid && !fin;
 #pragma unroll
-        for (int qq = 0; qq < 2; ++qq) {
-          const int c = 2 * qq + h;  // the lane's 8 halves of this K-half: logical chunk c (hi), 4 + c (lo)
-          const h8 xh = *reinterpret_cast<const h8*>(Ar + am_chunk(ar, c));
-          const h8 xl = *reinterpret_cast<const h8*>(Ar + am_chunk(ar, 4 + c));
-          const h8 yh = *reinterpret_cast<const h8*>(Br + am_chunk(brow, c));
-          const h8 yl = *reinterpret_cast<const h8*>(Br + am_chunk(brow, 4 + c));
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, yh, acc, 0, 0, 0);
-          acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, yh, acc2, 0, 0, 0);
-          acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, yl, acc3, 0, 0, 0);
+    for (int k = 1; k < 64; k <<= 1) {
+      mnx = min(mnx, __shfl_xor(mnx, k));
+      mny = min(mny, __shfl_xor(mny, k));
+      mxx = max(mxx, __shfl_xor(mxx, k));
+      mxy = max(mxy, __shfl_xor(mxy, k));
+      bad |= __shfl_xor(bad, k);
+    }
+    const int bx0 = __builtin_amdgcn_readfirstlane(mnx), by0 = __builtin_amdgcn_readfirstlane(mny);
+    const int bw = __builtin_amdgcn_readfirstlane(mxx) - bx0 + WD;
+    const int bh = __builtin_amdgcn_readfirstlane(mxy) - by0 + WD;
+    // any box up to AM_NB wide is consumed band by band (a tall box only costs more bands)
+    const bool fits = !__builtin_amdgcn_readfirstlane(bad) && bw <= AM_NB && bh <= AM_NB;
+    if (!fits) {
+      // wave g finishes pixels 8g .. 8g + 7 of the tile one at a time (per-pixel path)
+      float* ts = reinterpret_cast<float*>(Bs) + g * 128;
+      for (int i = 0; i < 8; ++i) {
+        const int q = 8 * g + i;
+        const int pq = __shfl(p, q), vq = __shfl((int)valid, q);
+        alt_pixel<1>(a, bn * P1 + pq, vq != 0, lane, ts);
+      }
+      __syncthreads();  // the band region is free for the next level
+      continue;
+    }
+    const int br = AM_NB / bw;  // box rows per band: as many whole rows as fit 96 pixels (>= 1)
+    // ---- fmap2 band loads: thread = (band pixel, quad), AM_PER per thread; zeros off the map / band
+    const float* f2b = a.f2 + (long)b * a.H2 * a.W2 * a.C;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(f2b), (short)0, (int)((long)a.H2 * a.W2 * a.C * 4), 0x00020000);
+    f32x4 bv[AM_PER];
+    auto load_band = [&](int r0) {
+#pragma unroll
+      for (int k = 0; k < AM_PER; ++k) {
+        const int i = tid + 512 * k;  // (pixel j, quad) with 64 quads per pixel (C = 256 max)
+        const int j = i >> 6, qd = i & 63;
+        const int rr = j / bw, xx = j - rr * bw;
+        const int h2 = by0 + r0 + rr, w2 = bx0 + xx;
+        const bool in = rr < br && r0 + rr < bh && 4 * qd < a.C && (unsigned)h2 < (unsigned)a.H2 &&
+                        (unsigned)w2 < (unsigned)a.W2;
+        const unsigned off = in ? (unsigned)((h2 * a.W2 + w2) * a.C + 4 * qd) * 4u : 0x80000000u;
+        bv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      }
+    };
+    auto store_band = [&]() {
+#pragma unroll
+      for (int k = 0; k < AM_PER; ++k) {
+        const int i = tid + 512 * k;
+        const int j = i >> 6, qd = i & 63, s = qd >> 3;
+        if (s < ks) am_split_store(Bs, s * AM_NB + j, qd & 7, bv[k]);
+      }
+    };
+    // box-relative window origin of this lane's query; taps t = g + 8j
+    const int ox0 = valid ? x0 - bx0 : 0, oy0 = valid ? y0 - by0 : 0;
+    float tap[TPT];
+#pragma unroll
+    for (int j = 0; j < TPT; ++j) tap[j] = 0.f;
+    load_band(0);
+    for (int r0 = 0; r0 < bh; r0 += br) {
+      store_band();
+      __syncthreads();  // band r0 (and, first time round, the F1 tile) in LDS
+      if (r0 + br < bh) load_band(r0 + br);  // in flight under the MFMAs
+      f32x16 acc = {}, acc2 = {}, acc3 = {};
+      if (g < 6) {
+        for (int s = 0; s < ks; ++s) {
+          const int ar = s * (AT * AT) + 32 * mi + m, brow = s * AM_NB + 32 * ni + m;
+          const char* Ar = As + ar * AM_ROW;
+          const char* Br = Bs + brow * AM_ROW;
+#pragma unroll
+          for (int qq = 0; qq < 2; ++qq) {
+            const int c = 2 * qq + h;  // the lane's 8 halves of this K-half: logical chunk c (hi), 4 + c (lo)
+            const h8 xh = *reinterpret_cast<const h8*>(Ar + am_chunk(ar, c));
+            const h8 xl = *reinterpret_cast<const h8*>(Ar + am_chunk(ar, 4 + c));
+            const h8 yh = *reinterpret_cast<const h8*>(Br + am_chunk(brow, c));
+            const h8 yl = *reinterpret_cast<const h8*>(Br + am_chunk(brow, 4 + c));
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, yh, acc, 0, 0, 0);
+            acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, yh, acc2, 0, 0, 0);
+            acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, yl, acc3, 0, 0, 0);
+          }
         }
       }
-    }
-    __syncthreads();  // every MFMA wave has read the band: its region takes S
-    if (g < 6) {
-      // register r holds S[query 32mi + (r&3) + 8(r>>2) + 4h][band pixel 32ni + m]
+      __syncthreads();  // every MFMA wave has read the band: its region takes S
+      if (g < 6) {
+        // register r holds S[query 32mi + (r&3) + 8(r>>2) + 4h][band pixel 32ni + m]
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        S[(32 * mi + (r & 3) + 8 * (r >> 2) + 4 * h) * AM_SLD + 32 * ni + m] = acc[r] + acc2[r] + acc3[r];
+        for (int r = 0; r < 16; ++r)
+          S[(32 * mi + (r & 3) + 8 * (r >> 2) + 4 * h) * AM_SLD + 32 * ni + m] = acc[r] + acc2[r] + acc3[r];
+      }
+      __syncthreads();
+      // every lane (query) picks the taps of its window in box rows r0 .. r0 + br - 1
+#pragma unroll
+      for (int j = 0; j < TPT; ++j) {
+        const int t = g + 8 * j;
+        if (t < NT) {
+          const int iy = t / WD, ix = t - (t / WD) * WD;
+          const int rr = oy0 + iy - r0;
+          if ((unsigned)rr < (unsigned)br) tap[j] = S[lane * AM_SLD + rr * bw + ox0 + ix];
+        }
+      }
+      __syncthreads();  // S read: the region takes the next band (or the tap sums)
     }
-    __syncthreads();
-    // every lane (query) picks the taps of its window in box rows r0 .. r0 + br - 1
+    // ---- tap sums -> LDS ts[q][t] (over the band region), then the tile kernel's binning
+    float* ts = reinterpret_cast<float*>(Bs);
 #pragma unroll
     for (int j = 0; j < TPT; ++j) {
       const int t = g + 8 * j;
-      if (t < NT) {
-        const int iy = t / WD, ix = t - (t / WD) * WD;
-        const int rr = oy0 + iy - r0;
-        if ((unsigned)rr < (unsigned)br) tap[j] = S[lane * AM_SLD + rr * bw + ox0 + ix];
+      if (t < NT) ts[lane * (NT + 1) + t] = tap[j];
+    }
+    __syncthreads();
+    if (a.out_layout == 1) {
+      for (int q = g; q < AT * AT; q += 8) {
+        const float xq = __shfl(x, q), yq = __shfl(y, q);
+        const int pq = __shfl(p, q), vq = __shfl((int)valid, q);
+        if (!vq) continue;
+        for (int o = lane; o < RD * RD; o += 64) alt_bin_store(a, bn, pq, xq, yq, ts + q * (NT + 1), o);
       }
+    } else if (valid) {
+      for (int o = g; o < RD * RD; o += 8) alt_bin_store(a, bn, p, x, y, ts + lane * (NT + 1), o);
     }
-    __syncthreads();  // S read: the region takes the next band
-  }
-  // ---- tap sums -> LDS ts[q][t] (over the F1 region), then the tile kernel's binning
-  float* ts = reinterpret_cast<float*>(As);
-#pragma unroll
-  for (int j = 0; j < TPT; ++j) {
-    const int t = g + 8 * j;
-    if (t < NT) ts[lane * (NT + 1) + t] = tap[j];
-  }
-  __syncthreads();
-  if (a.out_layout == 1) {
-    for (int q = g; q < AT * AT; q += 8) {
-      const float xq = __shfl(x, q), yq = __shfl(y, q);
-      const int pq = __shfl(p, q), vq = __shfl((int)valid, q);
-      if (!vq) continue;
-      for (int o = lane; o < RD * RD; o += 64) alt_bin_store(a, bn, pq, xq, yq, ts + q * (NT + 1), o);
+    if (valid && a.flow && g == 0) {
+      a.flow[((long)b * P1 + p) * a.flow_ld + 0] = x * a.coord_div - (float)(p % a.W1);
+      a.flow[((long)b * P1 + p) * a.flow_ld + 1] = y * a.coord_div - (float)(p / a.W1);
     }
-    if (!valid) return;
-  } else {
-    if (!valid) return;
-    for (int o = g; o < RD * RD; o += 8) alt_bin_store(a, bn, p, x, y, ts + lane * (NT + 1), o);
-  }
-  if (a.flow && g == 0) {
-    a.flow[((long)b * P1 + p) * a.flow_ld + 0] = x * a.coord_div - (float)(p % a.W1);
-    a.flow[((long)b * P1 + p) * a.flow_ld + 1] = y * a.coord_div - (float)(p / a.W1);
+    __syncthreads();  // the tap sums are read: the band region takes the next level
   }
 }
 
@@ -719,7 +737,14 @@ int launch_alt(const AltArgs& a, raft_stream_t stream) {
   }();
   if (mfma && a.r == 4 && a.C % 32 == 0 && a.C <= 256) {
     const long tiles = (long)a.B * a.N * cdiv_l(a.H1, AT) * cdiv_l(a.W1, AT);
-    hipLaunchKernelGGL(alt_corr_mfma_kernel<4>, dim3((unsigned)tiles), dim3(512), 0, s, a);
+    AltLevels lv{};
+    lv.f2[0] = a.f2;
+    lv.out[0] = a.out;
+    lv.H2[0] = a.H2;
+    lv.W2[0] = a.W2;
+    lv.div[0] = a.coord_div;
+    lv.n = 1;
+    hipLaunchKernelGGL(alt_corr_mfma_kernel<4>, dim3((unsigned)tiles), dim3(512), 0, s, a, lv);
     return check_launch("raft_alt_corr(mfma)");
   }
   if (a.r == 4 && a.C % ACC == 0 && a.C <= 256) {
@@ -836,6 +861,68 @@ extern "C" int raft_alt_corr_lookup_nhwc(const float* fmap1, const float* fmap2,
   a.flow_ld = flow_ld;
   a.range_flag = range_flag;
   return launch_alt(a, stream);
+}
+
+extern "C" int raft_alt_corr_lookup_levels(const float* fmap1, const float* const* fmap2_levels, const int* h2s,
+                                           const int* w2s, int L, const float* coords, int coords_layout, float* out,
+                                           int out_ld, int B, int H1, int W1, int C, int radius, float scale_div,
+                                           float* flow_out, int flow_ld, int* range_flag, raft_stream_t stream) {
+  RAFT_REQUIRE(fmap2_levels && h2s && w2s && L >= 1 && L <= AM_MAXL,
+               "raft_alt_corr_lookup_levels: need 1..%d levels", AM_MAXL);
+  const int rd2 = (2 * radius + 1) * (2 * radius + 1);
+  RAFT_REQUIRE(out_ld >= L * rd2, "raft_alt_corr_lookup_levels: out_ld too small for %d levels", L);
+  for (int l = 0; l < L; ++l) {
+    int rc = alt_checks(fmap1, fmap2_levels[l], coords, out, B, H1, W1, h2s[l], w2s[l], C, 1, radius);
+    if (rc) return rc;
+  }
+  RAFT_REQUIRE(coords_layout == 0 || coords_layout == 1, "raft_alt_corr_lookup_levels: bad coords_layout");
+  static const bool mfma = [] {
+    const char* e = getenv("RAFT_ALT_MFMA");
+    return !(e && e[0] == '0');
+  }();
+  if (!(mfma && radius == 4 && C % 32 == 0 && C <= 256)) {
+    // one launch per level (raft_alt_corr_lookup_nhwc; the flow is written with level 0)
+    for (int l = 0; l < L; ++l) {
+      int rc = raft_alt_corr_lookup_nhwc(fmap1, fmap2_levels[l], coords, coords_layout, (float)(1 << l),
+                                         out + (long)l * rd2, out_ld, B, H1, W1, h2s[l], w2s[l], C, radius, scale_div,
+                                         l == 0 ? flow_out : nullptr, flow_ld, range_flag, stream);
+      if (rc) return rc;
+    }
+    return 0;
+  }
+  AltArgs a;
+  a.f1 = fmap1;
+  a.f2 = fmap2_levels[0];
+  a.coords = coords;
+  a.coords_layout = coords_layout;
+  a.coord_div = 1.f;
+  a.out = out;
+  a.out_layout = 1;
+  a.out_ld = out_ld;
+  a.B = B;
+  a.H1 = H1;
+  a.W1 = W1;
+  a.H2 = h2s[0];
+  a.W2 = w2s[0];
+  a.C = C;
+  a.N = 1;
+  a.r = radius;
+  a.scale_div = scale_div;
+  a.flow = flow_out;
+  a.flow_ld = flow_ld;
+  a.range_flag = range_flag;
+  AltLevels lv{};
+  for (int l = 0; l < L; ++l) {
+    lv.f2[l] = fmap2_levels[l];
+    lv.out[l] = out + (long)l * rd2;
+    lv.H2[l] = h2s[l];
+    lv.W2[l] = w2s[l];
+    lv.div[l] = (float)(1 << l);
+  }
+  lv.n = L;
+  const long tiles = (long)B * cdiv_l(H1, AT) * cdiv_l(W1, AT);
+  hipLaunchKernelGGL(alt_corr_mfma_kernel<4>, dim3((unsigned)tiles), dim3(512), 0, as_stream(stream), a, lv);
+  return check_launch("raft_alt_corr_lookup_levels");
 }
 
 extern "C" int raft_avgpool2_nhwc(const float* in, float* out, int B, int H, int W, int C, raft_stream_t stream) {

@@ -511,11 +511,11 @@ class RaftPlan:
                 L.append(Launch("raft_corr_lookup", self.pyramid.data_ptr(), B, h, w, lv, r, ub.coords.data_ptr(), 0,
                                 ub.corr.data_ptr(), corr_ld, 0, ub.hx.data_ptr() + 4 * flow_slot, pu.ld, gflag))
             else:
-                for i, (f2, hh, ww) in enumerate(self.f2levels):
-                    fl = ub.hx.data_ptr() + 4 * flow_slot if i == 0 else None
-                    L.append(Launch("raft_alt_corr_lookup_nhwc", fmap1.data_ptr(), f2.data_ptr(), ub.coords.data_ptr(),
-                                    0, float(2 ** i), ub.corr.data_ptr() + 4 * i * (2 * r + 1) ** 2, corr_ld,
-                                    B, h, w, hh, ww, C, r, div, fl, pu.ld, gflag))
+                # every level in one call (one launch for RAFT's r = 4, C = 256: raft_hip.h)
+                arrs = K.alt_levels_args(self.f2levels)
+                L.append(Launch("raft_alt_corr_lookup_levels", fmap1.data_ptr(), *arrs, len(self.f2levels),
+                                ub.coords.data_ptr(), 0, ub.corr.data_ptr(), corr_ld, B, h, w, C, r, div,
+                                ub.hx.data_ptr() + 4 * flow_slot, pu.ld, gflag, keep=arrs))
             want_up = last or not test_mode
             plan_update(L, pu, ub, B, h, w, with_mask=want_up and not pu.small)
             if want_up:

@@ -252,6 +252,16 @@ def conv_pair_launch(p0: ConvParams, p1: ConvParams) -> Launch:
     return Launch("raft_conv2d_pair", ctypes.byref(p0), ctypes.byref(p1), keep=(p0, p1))
 
 
+def alt_levels_args(f2_levels):
+    """ctypes arrays (fmap2 pointers, heights, widths) of raft_alt_corr_lookup_levels for
+    [(fmap2 rows tensor, h, w), ...]; keep them alive with the launch."""
+    n = len(f2_levels)
+    ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t, _, _ in f2_levels])
+    hs = (ctypes.c_int * n)(*[hh for _, hh, _ in f2_levels])
+    ws = (ctypes.c_int * n)(*[ww for _, _, ww in f2_levels])
+    return ptrs, hs, ws
+
+
 FORK = "fork"   # side stream waits for the main stream
 JOIN = "join"   # main stream waits for the side stream
 

@@ -219,6 +219,43 @@ def test_alt_corr_tiled_vs_oracle(layout):
         assert maxabs(got, ref[:, 0] / 8.0) < 2e-5
 
 
+@pytest.mark.parametrize("r,spread", [(4, 0.7), (4, 6.0), (3, 0.7)])
+def test_alt_corr_levels_equals_per_level_calls(r, spread):
+    """raft_alt_corr_lookup_levels (one launch at r = 4) == the L raft_alt_corr_lookup_nhwc calls, bit for bit,
+    with small and large window boxes (spread 6 px: boxes beyond the VALU kernel's 28 x 28)."""
+    from raft_optical_flow_amd import kernels as K
+    from raft_optical_flow_amd import _lib
+    g = torch.Generator().manual_seed(21)
+    B, h, w, C, L = 2, 24, 40, 256, 4
+    f1 = torch.randn(B * h * w, C, generator=g).to(DEV)
+    lv = [(torch.randn(B * (h >> l) * (w >> l), C, generator=g).to(DEV), h >> l, w >> l) for l in range(L)]
+    ys, xs = torch.meshgrid(torch.arange(h), torch.arange(w), indexing="ij")
+    grid = torch.stack([xs, ys], -1).float().reshape(1, h * w, 2).repeat(B, 1, 1)
+    coords = (grid + spread * torch.randn(grid.shape, generator=g)).reshape(-1, 2).contiguous().to(DEV)
+    nb = (2 * r + 1) ** 2
+    one = torch.full((B * h * w, L * nb), 7.0, device=DEV)
+    per = torch.full((B * h * w, L * nb), 7.0, device=DEV)
+    f1o, f1p = (torch.zeros(B * h * w, 2, device=DEV) for _ in range(2))
+    s = K.stream_handle()
+    arrs = K.alt_levels_args(lv)
+    _lib.call("raft_alt_corr_lookup_levels", f1.data_ptr(), *arrs, L, coords.data_ptr(), 0, one.data_ptr(), L * nb,
+              B, h, w, C, r, 16.0, f1o.data_ptr(), 2, None, s)
+    for l, (f2, hh, ww) in enumerate(lv):
+        _lib.call("raft_alt_corr_lookup_nhwc", f1.data_ptr(), f2.data_ptr(), coords.data_ptr(), 0, float(2 ** l),
+                  per.data_ptr() + 4 * l * nb, L * nb, B, h, w, hh, ww, C, r, 16.0,
+                  f1p.data_ptr() if l == 0 else None, 2, None, s)
+    torch.cuda.synchronize()
+    assert torch.equal(one, per) and torch.equal(f1o, f1p)
+    # and the oracle, per level
+    from oracle import raft_oracle as O
+    co = coords.cpu().numpy().reshape(B, 1, h, w, 2)
+    for l, (f2, hh, ww) in enumerate(lv):
+        ref = O.alt_corr_forward(f1.cpu().numpy().reshape(B, h, w, C), f2.cpu().numpy().reshape(B, hh, ww, C),
+                                 co / 2 ** l, r)[:, 0] / 16.0
+        got = one[:, l * nb:(l + 1) * nb].cpu().numpy().reshape(B, h, w, nb).transpose(0, 3, 1, 2)
+        assert np.abs(got - ref).max() < 2e-5, (l, np.abs(got - ref).max())
+
+
 @pytest.mark.parametrize("r", [4, 3])
 def test_alternate_corr_block_golden(r):
     from raft_optical_flow_amd import AlternateCorrBlock

@@ -28,8 +28,16 @@ ntap = L * (2 * r + 1) ** 2
 out = torch.empty(B * h * w, ntap, device=dev)
 
 
+ARRS = K.alt_levels_args([(f2s[l], h >> l, w >> l) for l in range(L)])
+PER_LEVEL = os.environ.get("ALT_PER_LEVEL") == "1"  # L raft_alt_corr_lookup_nhwc calls instead of one levels call
+
+
 def run():
     s = K.stream_handle()
+    if not PER_LEVEL:
+        _lib.call("raft_alt_corr_lookup_levels", f1.data_ptr(), *ARRS, L, coords.data_ptr(), 0, out.data_ptr(), ntap,
+                  B, h, w, C, r, 16.0, None, 0, None, s)
+        return
     for l in range(L):
         _lib.call("raft_alt_corr_lookup_nhwc", f1.data_ptr(), f2s[l].data_ptr(), coords.data_ptr(), 0, float(2 ** l),
                   out.data_ptr() + 4 * l * 81, ntap, B, h, w, h >> l, w >> l, C, r, 16.0, None, 0, None, s)
