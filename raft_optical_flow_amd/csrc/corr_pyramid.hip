@@ -205,6 +205,142 @@ __global__ __launch_bounds__(256) void corr_build_kernel(CorrBuildArgs a) {
   }
 }
 
+// K2 in the fp32-accurate split with 128 x 128 tiles (the forward's corr build): the same
+// arithmetic as corr_build_kernel<true> per output (hi*hi, lo*hi, hi*lo accumulated per
+// K-step in the same order), 8 waves of 32 x 64, so every fmap row staged serves twice the
+// products (the 64 x 64 kernel moved 2 x the L2 bytes per output).  The N tile is an 8 x 16
+// (h2, w2) block: per query pixel the epilogue writes two 256-B runs of level-0 tiles and one
+// 128-B run of two level-1 tiles.
+constexpr int CB2_BM = 128, CB2_BN = 128, CB2_TLD = CB2_BN + 1;
+
+__global__ __launch_bounds__(512, 2) void corr_build2_kernel(CorrBuildArgs a) {
+  constexpr int STAGE = (CB2_BM + CB2_BN) * CB_LDSK;  // floats per stage (144-B rows)
+  static_assert(2 * STAGE >= CB2_BM * CB2_TLD, "the epilogue tile fits the staging area");
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 3, wn = wave >> 2;  // 32 query rows x 64 block pixels per wave
+  const int b = blockIdx.z;
+  const int m0 = blockIdx.x * CB2_BM;
+  const int nbx = (a.W + 15) / 16;
+  const int by = blockIdx.y / nbx, bx = blockIdx.y - (blockIdx.y / nbx) * nbx;
+  const int lr = tid >> 3, lq = tid & 7;  // staged rows lr, lr + 64; channel quad lq of the K-step
+  const float* arow[2];
+  const float* brow[2];
+  bool av_[2], bv_[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = lr + 64 * i;
+    const int p1 = m0 + r;
+    av_[i] = p1 < a.P;
+    arow[i] = a.f1 + ((long)b * a.P + (av_[i] ? p1 : 0)) * a.ld + lq * 4;
+    const int h2 = by * 8 + (r >> 4), w2 = bx * 16 + (r & 15);
+    bv_[i] = h2 < a.H && w2 < a.W;
+    brow[i] = a.f2 + ((long)b * a.P + (bv_[i] ? h2 * a.W + w2 : 0)) * a.ld + lq * 4;
+  }
+  f32x4 ra[2], rb[2];
+  bool ok_a[2], ok_b[2];
+  auto gload = [&](int kc) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool cin = kc * CB_BK + lq * 4 < a.C;  // C % 4 == 0; zero-fill the K tail
+      ok_a[i] = av_[i] && cin;
+      ok_b[i] = bv_[i] && cin;
+      ra[i] = *reinterpret_cast<const f32x4*>(ok_a[i] ? arow[i] + kc * CB_BK : a.f1);
+      rb[i] = *reinterpret_cast<const f32x4*>(ok_b[i] ? brow[i] + kc * CB_BK : a.f2);
+    }
+  };
+  auto put = [&](float* base, int row, f32x4 v) {
+    h4 hi, lo;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const _Float16 hh = (_Float16)v[e];
+      hi[e] = hh;
+      lo[e] = (_Float16)(v[e] - (float)hh);
+    }
+    char* r = reinterpret_cast<char*>(base) + row * (CB_LDSK * 4) + lq * 8;
+    *reinterpret_cast<h4*>(r) = hi;
+    *reinterpret_cast<h4*>(r + 64) = lo;
+  };
+  auto sstore = [&](int buf) {
+    float* A = smem + buf * STAGE;
+    float* Bt = A + CB2_BM * CB_LDSK;
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      put(A, lr + 64 * i, ok_a[i] ? ra[i] : z);
+      put(Bt, lr + 64 * i, ok_b[i] ? rb[i] : z);
+    }
+  };
+  const int nk = cdiv(a.C, CB_BK);
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  f32x16 acc[2] = {}, accl[2] = {};  // hi*hi | lo*hi + hi*lo
+  for (int kc = 0; kc < nk; ++kc) {
+    const int cur = kc & 1;
+    const bool more = kc + 1 < nk;
+    if (more) gload(kc + 1);
+    const float* A = smem + cur * STAGE;
+    const float* Bt = A + CB2_BM * CB_LDSK;
+    const char* Ar = reinterpret_cast<const char*>(A) + (wm * 32 + (lane & 31)) * (CB_LDSK * 4) + (lane >> 5) * 16;
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      const h8 xh = *reinterpret_cast<const h8*>(Ar + 32 * qq), xl = *reinterpret_cast<const h8*>(Ar + 64 + 32 * qq);
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        const char* Br = reinterpret_cast<const char*>(Bt) + (wn * 64 + sb * 32 + (lane & 31)) * (CB_LDSK * 4) +
+                         (lane >> 5) * 16;
+        const h8 yh = *reinterpret_cast<const h8*>(Br + 32 * qq), yl = *reinterpret_cast<const h8*>(Br + 64 + 32 * qq);
+        acc[sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, yh, acc[sb], 0, 0, 0);
+        accl[sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, yh, accl[sb], 0, 0, 0);
+        accl[sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, yl, accl[sb], 0, 0, 0);
+      }
+    }
+    if (more) sstore(cur ^ 1);
+    __syncthreads();
+  }
+  // epilogue: scaled tile -> LDS T[128 p1][128 = 8 rows x 16 cols of the (h2, w2) block]
+  float* T = smem;
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+    const int n = wn * 64 + sb * 32 + (lane & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      T[row * CB2_TLD + n] = (acc[sb][r] + accl[sb][r]) / a.sqrt_c;
+    }
+  }
+  __syncthreads();
+  // level 0: tiles (2by + ti, 4bx + tj); the four tiles of a tile row are adjacent (256 B)
+  for (int idx = tid; idx < CB2_BM * 128; idx += 512) {
+    const int row = idx >> 7, o = idx & 127;
+    const int p1 = m0 + row;
+    const int ti = o >> 6, tj = (o >> 4) & 3, e = o & 15;
+    const int ty = 2 * by + ti, tx = 4 * bx + tj;
+    if (p1 < a.P && ty < a.l0.th && tx < a.l0.tw) {
+      const int n = (ti * 4 + (e >> 2)) * 16 + tj * 4 + (e & 3);
+      a.pyr[a.l0.off + ((long)b * a.P + p1) * a.l0.mapsz + ((long)ty * a.l0.tw + tx) * 16 + e] = T[row * CB2_TLD + n];
+    }
+  }
+  if (a.has_l1 && by < a.l1.th) {
+    // level 1: the block pooled 2x2 -> level-1 tiles (by, 2bx + tj), zeros beyond H1 x W1
+    for (int idx = tid; idx < CB2_BM * 32; idx += 512) {
+      const int row = idx >> 5, o = idx & 31;
+      const int p1 = m0 + row;
+      const int tj = o >> 4, e = o & 15;
+      const int tx1 = 2 * bx + tj;
+      if (p1 >= a.P || tx1 >= a.l1.tw) continue;
+      const int yy = e >> 2, xx = tj * 4 + (e & 3);
+      float v = 0.f;
+      if (by * 4 + yy < a.l1.h && bx * 8 + xx < a.l1.w) {
+        const float* t = T + row * CB2_TLD + (2 * yy) * 16 + 2 * xx;
+        v = (((t[0] + t[1]) + t[16]) + t[17]) / 4.0f;  // avg_pool2d window order
+      }
+      a.pyr[a.l1.off + ((long)b * a.P + p1) * a.l1.mapsz + ((long)by * a.l1.tw + tx1) * 16 + e] = v;
+    }
+  }
+}
+
 // Level l -> l+1 2x2 average pool (floor), tiled -> tiled, zeros in the padding.
 __global__ void pool2_tiled_kernel(const float* pyr, float* out_base, long n_maps, Level src,
                                    Level dst) {
@@ -698,11 +834,20 @@ extern "C" int raft_corr_build_prec(const float* fmap1, const float* fmap2, int 
   a.l1 = lv[L > 1 ? 1 : 0];
   a.nbx = cdiv(W, 8);
   hipStream_t s = as_stream(stream);
-  dim3 grid(cdiv((int)P, CB_BM), cdiv(H, 8) * a.nbx, B);
-  if (precision == RAFT_PREC_FP32)
+  static const bool big = [] {
+    const char* e = getenv("RAFT_CORR_BUILD_BIG");
+    return !(e && e[0] == '0');
+  }();
+  if (precision == RAFT_PREC_FP32) {
+    dim3 grid(cdiv((int)P, CB_BM), cdiv(H, 8) * a.nbx, B);
     hipLaunchKernelGGL(corr_build_kernel<false>, grid, dim3(256), 0, s, a);
-  else
+  } else if (big) {
+    dim3 grid(cdiv((int)P, CB2_BM), cdiv(H, 8) * cdiv(W, 16), B);
+    hipLaunchKernelGGL(corr_build2_kernel, grid, dim3(512), 0, s, a);
+  } else {
+    dim3 grid(cdiv((int)P, CB_BM), cdiv(H, 8) * a.nbx, B);
     hipLaunchKernelGGL(corr_build_kernel<true>, grid, dim3(256), 0, s, a);
+  }
   int rc = check_launch("raft_corr_build");
   if (rc) return rc;
   for (int l = 2; l < L; ++l) {
