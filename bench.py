@@ -134,7 +134,7 @@ def rotated_lookup(plan, batch, h8, w8, nrot, reps):
     del pyrs
     torch.cuda.empty_cache()
     alg = batch * h8 * w8 * lookup_bytes_per_pixel(L, r)
-    return {"kernel": "corr_lookup_kernel<4,4> (raft_corr_lookup)", "batch": batch, "bound": "hbm",
+    return {"kernel": "corr_lookup_kernel<4,4,false> (raft_corr_lookup)", "batch": batch, "bound": "hbm",
             "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": alg,
             "launch_us": round(t * 1e6, 2),
@@ -309,7 +309,15 @@ def main():
     # the update block's main-stream convolutions of one (non-final) iteration, replayed as a graph
     # (their operands are L2 / MALL-resident in the forward as well: 7 MB activations, <= 2 MB weights)
     lk_idx = [i for i, l in enumerate(plan.launches) if getattr(l, "name", "") in
-              ("raft_corr_lookup", "raft_alt_corr_lookup_levels")]
+              ("raft_corr_lookup", "raft_corr_lookup_convf1", "raft_alt_corr_lookup_levels")]
+    if not args.alternate_corr and plan.launches[lk_idx[0]].name == "raft_corr_lookup_convf1":
+        # the forward's lookup launch also runs the motion encoder's convf1 (raft_hip.h): its
+        # duration beside the lookup-only kernel's (cache-warm replays of the last iteration's)
+        fl1 = plan.launches[lk_idx[-1]]
+        roof["forward_launch"] = {
+            "kernel": "corr_lookup_kernel<4,4,true> (raft_corr_lookup_convf1: lookup + convf1)",
+            "launch_us": round(time_kernel_events(lambda: fl1(K.stream_handle()), 50) * 1e6, 2),
+            "timing": "HIP events around a hipGraph of 50 replays of the last iteration's launch (cache-warm)"}
     per_it = len(lk_idx) // args.iters
     it_convs = [plan.launches[i] for i in range(lk_idx[per_it] + 1, lk_idx[2 * per_it])
                 if getattr(plan.launches[i], "name", "") in ("raft_conv2d", "raft_conv2d_pair")

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define RAFT_HIP_ABI_VERSION 8
+#define RAFT_HIP_ABI_VERSION 9
 
 /* Negative return codes (argument errors, raised before any launch). */
 #define RAFT_E_INVALID (-1)   /* bad size / null pointer / unsupported shape */
@@ -92,6 +92,22 @@ int raft_corr_pyramid_level(const float* pyramid, int B, int H, int W, int num_l
 int raft_corr_lookup(const float* pyramid, int B, int H, int W, int num_levels, int radius,
                      const float* coords, int coords_layout, float* out, int out_ld, int out_layout,
                      float* flow_out, int flow_ld, int* range_flag, raft_stream_t stream);
+/* raft_corr_lookup and, in the same launch, the motion encoder's first flow conv
+ * (BasicMotionEncoder.convf1, core/update.py:186,205): f1_out rows [B*H*W][f1_out_ld]
+ * (16-B aligned, ld % 4 == 0) = relu(conv7x7(flow) + f1_bias), flow = coords - coords_grid
+ * with zero padding, as the reference's F.relu(self.convf1(flow)).  The convf1 work-groups
+ * run on the VALU beside the lookup's memory-bound waves instead of as a launch of their own.
+ * f1_weight: [f1_n/32][k*k][2][32] fp32 (16-B aligned), element ((g*k*k + dy*k + dx)*2 + ci)*32 + j
+ * = weight[32g + j][ci][dy][dx] of the OIHW tensor; f1_k = 7, f1_n % 32 == 0.  Products are
+ * exact fp32; f1_precision RAFT_PREC_F16 / RAFT_PREC_BF16 rounds the flow operand to that
+ * type (round the weights the same way, as the MFMA kernels' operands).  f1_range_flag:
+ * the range guard of the output (it feeds the split-precision convf2), or NULL.  The lookup
+ * outputs are bit-identical to raft_corr_lookup's. */
+int raft_corr_lookup_convf1(const float* pyramid, int B, int H, int W, int num_levels, int radius,
+                            const float* coords, int coords_layout, float* out, int out_ld, int out_layout,
+                            float* flow_out, int flow_ld, int* range_flag, const float* f1_weight,
+                            const float* f1_bias, int f1_n, int f1_k, int f1_precision, float* f1_out,
+                            int f1_out_ld, int* f1_range_flag, raft_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * On-the-fly ("alternate") correlation — the alt_cuda_corr plugin.

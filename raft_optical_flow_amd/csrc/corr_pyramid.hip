@@ -487,21 +487,154 @@ __device__ __forceinline__ unsigned long long lk_clock(bool real) {
 #define LK_STAMP(k)
 #endif
 
-template <int R, int LMAX>
-__global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
+// ============================================================================
+// The lookup and the motion encoder's first flow conv in one launch
+// (core/update.py:186,205: flo = relu(convf1(flow)), a 7x7 conv of the 2-channel
+// flow = coords1 - coords0).  convf1 does not read the lookup's outputs: it
+// takes the flow from the same coords.  As its own GEMM launch it is K = 98 —
+// a few microseconds of MFMA work behind a launch's fixed cost; here its
+// work-groups (dispatched first) run on the VALU beside the memory-bound
+// lookup waves, with no launch of their own.
+//
+// A convf1 work-group: a 4x16 pixel tile x 32 output channels; wave w owns
+// channels 8w .. 8w+7 of the group for all 64 pixels (lane = pixel).  The
+// group's weights (49 taps x 2 x 32, 12.5 KB, one coalesced copy) and the flow
+// patch (10x22 pixels, zeros off the image) are staged in the LDS the lookup
+// blocks use for their patches; per tap the lane reads its flow pair and the
+// wave's 16 weights (broadcast reads) and accumulates 16 fp32 FMAs (packed).
+// (Weights as wave-uniform scalar loads instead: each dy row waited on the
+// scalar cache, 16.2 us per fused launch in the forward under rocprof.)  Exact
+// fp32 products (the reference's fp32 conv, any summation order); the f16 /
+// bf16 modes round the flow here and the weights on the host, as the MFMA
+// kernels' operands.
+// ============================================================================
+struct FlowConvArgs {
+  const float* w;     // [n/32][k*k][2][32] fp32 (rounded to the conv precision's operand type)
+  const float* bias;  // [n] or null
+  float* out;
+  int out_ld;
+  int n, k;           // output channels (multiple of 32), kernel size (7: RAFT's convf1)
+  int rnd;            // flow operand rounding: 0 none, 1 f16, 2 bf16
+  int* range_flag;    // f16x3 range guard of the output (feeds convf2), or null
+  int tx, ty;         // 4x16 pixel tiles per image row / column
+  int ngrp;           // n / 32
+  int nblocks;        // B * ty * tx * ngrp
+};
+
+constexpr int FC_TH = 4, FC_TW = 16, FC_MAXK = 7, FC_CG = 32;  // 4x16 pixels x 32 channels per work-group
+constexpr int FC_PW = FC_TW + FC_MAXK - 1, FC_PH = FC_TH + FC_MAXK - 1;  // 22 x 10 patch
+
+__device__ __forceinline__ float round_operand(float v, int rnd) {
+  if (rnd == 1) return (float)(_Float16)v;
+  if (rnd == 2) return (float)(__bf16)v;
+  return v;
+}
+
+__device__ __forceinline__ void flowconv_block(const FlowConvArgs& f, const LookupArgs& a, int bid, float* lds) {
+  constexpr int KK = FC_MAXK * FC_MAXK;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int t = bid;
+  const int g = t % f.ngrp;
+  t /= f.ngrp;
+  const int tc = t % f.tx;
+  t /= f.tx;
+  const int tr = t % f.ty;
+  const int b = t / f.ty;
+  const int H = a.H, W = a.W, P = H * W;
+  constexpr int pad = FC_MAXK / 2;
+  const int y0 = tr * FC_TH - pad, x0 = tc * FC_TW - pad;
+  // LDS: the group's weights [tap][ci][32] (12.5 KB), then the flow patch (10 x 22 float2)
+  float* wl = lds;
+  float2* fl = reinterpret_cast<float2*>(lds + KK * 2 * FC_CG);
+  const f32x4* wsrc = reinterpret_cast<const f32x4*>(f.w + (long)g * KK * 2 * FC_CG);
+  for (int i = threadIdx.x; i < KK * 2 * FC_CG / 4; i += 256) reinterpret_cast<f32x4*>(wl)[i] = wsrc[i];
+  for (int i = threadIdx.x; i < FC_PH * FC_PW; i += 256) {
+    const int yy = y0 + i / FC_PW, xx = x0 + i % FC_PW;
+    float2 v = {0.f, 0.f};
+    if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) {
+      float cx, cy;
+      load_coords(a.coords, a.coords_layout, b, yy * W + xx, P, cx, cy);
+      // the lookup's flow output: coords1 - coords0, the same two subtractions
+      v.x = round_operand(cx - (float)xx, f.rnd);
+      v.y = round_operand(cy - (float)yy, f.rnd);
+    }
+    fl[i] = v;
+  }
+  __syncthreads();
+  const int ly = lane >> 4, lx = lane & 15;
+  // this wave: channels 8*wv .. 8*wv+7 of the group, weights as wave-uniform (broadcast) LDS reads
+  const float* ww = wl + wv * 8;
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll 1
+  for (int dy = 0; dy < FC_MAXK; ++dy) {
+    const float2* row = fl + (ly + dy) * FC_PW + lx;
+    const float* wr = ww + dy * FC_MAXK * 2 * FC_CG;
+#pragma unroll
+    for (int dx = 0; dx < FC_MAXK; ++dx) {
+      const float2 v = row[dx];
+      const f32x4 w0a = *reinterpret_cast<const f32x4*>(wr + dx * 2 * FC_CG);
+      const f32x4 w0b = *reinterpret_cast<const f32x4*>(wr + dx * 2 * FC_CG + 4);
+      const f32x4 w1a = *reinterpret_cast<const f32x4*>(wr + dx * 2 * FC_CG + FC_CG);
+      const f32x4 w1b = *reinterpret_cast<const f32x4*>(wr + dx * 2 * FC_CG + FC_CG + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[j] = fmaf(v.x, w0a[j], acc[j]);
+        acc[4 + j] = fmaf(v.x, w0b[j], acc[4 + j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[j] = fmaf(v.y, w1a[j], acc[j]);
+        acc[4 + j] = fmaf(v.y, w1b[j], acc[4 + j]);
+      }
+    }
+  }
+  const int oy = tr * FC_TH + ly, ox = tc * FC_TW + lx;
+  if (oy >= H || ox >= W) return;
+  const int c0 = g * FC_CG + wv * 8;
+  float o[8];
+  bool big = false;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    o[j] = fmaxf(acc[j] + (f.bias ? f.bias[c0 + j] : 0.f), 0.f);
+    big |= o[j] > RAFT_RANGE_LIMIT;
+  }
+  if (f.range_flag && big) *f.range_flag = 1;
+  float* dst = f.out + ((long)b * P + oy * W + ox) * f.out_ld + c0;
+  *reinterpret_cast<f32x4*>(dst) = f32x4{o[0], o[1], o[2], o[3]};
+  *reinterpret_cast<f32x4*>(dst + 4) = f32x4{o[4], o[5], o[6], o[7]};
+}
+
+// blocks [0, f.nblocks) of the F1 instantiation: convf1 tiles (above); the rest, and every
+// block of the plain lookup: four query pixels, one per wave (pixel (blockIdx - nblocks)*4 + wave)
+template <int R, int LMAX, bool F1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void corr_lookup_kernel(LookupArgs a,
+                                                                                                 FlowConvArgs f) {
+  __shared__ __attribute__((aligned(16))) float patch[4][16 * patch_rs<LMAX>()];
+  __shared__ __attribute__((aligned(16))) int4 ytab[4][LMAX * (2 * R + 1)];  // y-entries: (w, t, 1 - t, floor)
+  int bid = (int)blockIdx.x;
+  if constexpr (F1) {
+    static_assert(4 * 16 * patch_rs<LMAX>() >= FC_MAXK * FC_MAXK * 2 * FC_CG + 2 * FC_PW * FC_PH,
+                  "convf1's weights and flow patch fit the lookup patches");
+    if (bid < f.nblocks) {
+      flowconv_block(f, a, bid, &patch[0][0]);
+      return;
+    }
+    bid -= f.nblocks;
+  }
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   constexpr int RD = 2 * R + 1;
   constexpr int WD = 2 * R + 2;  // integer window (<= 10 -> <= 4 tiles per axis)
   constexpr int RS = patch_rs<LMAX>();  // patch row stride (floats)
   static_assert(WD <= 13, "window must fit 4 tiles");
   static_assert(LMAX * RD <= 64, "one lane per (level, x offset)");
   static_assert(RS + 16 <= 255, "ds_read2 offsets");
-  __shared__ __attribute__((aligned(16))) float patch[4][16 * RS];
-  __shared__ __attribute__((aligned(16))) int4 ytab[4][LMAX * RD];  // y-entries: (w, t, 1 - t, floor)
   const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int P = a.H * a.W;
   // global pixel index b*P + p: wave-uniform, so the index math stays scalar (B*P < 2^30, host-checked)
-  const int gp = (int)blockIdx.x * 4 + wv;
+  const int gp = bid * 4 + wv;
   const bool valid = gp < a.B * P;
   const int gpc = valid ? gp : 0;
   const int b = gpc / P;
@@ -709,6 +842,7 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(LookupArgs a) {
 }
 
 
+
 // Any radius / level count (the reference's CorrBlock takes any r; RAFT's r = 3, 4 use the
 // kernel above): one thread per (query pixel, level, output channel), the same per-axis
 // arithmetic as axis_entry, corners read from the tiled maps (zeros off the map; NaN where
@@ -872,9 +1006,11 @@ extern "C" int raft_corr_pyramid_level(const float* pyramid, int B, int H, int W
   return check_launch("raft_corr_pyramid_level");
 }
 
-extern "C" int raft_corr_lookup(const float* pyramid, int B, int H, int W, int L, int radius, const float* coords,
-                                int coords_layout, float* out, int out_ld, int out_layout, float* flow_out,
-                                int flow_ld, int* range_flag, raft_stream_t stream) {
+namespace {
+// validated LookupArgs of a raft_corr_lookup call (0, or the error code)
+int lookup_args(LookupArgs& a, const float* pyramid, int B, int H, int W, int L, int radius, const float* coords,
+                int coords_layout, float* out, int out_ld, int out_layout, float* flow_out, int flow_ld,
+                int* range_flag) {
   RAFT_REQUIRE(pyramid && coords && out, "raft_corr_lookup: null pointer");
   RAFT_REQUIRE(B > 0 && H > 0 && W > 0 && L >= 1 && L <= LK_MAXL, "raft_corr_lookup: bad sizes");
   RAFT_REQUIRE(radius >= 0 && radius <= 32, "raft_corr_lookup: radius must be 0..32 (got %d)", radius);
@@ -886,7 +1022,6 @@ extern "C" int raft_corr_lookup(const float* pyramid, int B, int H, int W, int L
   RAFT_REQUIRE(((uintptr_t)pyramid & 15) == 0, "raft_corr_lookup: pyramid must be 16-byte aligned");
   RAFT_REQUIRE((long)B * H * W < (1L << 30), "raft_corr_lookup: more than 2^30 query pixels (split the batch)");
   RAFT_REQUIRE((long)H * W * 16 * 4 < (1L << 31), "raft_corr_lookup: a per-pixel map exceeds 2 GiB");
-  LookupArgs a;
   RAFT_REQUIRE(pyramid_levels(B, H, W, L, a.lv), "raft_corr_lookup: a pyramid level is empty");
   for (int l = L; l < LK_MAXL; ++l) a.lv[l] = a.lv[L - 1];
   for (int l = 0; l < LK_MAXL; ++l) {
@@ -911,6 +1046,18 @@ extern "C" int raft_corr_lookup(const float* pyramid, int B, int H, int W, int L
   a.flow = flow_out;
   a.flow_ld = flow_ld;
   a.range_flag = range_flag;
+  return 0;
+}
+}  // namespace
+
+extern "C" int raft_corr_lookup(const float* pyramid, int B, int H, int W, int L, int radius, const float* coords,
+                                int coords_layout, float* out, int out_ld, int out_layout, float* flow_out,
+                                int flow_ld, int* range_flag, raft_stream_t stream) {
+  LookupArgs a;
+  const int rc = lookup_args(a, pyramid, B, H, W, L, radius, coords, coords_layout, out, out_ld, out_layout, flow_out,
+                             flow_ld, range_flag);
+  if (rc) return rc;
+  const int rd = 2 * radius + 1;
   dim3 grid((unsigned)cdiv_l((long)B * H * W, 4));
   hipStream_t s = as_stream(stream);
   if (radius > 4 || radius < 1) {  // any other radius: the generic kernel
@@ -921,9 +1068,9 @@ extern "C" int raft_corr_lookup(const float* pyramid, int B, int H, int W, int L
 #define RAFT_LOOKUP_CASE(RR)                                                           \
   case RR:                                                                             \
     if (L <= 4)                                                                        \
-      hipLaunchKernelGGL((corr_lookup_kernel<RR, 4>), grid, dim3(256), 0, s, a);       \
+      hipLaunchKernelGGL((corr_lookup_kernel<RR, 4, false>), grid, dim3(256), 0, s, a, FlowConvArgs{}); \
     else                                                                               \
-      hipLaunchKernelGGL((corr_lookup_kernel<RR, LK_MAXL>), grid, dim3(256), 0, s, a); \
+      hipLaunchKernelGGL((corr_lookup_kernel<RR, LK_MAXL, false>), grid, dim3(256), 0, s, a, FlowConvArgs{}); \
     break;
   switch (radius) {
     RAFT_LOOKUP_CASE(1)
@@ -934,4 +1081,65 @@ extern "C" int raft_corr_lookup(const float* pyramid, int B, int H, int W, int L
   }
 #undef RAFT_LOOKUP_CASE
   return check_launch("raft_corr_lookup");
+}
+
+extern "C" int raft_corr_lookup_convf1(const float* pyramid, int B, int H, int W, int L, int radius,
+                                       const float* coords, int coords_layout, float* out, int out_ld, int out_layout,
+                                       float* flow_out, int flow_ld, int* range_flag, const float* f1_weight,
+                                       const float* f1_bias, int f1_n, int f1_k, int f1_precision, float* f1_out,
+                                       int f1_out_ld, int* f1_range_flag, raft_stream_t stream) {
+  LookupArgs a;
+  int rc = lookup_args(a, pyramid, B, H, W, L, radius, coords, coords_layout, out, out_ld, out_layout, flow_out,
+                       flow_ld, range_flag);
+  if (rc) return rc;
+  RAFT_REQUIRE(f1_weight && f1_out, "raft_corr_lookup_convf1: null convf1 pointer");
+  RAFT_REQUIRE(f1_k == FC_MAXK, "raft_corr_lookup_convf1: kernel size must be 7 (got %d)", f1_k);
+  RAFT_REQUIRE(f1_n > 0 && f1_n % FC_CG == 0,
+               "raft_corr_lookup_convf1: output channels must be a multiple of 32 (got %d)", f1_n);
+  RAFT_REQUIRE(f1_out_ld >= f1_n && f1_out_ld % 4 == 0 && (((uintptr_t)f1_out | (uintptr_t)f1_weight) & 15) == 0,
+               "raft_corr_lookup_convf1: weight and output rows must be 16-byte aligned (ld >= n, ld %% 4 == 0)");
+  RAFT_REQUIRE(f1_precision == RAFT_PREC_FP32 || f1_precision == RAFT_PREC_F16X3 || f1_precision == RAFT_PREC_F16 ||
+                   f1_precision == RAFT_PREC_BF16,
+               "raft_corr_lookup_convf1: bad precision %d", f1_precision);
+  FlowConvArgs f;
+  f.w = f1_weight;
+  f.bias = f1_bias;
+  f.out = f1_out;
+  f.out_ld = f1_out_ld;
+  f.n = f1_n;
+  f.k = f1_k;
+  f.rnd = f1_precision == RAFT_PREC_F16 ? 1 : f1_precision == RAFT_PREC_BF16 ? 2 : 0;
+  f.range_flag = f1_range_flag;
+  f.tx = cdiv(W, FC_TW);
+  f.ty = cdiv(H, FC_TH);
+  f.ngrp = f1_n / FC_CG;
+  const long nb = (long)B * f.tx * f.ty * f.ngrp;
+  RAFT_REQUIRE(nb + cdiv_l((long)B * H * W, 4) < (1L << 31), "raft_corr_lookup_convf1: grid too large");
+  f.nblocks = (int)nb;
+  hipStream_t s = as_stream(stream);
+  const unsigned nlk = (unsigned)cdiv_l((long)B * H * W, 4);
+  if (radius > 4 || radius < 1) {  // the generic lookup, then the convf1 blocks alone
+    rc = raft_corr_lookup(pyramid, B, H, W, L, radius, coords, coords_layout, out, out_ld, out_layout, flow_out,
+                          flow_ld, range_flag, stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL((corr_lookup_kernel<4, 4, true>), dim3(f.nblocks), dim3(256), 0, s, a, f);
+    return check_launch("raft_corr_lookup_convf1(convf1)");
+  }
+  const dim3 grid((unsigned)f.nblocks + nlk);
+#define RAFT_LOOKUP_F1_CASE(RR)                                                                \
+  case RR:                                                                                     \
+    if (L <= 4)                                                                                \
+      hipLaunchKernelGGL((corr_lookup_kernel<RR, 4, true>), grid, dim3(256), 0, s, a, f);       \
+    else                                                                                       \
+      hipLaunchKernelGGL((corr_lookup_kernel<RR, LK_MAXL, true>), grid, dim3(256), 0, s, a, f); \
+    break;
+  switch (radius) {
+    RAFT_LOOKUP_F1_CASE(1)
+    RAFT_LOOKUP_F1_CASE(2)
+    RAFT_LOOKUP_F1_CASE(3)
+    default:
+    RAFT_LOOKUP_F1_CASE(4)
+  }
+#undef RAFT_LOOKUP_F1_CASE
+  return check_launch("raft_corr_lookup_convf1");
 }

@@ -346,10 +346,36 @@ def plan_gru_context(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w):
         _conv(L, ctx, ub.inp(pu), B, h, w, Rows(buf), epilogue=_lib.EPI_LINEAR)
 
 
-def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool):
+def convf1_fused(pu: PackedUpdate) -> bool:
+    """Whether the all-pairs loop computes convf1 inside the lookup launch
+    (raft_corr_lookup_convf1; RAFT_FUSE_CONVF1=0 keeps it a conv launch of its own)."""
+    return (not pu.small and pu.convf1.kh == 7 and pu.convf1.n % 32 == 0
+            and os.environ.get("RAFT_FUSE_CONVF1", "1") != "0")
+
+
+def convf1_vec_weight(pu: PackedUpdate) -> torch.Tensor:
+    """convf1's weight in raft_corr_lookup_convf1's layout [n/32][k*k][2][32] (raft_hip.h),
+    rounded to the operand type of the conv precision (f16 / bf16 modes), cached per precision."""
+    pc = pu.convf1
+    prec = pc.precision
+    cached = getattr(pu, "_convf1_vec", None)
+    if cached is not None and cached[0] == prec:
+        return cached[1]
+    n, kk = pc.n, pc.kh * pc.kw
+    w = pc.weight[:n, : kk * 2].reshape(n // 32, 32, kk, 2).permute(0, 2, 3, 1).contiguous()
+    if prec == _lib.PREC_F16:
+        w = w.half().float()
+    elif prec == _lib.PREC_BF16:
+        w = w.bfloat16().float()
+    pu._convf1_vec = (prec, w)
+    return w
+
+
+def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool, convf1_done: bool = False):
     """One BasicUpdateBlock / SmallUpdateBlock step (core/update.py:297-325 / :250-263)
     followed by coords1 += delta_flow (core/raft.py:232).  Assumes ub.corr and the
-    flow slot of HX were filled by the lookup and plan_gru_context ran for this pair."""
+    flow slot of HX were filled by the lookup and plan_gru_context ran for this pair
+    (convf1_done: the lookup launch also wrote convf1's output, ub.flo1)."""
     flow = Rows(ub.hx, ub.flow_off(pu), 2)
     cf = Rows(ub.cf)
     # RAFT-full: one stream; convc2 (corr branch) and convf2 (flow branch) are two 3x3 halo
@@ -366,7 +392,8 @@ def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool
         _conv(L, pu.convf2, Rows(ub.flo1), B, h, w, cf.sub(96, 32), epilogue=_lib.EPI_RELU, side=side)
         _conv(L, pu.convc1, Rows(ub.corr), B, h, w, cf.sub(0, 96), epilogue=_lib.EPI_RELU)
     elif pair:
-        _conv(L, pu.convf1, flow, B, h, w, Rows(ub.flo1), epilogue=_lib.EPI_RELU)
+        if not convf1_done:
+            _conv(L, pu.convf1, flow, B, h, w, Rows(ub.flo1), epilogue=_lib.EPI_RELU)
         _conv(L, pu.convc1, Rows(ub.corr), B, h, w, Rows(ub.cor1), epilogue=_lib.EPI_RELU)
         c2 = conv_params(pu.convc2, Rows(ub.cor1), B, h, w, cf.sub(0, 192), epilogue=_lib.EPI_RELU,
                          range_flag=_GUARD["flag"])
@@ -505,9 +532,21 @@ class RaftPlan:
         self.flow_up = [torch.empty(B, 2, H, W, device=device) for _ in range(1 if test_mode else iters)]
         flow_slot = ub.flow_off(pu)
         gflag = self.range_flag.data_ptr() if self.guarded else None
+        # all-pairs RAFT-full: the motion encoder's convf1 runs inside the lookup launch
+        # (its own launch would be a K = 98 GEMM behind a launch's fixed cost)
+        fuse_f1 = not alternate and convf1_fused(pu) and os.environ.get("RAFT_CONV_PAIR", "1") != "0"
+        if fuse_f1:
+            f1w = convf1_vec_weight(pu)
+            f1b = pu.convf1.bias.data_ptr() if pu.convf1.bias is not None else None
         for it in range(iters):
             last = it == iters - 1
-            if not alternate:
+            if fuse_f1:
+                L.append(Launch("raft_corr_lookup_convf1", self.pyramid.data_ptr(), B, h, w, lv, r,
+                                ub.coords.data_ptr(), 0, ub.corr.data_ptr(), corr_ld, 0,
+                                ub.hx.data_ptr() + 4 * flow_slot, pu.ld, gflag, f1w.data_ptr(), f1b, pu.convf1.n,
+                                pu.convf1.kh, pu.convf1.precision, ub.flo1.data_ptr(), ub.flo1.shape[1], gflag,
+                                keep=f1w))
+            elif not alternate:
                 L.append(Launch("raft_corr_lookup", self.pyramid.data_ptr(), B, h, w, lv, r, ub.coords.data_ptr(), 0,
                                 ub.corr.data_ptr(), corr_ld, 0, ub.hx.data_ptr() + 4 * flow_slot, pu.ld, gflag))
             else:
@@ -517,7 +556,7 @@ class RaftPlan:
                                 ub.coords.data_ptr(), 0, ub.corr.data_ptr(), corr_ld, B, h, w, C, r, div,
                                 ub.hx.data_ptr() + 4 * flow_slot, pu.ld, gflag, keep=arrs))
             want_up = last or not test_mode
-            plan_update(L, pu, ub, B, h, w, with_mask=want_up and not pu.small)
+            plan_update(L, pu, ub, B, h, w, with_mask=want_up and not pu.small, convf1_done=fuse_f1)
             if want_up:
                 dst = self.flow_up[-1 if test_mode else it]
                 if pu.small:

@@ -172,6 +172,83 @@ def test_lookup_pipelined_grid_vs_oracle(B, h, w):
     assert maxabs(cb(t(coords)), ref) < 2e-5
 
 
+def _lookup_convf1_case(B, h, w, r, prec, coord_scale=1.0, seed=11):
+    """raft_corr_lookup_convf1 vs raft_corr_lookup + an fp64 torch conv of the flow."""
+    from raft_optical_flow_amd import _lib
+    from raft_optical_flow_amd import kernels as K
+    rng = np.random.default_rng(seed)
+    C, L = 64, 4
+    f1 = rng.standard_normal((B, C, h, w)).astype(np.float32)
+    f2 = rng.standard_normal((B, C, h, w)).astype(np.float32)
+    r1, r2 = K.nchw_to_rows(t(f1)), K.nchw_to_rows(t(f2))
+    pyr = torch.empty(K.pyramid_floats(B, h, w, L), device=DEV)
+    _lib.call("raft_corr_build", r1.data_ptr(), r2.data_ptr(), C, B, h, w, C, L, K.sqrt_c(C), pyr.data_ptr(),
+              K.stream_handle())
+    ys, xs = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    grid = np.stack([xs, ys], -1)[None].astype(np.float32)
+    coords = (grid + coord_scale * rng.normal(0, 3.0, (B, h, w, 2))).astype(np.float32)
+    cr = t(coords.reshape(-1, 2))
+    ntap = L * (2 * r + 1) ** 2
+    P = B * h * w
+    out_a = torch.full((P, ntap), -7.0, device=DEV)
+    out_b = torch.full((P, ntap), -7.0, device=DEV)
+    flow_a = torch.zeros(P, 4, device=DEV)
+    flow_b = torch.zeros(P, 4, device=DEV)
+    n = 128
+    wt = rng.standard_normal((n, 2, 7, 7)).astype(np.float32) * 0.1
+    bias = rng.standard_normal(n).astype(np.float32) * 0.1
+    rnd = {_lib.PREC_F16: torch.float16, _lib.PREC_BF16: torch.bfloat16}.get(prec)
+    wq = torch.from_numpy(wt)
+    if rnd is not None:
+        wq = wq.to(rnd).float()
+    wv = wq.reshape(n // 32, 32, 2, 49).permute(0, 3, 2, 1).contiguous().to(DEV)  # [n/32][k*k][2][32]
+    f1o = torch.full((P, n + 4), -7.0, device=DEV)
+    flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+    _lib.call("raft_corr_lookup", pyr.data_ptr(), B, h, w, L, r, cr.data_ptr(), 0, out_a.data_ptr(), ntap, 0,
+              flow_a.data_ptr(), 4, None, K.stream_handle())
+    _lib.call("raft_corr_lookup_convf1", pyr.data_ptr(), B, h, w, L, r, cr.data_ptr(), 0, out_b.data_ptr(), ntap, 0,
+              flow_b.data_ptr(), 4, None, wv.data_ptr(), t(bias).data_ptr(), n, 7, prec, f1o.data_ptr(), n + 4,
+              flag.data_ptr(), K.stream_handle())
+    torch.cuda.synchronize()
+    # the lookup's outputs are the plain lookup's, bit for bit
+    def same(x, y):  # bitwise, NaN where NaN
+        return bool(((x == y) | (torch.isnan(x) & torch.isnan(y))).all())
+
+    assert same(out_a, out_b) and same(flow_a, flow_b)
+    # convf1 = relu(conv7x7(flow) + b) (core/update.py:205), fp64 reference on the same operands
+    flow = torch.from_numpy(coords - grid).permute(0, 3, 1, 2)
+    if rnd is not None:
+        flow = flow.to(rnd).float()
+    ref = torch.relu(F.conv2d(flow.double(), wq.double(), torch.from_numpy(bias).double(), padding=3))
+    ref = ref.permute(0, 2, 3, 1).reshape(P, n)
+    got = f1o[:, :n].cpu().double()
+    scale = float(ref.abs().max())
+    err = float((got - ref).abs().max())
+    assert err < 2e-6 * max(1.0, scale) * 10, (err, scale)
+    assert bool((f1o[:, n:] == -7.0).all())  # nothing past n channels of a row
+    return int(flag.item()), scale
+
+
+@pytest.mark.parametrize("B,h,w,r", [(1, 55, 128, 4), (2, 17, 21, 3), (1, 19, 27, 6)])
+@pytest.mark.parametrize("prec", ["f16x3", "f16", "bf16"])
+def test_lookup_convf1_equals_lookup_and_conv(B, h, w, r, prec):
+    """The fused lookup + motion-encoder convf1 (raft_corr_lookup_convf1): lookup outputs
+    bit-identical to raft_corr_lookup's (RAFT's r = 4, r = 3, and r = 6 through the generic
+    lookup then the convf1 blocks alone), convf1 within fp32 rounding of an fp64 conv of the
+    same operands (flow and weights rounded to f16 / bf16 in those modes); ragged tiles."""
+    from raft_optical_flow_amd import _lib
+    p = {"f16x3": _lib.PREC_F16X3, "f16": _lib.PREC_F16, "bf16": _lib.PREC_BF16}[prec]
+    flag, _ = _lookup_convf1_case(B, h, w, r, p)
+    assert flag == 0
+
+
+def test_lookup_convf1_range_guard():
+    """A flow so large that convf1's output leaves the f16x3 split range raises the flag."""
+    from raft_optical_flow_amd import _lib
+    flag, scale = _lookup_convf1_case(1, 12, 20, 4, _lib.PREC_F16X3, coord_scale=3e5, seed=3)
+    assert scale > 32768 and flag == 1
+
+
 @pytest.mark.parametrize("n", [1, 2])
 @pytest.mark.parametrize("C", [96, 260])
 def test_alt_cuda_corr_forward_vs_oracle(n, C):

@@ -1,7 +1,7 @@
 """Per-dispatch averages of bench.py's roofline kernels from a rocprofv3 kernel trace of the same
 bench command, to check bench.py's live figures against rocprof:
 
-  * corr_lookup_kernel<4,4>, B=1 grid (1760 x 256 threads) and B=8 grid (14080 x 256), split into
+  * corr_lookup_kernel<4,4,false>, B=1 grid (1760 x 256 threads) and B=8 grid (14080 x 256), split into
       - rotated: the dispatches of bench.py's cache-cold rotation graphs (runs of >= 16 consecutive
         lookups with no other kernel between them)  -> compare with roofline / lookup_b8 launch_us
       - in-forward: every other lookup dispatch (the 32 per forward of the timed graph replays)
@@ -23,7 +23,7 @@ def dur(r):
 
 
 def is_lookup(r):
-    return "corr_lookup_kernel<4, 4>" in r["Kernel_Name"]
+    return "corr_lookup_kernel<4, 4, false>" in r["Kernel_Name"]
 
 
 # runs of consecutive lookup dispatches
@@ -48,13 +48,27 @@ for grid, tag in ((1760 * 256, "B=1"), (14080 * 256, "B=8")):
 # the B=1 update-loop launches of conv_halo_kernel<3,3,64,1> (the convc2 | convf2 pair and the flow
 # head's conv1: 224 work-groups each): dispatches between a forward's first lookup and the end of that
 # forward (prep_images starts the next one), so the encoder's 1/8-res 3x3 convs do not count
-h, in_loop = [], False
+fz, in_fwd = [], False
+for r in rows:
+    if "prep_images" in r["Kernel_Name"]:
+        in_fwd = True
+    elif "flow_from_coords" in r["Kernel_Name"]:
+        in_fwd = False
+    elif in_fwd and "corr_lookup_kernel<4, 4, true>" in r["Kernel_Name"]:
+        fz.append(dur(r))
+if fz:
+    res["corr_lookup + convf1 B=1 in-forward"] = {"dispatches": len(fz), "mean_us": round(statistics.mean(fz), 3),
+                                                   "median_us": round(statistics.median(fz), 3)}
+h, in_fwd, in_loop = [], False, False
 for r in rows:
     name = r["Kernel_Name"]
-    if "prep_images" in name:
-        in_loop = False
-    elif is_lookup(r) and int(r["Grid_Size_X"]) == 1760 * 256:
-        in_loop = True
+    if "prep_images" in name:  # a forward starts
+        in_fwd, in_loop = True, False
+    elif "flow_from_coords" in name:  # ... and ends (the bench's per-kernel replays come after)
+        in_fwd = in_loop = False
+    elif in_fwd and ("corr_lookup_kernel<4, 4, true>" in name or
+                     ("corr_lookup_kernel<4, 4" in name and int(r["Grid_Size_X"]) == 1760 * 256)):
+        in_loop = True  # a B=1 lookup of the forward (lookup-only, or the lookup + convf1 launch)
     elif in_loop and "conv_halo_kernel<3, 3, 64, 1>" in name and int(r["Grid_Size_X"]) in (168 * 512, 224 * 512):
         h.append(dur(r))
 if h:

@@ -11,6 +11,10 @@ import sys
 
 import torch
 
+# the lookup counters are for the lookup-only kernel that bench.py's roofline times (the forward
+# otherwise runs convf1 inside the lookup launch, raft_corr_lookup_convf1)
+os.environ.setdefault("RAFT_FUSE_CONVF1", "0")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
