@@ -49,6 +49,37 @@ def make_model(small, seed=0, alternate=False, precision=None):
     return m.to(DEV).eval(), {k: v.numpy() for k, v in sd.items()}
 
 
+# ----------------------------------------------------------------------------- instance norm
+
+
+@pytest.mark.parametrize("B,HW,C,ld", [(2, 220 * 512, 64, 64), (3, 1000, 96, 100), (1, 77, 6, 6), (2, 513, 300, 300)])
+def test_instnorm_stats_vs_fp64(B, HW, C, ld):
+    """raft_instnorm_stats (one launch: chunk partials, the last block of each image finalizes):
+    mean and 1/sqrt(var + eps) against fp64, per (image, channel); the vectorised and scalar
+    partial kernels, > 256 channels; three calls on one workspace (its arrival counters re-arm)
+    give bit-identical stats."""
+    from raft_optical_flow_amd import _lib
+    from raft_optical_flow_amd import kernels as K
+    g = torch.Generator().manual_seed(B * 7 + C)
+    x = (torch.randn(B * HW, ld, generator=g) * 3 + torch.linspace(-5, 5, ld)).float()
+    xd = x.to(DEV)
+    ws = K.instnorm_workspace(B, HW, C, DEV)
+    outs = []
+    for _ in range(3):
+        st = torch.full((B * C * 2,), -1.0, device=DEV)
+        _lib.call("raft_instnorm_stats", xd.data_ptr(), ld, B, HW, C, 1e-5, st.data_ptr(), ws.data_ptr(),
+                  K.stream_handle())
+        torch.cuda.synchronize()
+        outs.append(st.cpu())
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    xv = x[:, :C].double().reshape(B, HW, C)
+    mean = xv.mean(1)
+    rstd = 1.0 / torch.sqrt(xv.var(1, unbiased=False) + 1e-5)
+    got = outs[0].double().reshape(B, C, 2)
+    assert float((got[..., 0] - mean).abs().max()) < 1e-5 * max(1.0, float(mean.abs().max()))
+    assert float(((got[..., 1] - rstd) / rstd).abs().max()) < 1e-5
+
+
 # ----------------------------------------------------------------------------- correlation
 
 
