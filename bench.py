@@ -207,10 +207,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # rehearsal of the N > 1 path on a one-GPU box (tests / development only): every rank on
+    # cuda:0 over gloo (RCCL, like NCCL, refuses two ranks on one device)
+    rehearse = os.environ.get("RAFT_BENCH_REHEARSE_1GPU") == "1"
+    dev_index = 0 if rehearse else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from raft_optical_flow_amd import RAFT, InputPadder
     from raft_optical_flow_amd.dist import broadcast_state_dict

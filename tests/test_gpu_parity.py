@@ -327,6 +327,40 @@ def test_alt_corr_tiled_vs_oracle(layout):
         assert maxabs(got, ref[:, 0] / 8.0) < 2e-5
 
 
+@pytest.mark.parametrize("C,size", [(64, 95), (64, 96), (64, 97), (40, 27), (40, 28), (40, 29)])
+@pytest.mark.parametrize("edge", [False, True])
+def test_alt_corr_box_size_limits_vs_oracle(C, size, edge):
+    """Exact window-box sizes at the alternate lookup's path limits: the 8x8 query
+    tile at (0, 0) gets a box of exactly size x size fmap2 pixels — C = 64 runs the MFMA box
+    GEMM (box <= 96, per-pixel path at 97), C = 40 the VALU tile kernel (box <= 28, per-pixel
+    at 29); edge=True puts that box over the map's right and bottom edges (zeros there)."""
+    from raft_optical_flow_amd import _lib
+    from raft_optical_flow_amd import kernels as K
+    rng = np.random.default_rng(size + C)
+    B, H1, W1, r = 1, 16, 16, 4
+    H2 = W2 = 112
+    f1 = rng.standard_normal((B, H1, W1, C)).astype(np.float32)
+    f2 = rng.standard_normal((B, H2, W2, C)).astype(np.float32)
+    ys, xs = np.meshgrid(np.arange(H1), np.arange(W1), indexing="ij")
+    coords = np.stack([xs, ys], -1)[None, None].astype(np.float32)
+    coords = (coords + rng.normal(0, 0.7, coords.shape)).astype(np.float32)
+    # tile (0, 0): floor(x) spans exactly size - (2r + 2) columns (and rows): box = size x size
+    span = size - (2 * r + 2)
+    x0 = (W2 - span + 2.3) if edge else 6.3
+    y0 = (H2 - span + 1.6) if edge else 5.6
+    jj, ii = np.meshgrid(np.arange(8), np.arange(8))
+    coords[0, 0, :8, :8, 0] = x0 + np.round(span * jj / 7.0)
+    coords[0, 0, :8, :8, 1] = y0 + np.round(span * ii / 7.0)
+    ref = O.alt_corr_forward(f1, f2, coords, r)  # [B, 1, 81, H1, W1], unscaled
+    out = torch.empty(B * H1 * W1, 81, device=DEV)
+    f1t, f2t, ct = t(f1), t(f2), t(coords)
+    _lib.call("raft_alt_corr_lookup_nhwc", f1t.data_ptr(), f2t.data_ptr(), ct.data_ptr(), 0, 1.0, out.data_ptr(), 81,
+              B, H1, W1, H2, W2, C, r, 8.0, None, 0, None, K.stream_handle())
+    torch.cuda.synchronize()
+    got = out.reshape(B, H1, W1, 81).permute(0, 3, 1, 2).cpu().numpy()
+    assert maxabs(got, ref[:, 0] / 8.0) < 2e-5
+
+
 @pytest.mark.parametrize("r,spread", [(4, 0.7), (4, 6.0), (3, 0.7)])
 def test_alt_corr_levels_equals_per_level_calls(r, spread):
     """raft_alt_corr_lookup_levels (one launch at r = 4) == the L raft_alt_corr_lookup_nhwc calls, bit for bit,
