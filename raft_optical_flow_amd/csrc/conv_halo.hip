@@ -203,11 +203,20 @@ template <int KH, int KW, int BNT, int PREC>
 __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
   using C = HaloCfg<KH, KW, BNT>;
   constexpr int T = C::T, U = C::U, D = C::D, PW = C::PW, NPIX = C::NPIX, PI = C::PI, PA = C::PA, SB = C::SB;
-  constexpr int NBI = BNT / 8;      // 1-KiB DMA pieces per weight block (one K-step)
-  constexpr int NWP = U * NBI / 4;  // weight pieces per loader wave per load set
-  constexpr int NSUB = BNT / 32;    // 32-column MFMA subtiles per compute wave
   constexpr bool X3 = PREC == RAFT_PREC_F16X3;
   constexpr bool BF = PREC == RAFT_PREC_BF16;
+  // Weight rows in LDS: f16x3 the packed K-step row as it is (32 hi then 32 lo halves, 128 B);
+  // the one-product modes (F16, BF16) read only hi, so only the 64-B hi half of each row
+  // moves (half the weight bytes a CU ingests per K-step).  16-B quads XOR-swizzled by row
+  // so that the fragment reads are conflict-free: 128-B rows by (row >> 1) & 7, 64-B rows
+  // by (row >> 2) & 3.
+  constexpr int WROW = X3 ? 128 : 64;          // bytes per weight row in LDS
+  constexpr int QPR = WROW / 16;               // 16-B quads per row
+  constexpr int RPP = 1024 / WROW;             // rows per 1-KiB DMA piece
+  constexpr int NBI = BNT / RPP;    // 1-KiB DMA pieces per weight block (one K-step)
+  constexpr int NWP = U * NBI / 4;  // weight pieces per loader wave per load set
+  constexpr int NSUB = BNT / 32;    // 32-column MFMA subtiles per compute wave
+
   // LSPLIT: the loaders stage each patch through registers and store it
   // pre-split (f16 hi | lo, the weight-row format), so the MFMA waves read
   // ready fragments; 1x1 convs (a patch per K-step, D = 2) keep fp32 patches
@@ -248,8 +257,8 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
   unsigned wvoff[NWP];
 #pragma unroll
   for (int k = 0; k < NWP; ++k) {
-    const int r = 8 * (wpc0 + k) + (lane >> 3);
-    const int qd = (lane & 7) ^ ((r >> 1) & 7);
+    const int r = RPP * (wpc0 + k) + lane / QPR;
+    const int qd = X3 ? (lane & 7) ^ ((r >> 1) & 7) : (lane & 3) ^ ((r >> 2) & 3);
     wvoff[k] = (unsigned)(n0 + r) * ((unsigned)a.K * 4u) + (unsigned)qd * 16u;
   }
   auto issue_weights = [&](int u) {
@@ -463,7 +472,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
   // ---- compute waves: fragments --------------------------------------------
   const int m = lane & 31, h = lane >> 5;
   const int ppbase = (2 * w + (m >> 4)) * PW + (m & 15);
-  const int bsw = (m >> 1) & 7;  // swizzle of weight row sb*32 + m
+  const int bsw = X3 ? (m >> 1) & 7 : (m >> 2) & 3;  // swizzle of weight row sb*32 + m
   f32x16 acc[NSUB], accx[NSUB];
 #pragma unroll
   for (int sb = 0; sb < NSUB; ++sb) {
@@ -489,9 +498,9 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
     for (int sb = 0; sb < NSUB; ++sb) {
 #pragma unroll
       for (int qq = 0; qq < 2; ++qq) {
-        F.bh[sb][qq] = *reinterpret_cast<const h8*>(Bb + (sb * 32 + m) * 128 + (((2 * h + qq) ^ bsw) << 4));
+        F.bh[sb][qq] = *reinterpret_cast<const h8*>(Bb + (sb * 32 + m) * WROW + (((2 * h + qq) ^ bsw) << 4));
         if constexpr (X3)
-          F.bl[sb][qq] = *reinterpret_cast<const h8*>(Bb + (sb * 32 + m) * 128 + (((4 + 2 * h + qq) ^ bsw) << 4));
+          F.bl[sb][qq] = *reinterpret_cast<const h8*>(Bb + (sb * 32 + m) * WROW + (((4 + 2 * h + qq) ^ bsw) << 4));
       }
     }
     b_bs = b_bs + 1 == SB ? 0 : b_bs + 1;
