@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define RAFT_HIP_ABI_VERSION 9
+#define RAFT_HIP_ABI_VERSION 10
 
 /* Negative return codes (argument errors, raised before any launch). */
 #define RAFT_E_INVALID (-1)   /* bad size / null pointer / unsupported shape */
@@ -108,6 +108,11 @@ int raft_corr_lookup_convf1(const float* pyramid, int B, int H, int W, int num_l
                             float* flow_out, int flow_ld, int* range_flag, const float* f1_weight,
                             const float* f1_bias, int f1_n, int f1_k, int f1_precision, float* f1_out,
                             int f1_out_ld, int* f1_range_flag, raft_stream_t stream);
+/* The same convf1 alone (the alternate-correlation loop, whose lookup launch has no room
+ * for it): f1_out = relu(conv7x7(coords - coords_grid) + f1_bias), arguments as above. */
+int raft_convf1_flow(const float* coords, int coords_layout, int B, int H, int W, const float* f1_weight,
+                     const float* f1_bias, int f1_n, int f1_k, int f1_precision, float* f1_out, int f1_out_ld,
+                     int* f1_range_flag, raft_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * On-the-fly ("alternate") correlation — the alt_cuda_corr plugin.

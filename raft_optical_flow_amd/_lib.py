@@ -29,7 +29,7 @@ PREC_F16 = 2     # single f16 product (mixed precision)
 PREC_BF16 = 3    # single bf16 product on v_mfma_f32_32x32x16_bf16 (bf16 mixed precision)
 PRECISIONS = {"fp32": PREC_FP32, "f16x3": PREC_F16X3, "f16": PREC_F16, "bf16": PREC_BF16}
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 RANGE_LIMIT = 32768.0  # RAFT_RANGE_LIMIT: |x| above it raises the f16x3 range guard
 
 EPI_LINEAR = 0
@@ -76,6 +76,7 @@ _PROTOS = {
     "raft_corr_lookup": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, c_int, c_int, P, c_int, P, P]),
     "raft_corr_lookup_convf1": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, c_int, c_int, P, c_int, P,
                                         P, P, c_int, c_int, c_int, P, c_int, P, P]),
+    "raft_convf1_flow": (c_int, [P, c_int, c_int, c_int, c_int, P, P, c_int, c_int, c_int, P, c_int, P, P]),
     "raft_alt_corr_forward": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, P]),
     "raft_alt_corr_lookup_levels": (c_int, [P, P, P, P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                             ctypes.c_float, P, c_int, P, P]),

@@ -1083,25 +1083,18 @@ extern "C" int raft_corr_lookup(const float* pyramid, int B, int H, int W, int L
   return check_launch("raft_corr_lookup");
 }
 
-extern "C" int raft_corr_lookup_convf1(const float* pyramid, int B, int H, int W, int L, int radius,
-                                       const float* coords, int coords_layout, float* out, int out_ld, int out_layout,
-                                       float* flow_out, int flow_ld, int* range_flag, const float* f1_weight,
-                                       const float* f1_bias, int f1_n, int f1_k, int f1_precision, float* f1_out,
-                                       int f1_out_ld, int* f1_range_flag, raft_stream_t stream) {
-  LookupArgs a;
-  int rc = lookup_args(a, pyramid, B, H, W, L, radius, coords, coords_layout, out, out_ld, out_layout, flow_out,
-                       flow_ld, range_flag);
-  if (rc) return rc;
-  RAFT_REQUIRE(f1_weight && f1_out, "raft_corr_lookup_convf1: null convf1 pointer");
-  RAFT_REQUIRE(f1_k == FC_MAXK, "raft_corr_lookup_convf1: kernel size must be 7 (got %d)", f1_k);
-  RAFT_REQUIRE(f1_n > 0 && f1_n % FC_CG == 0,
-               "raft_corr_lookup_convf1: output channels must be a multiple of 32 (got %d)", f1_n);
+namespace {
+// validated FlowConvArgs of a convf1 call (0, or the error code); who = the entry point's name
+int flowconv_args(FlowConvArgs& f, const char* who, int B, int H, int W, const float* f1_weight, const float* f1_bias,
+                  int f1_n, int f1_k, int f1_precision, float* f1_out, int f1_out_ld, int* f1_range_flag) {
+  RAFT_REQUIRE(f1_weight && f1_out, "%s: null convf1 pointer", who);
+  RAFT_REQUIRE(f1_k == FC_MAXK, "%s: kernel size must be 7 (got %d)", who, f1_k);
+  RAFT_REQUIRE(f1_n > 0 && f1_n % FC_CG == 0, "%s: output channels must be a multiple of 32 (got %d)", who, f1_n);
   RAFT_REQUIRE(f1_out_ld >= f1_n && f1_out_ld % 4 == 0 && (((uintptr_t)f1_out | (uintptr_t)f1_weight) & 15) == 0,
-               "raft_corr_lookup_convf1: weight and output rows must be 16-byte aligned (ld >= n, ld %% 4 == 0)");
+               "%s: weight and output rows must be 16-byte aligned (ld >= n, ld %% 4 == 0)", who);
   RAFT_REQUIRE(f1_precision == RAFT_PREC_FP32 || f1_precision == RAFT_PREC_F16X3 || f1_precision == RAFT_PREC_F16 ||
                    f1_precision == RAFT_PREC_BF16,
-               "raft_corr_lookup_convf1: bad precision %d", f1_precision);
-  FlowConvArgs f;
+               "%s: bad precision %d", who, f1_precision);
   f.w = f1_weight;
   f.bias = f1_bias;
   f.out = f1_out;
@@ -1114,8 +1107,25 @@ extern "C" int raft_corr_lookup_convf1(const float* pyramid, int B, int H, int W
   f.ty = cdiv(H, FC_TH);
   f.ngrp = f1_n / FC_CG;
   const long nb = (long)B * f.tx * f.ty * f.ngrp;
-  RAFT_REQUIRE(nb + cdiv_l((long)B * H * W, 4) < (1L << 31), "raft_corr_lookup_convf1: grid too large");
+  RAFT_REQUIRE(nb + cdiv_l((long)B * H * W, 4) < (1L << 31), "%s: grid too large", who);
   f.nblocks = (int)nb;
+  return 0;
+}
+}  // namespace
+
+extern "C" int raft_corr_lookup_convf1(const float* pyramid, int B, int H, int W, int L, int radius,
+                                       const float* coords, int coords_layout, float* out, int out_ld, int out_layout,
+                                       float* flow_out, int flow_ld, int* range_flag, const float* f1_weight,
+                                       const float* f1_bias, int f1_n, int f1_k, int f1_precision, float* f1_out,
+                                       int f1_out_ld, int* f1_range_flag, raft_stream_t stream) {
+  LookupArgs a;
+  int rc = lookup_args(a, pyramid, B, H, W, L, radius, coords, coords_layout, out, out_ld, out_layout, flow_out,
+                       flow_ld, range_flag);
+  if (rc) return rc;
+  FlowConvArgs f;
+  rc = flowconv_args(f, "raft_corr_lookup_convf1", B, H, W, f1_weight, f1_bias, f1_n, f1_k, f1_precision, f1_out,
+                     f1_out_ld, f1_range_flag);
+  if (rc) return rc;
   hipStream_t s = as_stream(stream);
   const unsigned nlk = (unsigned)cdiv_l((long)B * H * W, 4);
   if (radius > 4 || radius < 1) {  // the generic lookup, then the convf1 blocks alone
@@ -1142,4 +1152,24 @@ extern "C" int raft_corr_lookup_convf1(const float* pyramid, int B, int H, int W
   }
 #undef RAFT_LOOKUP_F1_CASE
   return check_launch("raft_corr_lookup_convf1");
+}
+
+extern "C" int raft_convf1_flow(const float* coords, int coords_layout, int B, int H, int W, const float* f1_weight,
+                                const float* f1_bias, int f1_n, int f1_k, int f1_precision, float* f1_out,
+                                int f1_out_ld, int* f1_range_flag, raft_stream_t stream) {
+  RAFT_REQUIRE(coords && B > 0 && H > 0 && W > 0, "raft_convf1_flow: bad arguments");
+  RAFT_REQUIRE(coords_layout == 0 || coords_layout == 1, "raft_convf1_flow: bad coords_layout");
+  RAFT_REQUIRE((long)B * H * W < (1L << 30), "raft_convf1_flow: more than 2^30 pixels");
+  FlowConvArgs f;
+  const int rc = flowconv_args(f, "raft_convf1_flow", B, H, W, f1_weight, f1_bias, f1_n, f1_k, f1_precision, f1_out,
+                               f1_out_ld, f1_range_flag);
+  if (rc) return rc;
+  LookupArgs a{};  // the convf1 blocks read only the coords and the geometry
+  a.coords = coords;
+  a.coords_layout = coords_layout;
+  a.B = B;
+  a.H = H;
+  a.W = W;
+  hipLaunchKernelGGL((corr_lookup_kernel<4, 4, true>), dim3(f.nblocks), dim3(256), 0, as_stream(stream), a, f);
+  return check_launch("raft_convf1_flow");
 }

@@ -534,13 +534,15 @@ class RaftPlan:
         gflag = self.range_flag.data_ptr() if self.guarded else None
         # all-pairs RAFT-full: the motion encoder's convf1 runs inside the lookup launch
         # (its own launch would be a K = 98 GEMM behind a launch's fixed cost)
-        fuse_f1 = not alternate and convf1_fused(pu) and os.environ.get("RAFT_CONV_PAIR", "1") != "0"
+        # (alternate corr: convf1 as its own VALU launch, raft_convf1_flow: the alternate lookup's
+        # launch has no room for it)
+        fuse_f1 = convf1_fused(pu) and os.environ.get("RAFT_CONV_PAIR", "1") != "0"
         if fuse_f1:
             f1w = convf1_vec_weight(pu)
             f1b = pu.convf1.bias.data_ptr() if pu.convf1.bias is not None else None
         for it in range(iters):
             last = it == iters - 1
-            if fuse_f1:
+            if fuse_f1 and not alternate:
                 L.append(Launch("raft_corr_lookup_convf1", self.pyramid.data_ptr(), B, h, w, lv, r,
                                 ub.coords.data_ptr(), 0, ub.corr.data_ptr(), corr_ld, 0,
                                 ub.hx.data_ptr() + 4 * flow_slot, pu.ld, gflag, f1w.data_ptr(), f1b, pu.convf1.n,
@@ -555,6 +557,10 @@ class RaftPlan:
                 L.append(Launch("raft_alt_corr_lookup_levels", fmap1.data_ptr(), *arrs, len(self.f2levels),
                                 ub.coords.data_ptr(), 0, ub.corr.data_ptr(), corr_ld, B, h, w, C, r, div,
                                 ub.hx.data_ptr() + 4 * flow_slot, pu.ld, gflag, keep=arrs))
+                if fuse_f1:
+                    L.append(Launch("raft_convf1_flow", ub.coords.data_ptr(), 0, B, h, w, f1w.data_ptr(), f1b,
+                                    pu.convf1.n, pu.convf1.kh, pu.convf1.precision, ub.flo1.data_ptr(),
+                                    ub.flo1.shape[1], gflag, keep=f1w))
             want_up = last or not test_mode
             plan_update(L, pu, ub, B, h, w, with_mask=want_up and not pu.small, convf1_done=fuse_f1)
             if want_up:

@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_queries_without_gpu():
     lib = _lib.load()
-    assert lib.raft_hip_abi_version() == _lib.ABI_VERSION == 9
+    assert lib.raft_hip_abi_version() == _lib.ABI_VERSION == 10
     assert lib.raft_hip_arch() == b"gfx950"
     # size queries are pure host arithmetic
     assert lib.raft_corr_pyramid_floats(1, 55, 128, 4) == 7040 * 16 * (14 * 32 + 7 * 16 + 4 * 8 + 2 * 4)
@@ -64,3 +64,5 @@ def test_argument_errors_are_reported_without_launch():
     rc = lib.raft_corr_lookup_convf1(16, 1, 8, 8, 4, 4, 16, 0, 16, 324, 0, None, 0, None, 16, None, 80, 7, 0, 16,
                                      128, None, None)
     assert rc == -1 and b"multiple of 32" in lib.raft_hip_last_error()
+    rc = lib.raft_convf1_flow(16, 0, 1, 8, 8, 16, None, 128, 5, 0, 16, 128, None, None)
+    assert rc == -1 and b"kernel size must be 7" in lib.raft_hip_last_error()

@@ -240,7 +240,11 @@ def _lookup_convf1_case(B, h, w, r, prec, coord_scale=1.0, seed=11):
     _lib.call("raft_corr_lookup_convf1", pyr.data_ptr(), B, h, w, L, r, cr.data_ptr(), 0, out_b.data_ptr(), ntap, 0,
               flow_b.data_ptr(), 4, None, wv.data_ptr(), t(bias).data_ptr(), n, 7, prec, f1o.data_ptr(), n + 4,
               flag.data_ptr(), K.stream_handle())
+    f1s = torch.full((P, n + 4), -7.0, device=DEV)  # convf1 alone (raft_convf1_flow, the alternate loop's)
+    _lib.call("raft_convf1_flow", cr.data_ptr(), 0, B, h, w, wv.data_ptr(), t(bias).data_ptr(), n, 7, prec,
+              f1s.data_ptr(), n + 4, None, K.stream_handle())
     torch.cuda.synchronize()
+    assert torch.equal(f1s, f1o)
     # the lookup's outputs are the plain lookup's, bit for bit
     def same(x, y):  # bitwise, NaN where NaN
         return bool(((x == y) | (torch.isnan(x) & torch.isnan(y))).all())
