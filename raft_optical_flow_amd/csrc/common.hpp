@@ -51,6 +51,7 @@ __device__ inline int xcd_tile(int L, int T) {
 }
 
 using f32x4 = __attribute__((ext_vector_type(4))) float;
+using f32x2 = __attribute__((ext_vector_type(2))) float;
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
 }  // namespace raft

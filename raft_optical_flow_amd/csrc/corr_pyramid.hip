@@ -435,10 +435,11 @@ __device__ __forceinline__ float div_rn(float a, float b, float rcp) {
 constexpr int OFF_PATCH = -1000000;
 constexpr int NAN_POS = -2000000;
 
+// (fc = floor(c), computed by the caller: an integer shift of the wave's level-0 floor)
 template <int R>
-__device__ __forceinline__ void axis_entry(float c, int d, float m1, float rcp, int& w, float& t, int& i) {
+__device__ __forceinline__ void axis_entry(float c, int fc, int d, float m1, float rcp, int& w, float& t, int& i) {
   constexpr int WD = 2 * R + 2;
-  const int v0 = (int)floorf(c) - R;
+  const int v0 = fc - R;
   const int o = (v0 >> 2) * 4;                               // patch origin on this axis
   const int ext = (((v0 + WD - 1) >> 2) - (v0 >> 2) + 1) * 4;  // patch extent (12 or 16)
   const float X = c + (float)(d - R);
@@ -609,7 +610,10 @@ __device__ __forceinline__ void flowconv_block(const FlowConvArgs& f, const Look
 
 // blocks [0, f.nblocks) of the F1 instantiation: convf1 tiles (above); the rest, and every
 // block of the plain lookup: four query pixels, one per wave (pixel (blockIdx - nblocks)*4 + wave)
-template <int R, int LMAX, bool F1>
+// SCAL: the window tests as scalar intervals (fewer VALU, more SALU per wave) for grids of
+// at most two resident rounds, where a wave's latency sets the time; larger grids run the
+// VALU form, since at 8 waves per SIMD the scalar unit becomes the limit (see below).
+template <int R, int LMAX, bool F1, bool SCAL = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void corr_lookup_kernel(LookupArgs a,
                                                                                                  FlowConvArgs f) {
   __shared__ __attribute__((aligned(16))) float patch[4][16 * patch_rs<LMAX>()];
@@ -668,31 +672,64 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
   const int ix = lane - l * RD;
   const f32x4 prm = a.prm[l];
   f32x4 v[LMAX];
+  // The window geometry is wave-uniform and comes from ONE float floor per axis:
+  // floor(x / 2^k) = floor(floor(x) / 2^k) = floor(x) >> k, and x * 2^-k is exact, so every
+  // level's window origin is an integer shift of level 0's (the same tiles as flooring
+  // x * 2^-k per level; coords beyond the int range put both windows far off every map).
+  // The per-level shifts then run on the SALU instead of four float floors + converts per
+  // axis on the VALU.  (The builtin, not an inline-asm v_readfirstlane: issued right behind
+  // the v_cvt that wrote its operand, the asm version read a stale value on gfx950 -- the
+  // hazard recognizer does not look into asm -- and fetched wrong tiles.)
+  const int xf = __builtin_amdgcn_readfirstlane((int)floorf(x));
+  const int yf = __builtin_amdgcn_readfirstlane((int)floorf(y));
 #pragma unroll
   for (int k = 0; k < LMAX; ++k) {
-    const float s = 1.0f / (float)(1 << k);  // coords / 2**k (exact power-of-two scaling)
-    // the window geometry is wave-uniform: kept in SGPRs (SALU), not recomputed per lane.
-    // (The builtin, not an inline-asm v_readfirstlane: issued right behind the v_cvt that
-    // wrote its operand, the asm version read a stale value on gfx950 -- the hazard
-    // recognizer does not look into asm -- and fetched wrong tiles.)
-    const int x0 = __builtin_amdgcn_readfirstlane((int)floorf(x * s)) - R;
-    const int y0 = __builtin_amdgcn_readfirstlane((int)floorf(y * s)) - R;
+    const int x0 = (xf >> k) - R;
+    const int y0 = (yf >> k) - R;
     const int tyo = y0 >> 2, txo = x0 >> 2;  // arithmetic shift = floor division by 4 (negative too)
     const int ntx = ((x0 + WD - 1) >> 2) - txo + 1;  // tile columns the window needs (3 or 4)
     const Level& lv = a.lv[k];
-    const int ty = tyo + ti, tx = txo + tj;
-    // only tile rows inside the window's WD rows are fetched (that also bounds the tile
-    // row count), only the window's tile columns, only tiles on the map
-    const bool ok = (k < a.L) & valid & (tj < ntx) & ((unsigned)(lrow + (tyo * 4 - y0)) < (unsigned)WD) &
-                    ((unsigned)ty < (unsigned)lv.th) & ((unsigned)tx < (unsigned)lv.tw);
-    // a raw buffer over this pixel's level map: lanes without a tile row to fetch pass an
-    // out-of-range offset and get zeros (the map's zero padding) without a memory access
-    const float* mapb = a.pyr + lv.off + (long)gpc * lv.mapsz;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(mapb), (short)0, (int)(lv.mapsz * 4), 0x00020000);
-    const unsigned off = ok ? ((__umul24((unsigned)ty, (unsigned)lv.tw) + (unsigned)tx) * 64u + (unsigned)(rr * 16)) : 0x80000000u;
+    __amdgpu_buffer_rsrc_t rs;
+    unsigned off;
+    if constexpr (SCAL) {
+      // Fetched: the rows of the window's WD rows that lie on the map's tile rows, the
+      // window's tile columns that lie on the map -- two scalar intervals, so a lane's test is
+      // one subtract + one unsigned compare per axis: patch row lrow <-> map row tyo*4 + lrow
+      // in [max(y0, 0), min(y0 + WD, 4 th)); tile column tj <-> txo + tj in
+      // [max(txo, 0), min(txo + ntx, tw)).  (The interval origins through readfirstlane: one
+      // SGPR each, so the test is not re-associated into two VALU adds.)
+      const int rlo = max(y0, 0), rhi = min(y0 + WD, 4 * lv.th);
+      const int clo = max(txo, 0), chi = min(txo + ntx, lv.tw);
+      const int rb = __builtin_amdgcn_readfirstlane(rlo - 4 * tyo), cb = __builtin_amdgcn_readfirstlane(clo - txo);
+      const bool ok = (k < a.L) & valid & ((unsigned)(lrow - rb) < (unsigned)max(rhi - rlo, 0)) &
+                      ((unsigned)(tj - cb) < (unsigned)max(chi - clo, 0));
+      // a raw buffer whose base is the window's first tile (tile (tyo, txo) of this pixel's
+      // level map; before the map's start when the window hangs over its top or left edge): a
+      // lane's byte offset is (ti tw + tj) 64 + 16 rr = ti (64 tw) + 16 (lane & 15); lanes
+      // without a tile row to fetch pass an offset above num_records (zeros, no access; the
+      // fetched lanes' offsets lie in the map by the tests above)
+      const float* wb = a.pyr + lv.off + (long)((unsigned long long)(unsigned)gpc * (unsigned)lv.mapsz) +
+                        ((long)tyo * lv.tw + txo) * 16;
+      rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wb), (short)0, 0x7FFFFFFF, 0x00020000);
+      off = ok ? __umul24((unsigned)ti, (unsigned)(64 * lv.tw)) + 16u * (unsigned)(lane & 15) : 0x80000000u;
+    } else {
+      const int ty = tyo + ti, tx = txo + tj;
+      // only tile rows inside the window's WD rows are fetched (that also bounds the tile
+      // row count), only the window's tile columns, only tiles on the map.  (These tests stay
+      // on the VALU: at 8 waves per SIMD the scalar unit is the other limit -- moving them to
+      // scalar interval bounds cut VALU 290 -> 271 per wave but raised SALU 328 -> 406, and B=8
+      // ran 8 % slower.)
+      const bool ok = (k < a.L) & valid & (tj < ntx) & ((unsigned)(lrow + (tyo * 4 - y0)) < (unsigned)WD) &
+                      ((unsigned)ty < (unsigned)lv.th) & ((unsigned)tx < (unsigned)lv.tw);
+      // a raw buffer over this pixel's level map: lanes without a tile row to fetch pass an
+      // out-of-range offset and get zeros (the map's zero padding) without a memory access.
+      // (The map offset as one 32 x 32 -> 64-bit scalar product: mapsz < 2^31.)
+      const float* mapb = a.pyr + lv.off + (long)((unsigned long long)(unsigned)gpc * (unsigned)lv.mapsz);
+      rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(mapb), (short)0, (int)(lv.mapsz * 4), 0x00020000);
+      off = ok ? ((__umul24((unsigned)ty, (unsigned)lv.tw) + (unsigned)tx) * 64u + (unsigned)(rr * 16)) : 0x80000000u;
+    }
 #ifdef LK_ABL_NOLOAD  // timing ablation (dev builds only): no tile loads
-    v[k] = f32x4{(float)off, (float)(long)mapb, 0.f, 0.f};
+    v[k] = f32x4{(float)off, 0.f, 0.f, 0.f};
 #else
     v[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
 #endif
@@ -709,12 +746,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
   {
     const float wm1 = prm[0], rw = prm[1], hm1 = prm[2], rh = prm[3];
     const float s = __builtin_ldexpf(1.0f, -l);
-    axis_entry<R>(x * s, ix, wm1, rw, xw, xt, xi);
+    axis_entry<R>(x * s, xf >> l, ix, wm1, rw, xw, xt, xi);
     int yi;
     float yt;
-    axis_entry<R>(y * s, ix, hm1, rh, yw, yt, yi);
-    // .x: the row's float offset in the patch (row * RS), or the negative OFF_PATCH / NAN_POS code
-    if (col) ytab[wv][lane] = int4{yw >= 0 ? yw * RS : yw, __float_as_int(yt), __float_as_int(1.0f - yt), yi};
+    axis_entry<R>(y * s, yf >> l, ix, hm1, rh, yw, yt, yi);
+    // .x: the row's byte offset in the patch (row * RS * 4), or the negative OFF_PATCH / NAN_POS code
+    if (col) ytab[wv][lane] = int4{yw >= 0 ? yw * RS * 4 : yw, __float_as_int(yt), __float_as_int(1.0f - yt), yi};
   }
   // (lanes that fetched nothing hold zeros from the out-of-range buffer load)
 #pragma unroll
@@ -738,16 +775,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
   // the common case: every entry of the wave is finite and on the patch
   if (__all(!col || (xw >= 0 && yw >= 0))) {
     if (col) {
-      const float* p0 = &patch[wv][pidx<LMAX>(0, xw, l)];
-      const float* p1 = &patch[wv][pidx<LMAX>(0, xw + 1, l)];
+      const char* p0 = reinterpret_cast<const char*>(&patch[wv][pidx<LMAX>(0, xw, l)]);
+      const char* p1 = reinterpret_cast<const char*>(&patch[wv][pidx<LMAX>(0, xw + 1, l)]);
+      auto at = [](const char* b, int byte) { return *reinterpret_cast<const float*>(b + byte); };
 #pragma unroll
       for (int iy = 0; iy < RD; ++iy) {
         const int4 ye = ytab[wv][l * RD + iy];
         const int ro = ye.x;
         const float ty = __int_as_float(ye.y), sS = __int_as_float(ye.z);
-        const float h0 = fmaf(p0[ro], ex, p1[ro] * xt);
-        const float h1 = fmaf(p0[ro + RS], ex, p1[ro + RS] * xt);
-        val[iy] = fmaf(sS, h0, ty * h1);
+        // (h0, h1) = the two rows' horizontal interpolations as one packed pair: each
+        // ds_read2 returns a column's two rows in consecutive registers, so the pair
+        // needs no repacking (v_pk_mul + v_pk_fma, the same roundings as two fmaf)
+        const f32x2 c0 = {at(p0, ro), at(p0, ro + 4 * RS)}, c1 = {at(p1, ro), at(p1, ro + 4 * RS)};
+        const f32x2 hh = __builtin_elementwise_fma(c0, (f32x2){ex, ex}, c1 * (f32x2){xt, xt});
+        val[iy] = fmaf(sS, hh.x, ty * hh.y);
       }
     }
   } else if (col) {
@@ -755,11 +796,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
 #pragma unroll
     for (int iy = 0; iy < RD; ++iy) {
       const int4 ye = ytab[wv][l * RD + iy];
-      const int yw2 = ye.x;  // row * RS, or a negative code
+      const int yw2 = ye.x;  // row * RS * 4 (bytes), or a negative code
       const float ty = __int_as_float(ye.y), sS = __int_as_float(ye.z);
       const bool on = (xw | yw2) >= 0;
       const bool nan = xw == NAN_POS || yw2 == NAN_POS;
-      const int r0 = on ? yw2 / RS : 0, c0 = on ? xw : 0;
+      const int r0 = on ? yw2 / (4 * RS) : 0, c0 = on ? xw : 0;
       const float* pl = &patch[wv][0];
       const float v = pl[pidx<LMAX>(r0, c0, l)] * (sS * ex) + pl[pidx<LMAX>(r0, c0 + 1, l)] * (sS * xt) +
                       pl[pidx<LMAX>(r0 + 1, c0, l)] * (ty * ex) + pl[pidx<LMAX>(r0 + 1, c0 + 1, l)] * (ty * xt);
@@ -1048,6 +1089,17 @@ int lookup_args(LookupArgs& a, const float* pyramid, int B, int H, int W, int L,
   a.range_flag = range_flag;
   return 0;
 }
+
+// The 4-level lookup: the scalar-interval form (SCAL) when the query pixels fill at most
+// two resident rounds of lookup waves (latency-bound: B=1 9.8 -> 9.0 us at config 2), the
+// VALU form beyond (scalar-unit-bound at full occupancy: B=8 44.7 vs 41-43 us).
+template <int RR, bool F1>
+void launch_lookup4(dim3 grid, hipStream_t s, const LookupArgs& a, const FlowConvArgs& f) {
+  if (RR == 4 && (long)a.B * a.H * a.W <= 16384)
+    hipLaunchKernelGGL((corr_lookup_kernel<RR, 4, F1, RR == 4>), grid, dim3(256), 0, s, a, f);
+  else
+    hipLaunchKernelGGL((corr_lookup_kernel<RR, 4, F1>), grid, dim3(256), 0, s, a, f);
+}
 }  // namespace
 
 extern "C" int raft_corr_lookup(const float* pyramid, int B, int H, int W, int L, int radius, const float* coords,
@@ -1068,7 +1120,7 @@ extern "C" int raft_corr_lookup(const float* pyramid, int B, int H, int W, int L
 #define RAFT_LOOKUP_CASE(RR)                                                           \
   case RR:                                                                             \
     if (L <= 4)                                                                        \
-      hipLaunchKernelGGL((corr_lookup_kernel<RR, 4, false>), grid, dim3(256), 0, s, a, FlowConvArgs{}); \
+      launch_lookup4<RR, false>(grid, s, a, FlowConvArgs{});                           \
     else                                                                               \
       hipLaunchKernelGGL((corr_lookup_kernel<RR, LK_MAXL, false>), grid, dim3(256), 0, s, a, FlowConvArgs{}); \
     break;
@@ -1139,7 +1191,7 @@ extern "C" int raft_corr_lookup_convf1(const float* pyramid, int B, int H, int W
 #define RAFT_LOOKUP_F1_CASE(RR)                                                                \
   case RR:                                                                                     \
     if (L <= 4)                                                                                \
-      hipLaunchKernelGGL((corr_lookup_kernel<RR, 4, true>), grid, dim3(256), 0, s, a, f);       \
+      launch_lookup4<RR, true>(grid, s, a, f);                                                 \
     else                                                                                       \
       hipLaunchKernelGGL((corr_lookup_kernel<RR, LK_MAXL, true>), grid, dim3(256), 0, s, a, f); \
     break;
