@@ -186,10 +186,11 @@ def test_lookup_far_out_of_bounds_and_large_coords():
     assert maxabs(cb(t(coords)), ref) < 2e-5
 
 
-@pytest.mark.parametrize("B,h,w", [(32, 16, 20), (33, 17, 21)])
+@pytest.mark.parametrize("B,h,w", [(32, 16, 20), (33, 17, 21), (50, 17, 21)])
 def test_lookup_pipelined_grid_vs_oracle(B, h, w):
     """Batches past one resident grid of the lookup (> 8 blocks per CU), a ragged pixel
-    count, coords spread over and beyond the maps."""
+    count, coords spread over and beyond the maps.  Up to 16384 query pixels the launch runs
+    the scalar-interval window form, beyond it the VALU form (B=50: 17850 pixels)."""
     from raft_optical_flow_amd import CorrBlock
     rng = np.random.default_rng(7)
     f1 = rng.standard_normal((B, 32, h, w)).astype(np.float32)
@@ -201,6 +202,27 @@ def test_lookup_pipelined_grid_vs_oracle(B, h, w):
     cb = CorrBlock(t(f1), t(f2), num_levels=4, radius=4)
     ref = O.corr_lookup(O.corr_pyramid(f1, f2, 4), coords, 4)
     assert maxabs(cb(t(coords)), ref) < 2e-5
+
+
+def test_lookup_window_forms_bit_equal():
+    """The two window-test forms of the lookup kernel (scalar intervals for <= 16384 query
+    pixels, per-lane VALU tests beyond) fetch the same tiles and share the tap arithmetic:
+    a B=80 launch (VALU form) equals B=40 launches of its halves (scalar form) bit for bit,
+    with windows hanging off every map edge, far outside, and on exact integers."""
+    from raft_optical_flow_amd import CorrBlock
+    rng = np.random.default_rng(12)
+    B, h, w = 80, 17, 21
+    f1 = rng.standard_normal((B, 32, h, w)).astype(np.float32)
+    f2 = rng.standard_normal((B, 32, h, w)).astype(np.float32)
+    ys, xs = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    grid = np.stack([xs, ys])[None].astype(np.float32)
+    coords = (grid + rng.normal(0, 4.0, (B, 2, h, w))).astype(np.float32)
+    coords[::7] = rng.uniform(-30, 50, (len(coords[::7]), 2, h, w)).astype(np.float32)
+    coords[3] = np.round(coords[3])
+    full = CorrBlock(t(f1), t(f2), num_levels=4, radius=4)(t(coords))
+    for s in (slice(0, 40), slice(40, 80)):
+        half = CorrBlock(t(f1[s]), t(f2[s]), num_levels=4, radius=4)(t(coords[s]))
+        assert torch.equal(full[s], half)
 
 
 def _lookup_convf1_case(B, h, w, r, prec, coord_scale=1.0, seed=11):
