@@ -22,8 +22,9 @@ def dur(r):
     return (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
 
 
-def is_lookup(r):
-    return "corr_lookup_kernel<4, 4, false>" in r["Kernel_Name"]
+def is_lookup(r):  # the lookup-only kernel, either window form (<4, 4, false> / <4, 4, false, SCAL>)
+    n = r["Kernel_Name"]
+    return "corr_lookup_kernel<4, 4, false>" in n or "corr_lookup_kernel<4, 4, false," in n
 
 
 # runs of consecutive lookup dispatches
@@ -54,7 +55,8 @@ for r in rows:
         in_fwd = True
     elif "flow_from_coords" in r["Kernel_Name"]:
         in_fwd = False
-    elif in_fwd and "corr_lookup_kernel<4, 4, true>" in r["Kernel_Name"]:
+    elif in_fwd and ("corr_lookup_kernel<4, 4, true>" in r["Kernel_Name"] or
+                     "corr_lookup_kernel<4, 4, true," in r["Kernel_Name"]):
         fz.append(dur(r))
 if fz:
     res["corr_lookup + convf1 B=1 in-forward"] = {"dispatches": len(fz), "mean_us": round(statistics.mean(fz), 3),
@@ -66,7 +68,7 @@ for r in rows:
         in_fwd, in_loop = True, False
     elif "flow_from_coords" in name:  # ... and ends (the bench's per-kernel replays come after)
         in_fwd = in_loop = False
-    elif in_fwd and ("corr_lookup_kernel<4, 4, true>" in name or
+    elif in_fwd and ("corr_lookup_kernel<4, 4, true" in name or
                      ("corr_lookup_kernel<4, 4" in name and int(r["Grid_Size_X"]) == 1760 * 256)):
         in_loop = True  # a B=1 lookup of the forward (lookup-only, or the lookup + convf1 launch)
     elif in_loop and "conv_halo_kernel<3, 3, 64, 1>" in name and int(r["Grid_Size_X"]) in (168 * 512, 224 * 512):
