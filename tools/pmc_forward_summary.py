@@ -60,7 +60,7 @@ hit = [c for k, c in passes["p4"][0] if k.startswith("corr_lookup")]
 P = B * 55 * 128
 alg_read, alg_write = P * (4 * 100 * 4 + 8), P * 4 * 81 * 4
 res = {
-    "kernel": "corr_lookup_kernel<4, 4, false>", "source_sha": sha("corr_pyramid.hip"), "shape_bhw": [B, 440, 1024],
+    "kernel": "corr_lookup_kernel<4, 4, false, SCAL> (B=1: the scalar-interval window form)", "source_sha": sha("corr_pyramid.hip"), "shape_bhw": [B, 440, 1024],
     "workload": f"bench.py config-2 forward, B={B}, 436x1024 padded to 440x1024, iters=32, f16x3; "
                 f"the {len(lk_f)} lookups of the last of two eager forwards (tools/pmc_forward.py)",
     "fetch_size_kib_raw_avg": statistics.mean(lk_f), "write_size_kib_raw_avg": statistics.mean(lk_w),
