@@ -199,12 +199,8 @@ __device__ __forceinline__ void split8(const f32x4 x0, const f32x4 x1, h8& hi, h
     lo = __builtin_bit_cast(h8, (__attribute__((ext_vector_type(4))) unsigned){lp[0], lp[1], lp[2], lp[3]});
 }
 
-// CW: MFMA (compute) waves per work-group.  4: one per SIMD, each 32 pixels x BNT columns.
-// 8 (BNT = 64 only): two per SIMD, wave w owning tile rows 2(w&3), 2(w&3)+1 x the 32 columns
-// (w>>2)*32 .. +31, so each SIMD interleaves two independent MFMA streams (one's LDS
-// fragment reads under the other's MFMAs); the loaders are waves CW .. CW+3 either way.
-template <int KH, int KW, int BNT, int PREC, int CW = 4>
-__global__ __launch_bounds__(CW * 64 + 256) void conv_halo_kernel(HaloLaunch hl) {
+template <int KH, int KW, int BNT, int PREC>
+__global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
   using C = HaloCfg<KH, KW, BNT>;
   constexpr int T = C::T, U = C::U, D = C::D, PW = C::PW, NPIX = C::NPIX, PI = C::PI, PA = C::PA, SB = C::SB;
   constexpr bool X3 = PREC == RAFT_PREC_F16X3;
@@ -219,8 +215,7 @@ __global__ __launch_bounds__(CW * 64 + 256) void conv_halo_kernel(HaloLaunch hl)
   constexpr int RPP = 1024 / WROW;             // rows per 1-KiB DMA piece
   constexpr int NBI = BNT / RPP;    // 1-KiB DMA pieces per weight block (one K-step)
   constexpr int NWP = U * NBI / 4;  // weight pieces per loader wave per load set
-  static_assert(CW == 4 || (CW == 8 && BNT == 64), "two MFMA waves per SIMD split a 64-column tile");
-  constexpr int NSUB = BNT / 32 / (CW / 4);  // 32-column MFMA subtiles per compute wave
+  constexpr int NSUB = BNT / 32;    // 32-column MFMA subtiles per compute wave
 
   // LSPLIT: the loaders stage each patch through registers and store it
   // pre-split (f16 hi | lo, the weight-row format), so the MFMA waves read
@@ -237,10 +232,8 @@ __global__ __launch_bounds__(CW * 64 + 256) void conv_halo_kernel(HaloLaunch hl)
 #endif
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool loader = w >= CW;  // waves CW .. CW+3 move the operands, waves 0 .. CW-1 compute
+  const bool loader = w >= 4;  // waves 4-7 move the operands, waves 0-3 compute
   const int lw = w & 3;
-  const int wr = w & 3;                      // a compute wave's tile-row pair (2wr, 2wr+1)
-  const int nc0 = CW == 8 ? (w >> 2) * 32 : 0;  // ... and its first column within the N-tile
 
   // tile (N fastest: an output tile's N-tiles share its input patch in L2)
   int q = xcd_tile(blockIdx.x, gridDim.x);
@@ -478,7 +471,7 @@ __global__ __launch_bounds__(CW * 64 + 256) void conv_halo_kernel(HaloLaunch hl)
 
   // ---- compute waves: fragments --------------------------------------------
   const int m = lane & 31, h = lane >> 5;
-  const int ppbase = (2 * wr + (m >> 4)) * PW + (m & 15);
+  const int ppbase = (2 * w + (m >> 4)) * PW + (m & 15);
   const int bsw = X3 ? (m >> 1) & 7 : (m >> 2) & 3;  // swizzle of weight row sb*32 + m
   f32x16 acc[NSUB], accx[NSUB];
 #pragma unroll
@@ -505,9 +498,9 @@ __global__ __launch_bounds__(CW * 64 + 256) void conv_halo_kernel(HaloLaunch hl)
     for (int sb = 0; sb < NSUB; ++sb) {
 #pragma unroll
       for (int qq = 0; qq < 2; ++qq) {
-        F.bh[sb][qq] = *reinterpret_cast<const h8*>(Bb + (nc0 + sb * 32 + m) * WROW + (((2 * h + qq) ^ bsw) << 4));
+        F.bh[sb][qq] = *reinterpret_cast<const h8*>(Bb + (sb * 32 + m) * WROW + (((2 * h + qq) ^ bsw) << 4));
         if constexpr (X3)
-          F.bl[sb][qq] = *reinterpret_cast<const h8*>(Bb + (nc0 + sb * 32 + m) * WROW + (((4 + 2 * h + qq) ^ bsw) << 4));
+          F.bl[sb][qq] = *reinterpret_cast<const h8*>(Bb + (sb * 32 + m) * WROW + (((4 + 2 * h + qq) ^ bsw) << 4));
       }
     }
     b_bs = b_bs + 1 == SB ? 0 : b_bs + 1;
@@ -590,12 +583,8 @@ __global__ __launch_bounds__(CW * 64 + 256) void conv_halo_kernel(HaloLaunch hl)
   // all in load sets s and s+1), then one barrier.  K-steps past nk (up to
   // U*ns) run on zero weights and zero patches: they add exact zeros, and the
   // loop body has no branches.
-  // (the prologue's weight pieces are split over waves 0-3 like the loaders'; with CW = 8,
-  // waves 4-7 issue none, and their counted wait below passes at once)
-  if (CW == 4 || w < 4) {
 #pragma unroll
-    for (int u = 0; u < D; ++u) issue_weights(u);
-  }
+  for (int u = 0; u < D; ++u) issue_weights(u);
   wait_vm<NWP * (D - 2)>();      // the weights of sets 0 and 1 (sets 2 .. D-1: before the first loop barrier)
   __builtin_amdgcn_s_barrier();  // load sets 0 and 1 have landed
 #ifdef HALO_PRIO
@@ -666,11 +655,11 @@ __global__ __launch_bounds__(CW * 64 + 256) void conv_halo_kernel(HaloLaunch hl)
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int mm = (r & 3) + 8 * (r >> 2) + 4 * h;
-    const int y = y0 + 2 * wr + (mm >> 4), x = x0 + (mm & 15);
+    const int y = y0 + 2 * w + (mm >> 4), x = x0 + (mm & 15);
     rows[r] = (y < p.out_h && x < p.out_w) ? (b * p.out_h + y) * p.out_w + x : -1;
   }
 #pragma unroll
-  for (int sb = 0; sb < NSUB; ++sb) tile_epilogue(p, rows, n0 + nc0 + sb * 32 + m, acc[sb]);
+  for (int sb = 0; sb < NSUB; ++sb) tile_epilogue(p, rows, n0 + sb * 32 + m, acc[sb]);
 #ifdef STAMPS
   {
     const unsigned long long c_exit = hstamp_now(), r_exit = hstamp_real();
@@ -689,19 +678,9 @@ __global__ __launch_bounds__(CW * 64 + 256) void conv_halo_kernel(HaloLaunch hl)
 #endif
 }
 
-bool halo_cw8() {  // two MFMA waves per SIMD for the 64-column tiles (RAFT_HALO_CW8=1; default one)
-  static const bool on = [] {
-    const char* e = getenv("RAFT_HALO_CW8");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
 template <int KH, int KW, int PREC>
 void launch_halo_p(const HaloLaunch& l, int bn, dim3 grid, hipStream_t s) {
-  if (bn == 64 && halo_cw8())
-    hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 64, PREC, 8>), grid, dim3(768), 0, s, l);
-  else if (bn == 64)
+  if (bn == 64)
     hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 64, PREC>), grid, dim3(512), 0, s, l);
   else
     hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 32, PREC>), grid, dim3(512), 0, s, l);
