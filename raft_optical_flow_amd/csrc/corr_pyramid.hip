@@ -405,6 +405,9 @@ struct LookupArgs {
   float wm1[LK_MAXL], hm1[LK_MAXL], rw[LK_MAXL], rh[LK_MAXL];
   // the same per level as {W-1, 1/(W-1), H-1, 1/(H-1)}: one 16-B per-lane load (lane-varying level)
   f32x4 prm[LK_MAXL];
+  // pyr + lv[l].off: each level's base, so a wave's per-level map address is one 32x32-bit
+  // product and one 64-bit add on the scalar unit (the scalar unit is a co-limit at B=8)
+  const float* lbase[LK_MAXL];
 };
 
 __device__ __forceinline__ void load_coords(const float* c, int layout, int b, int p, int P, float& x, float& y) {
@@ -641,14 +644,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
   const int gp = bid * 4 + wv;
   const bool valid = gp < a.B * P;
   const int gpc = valid ? gp : 0;
-  const int b = gpc / P;
-  const int p = gpc - b * P;
+  // (b, p) by a division only where a layout needs them: the forward's NHWC coords and
+  // outputs index by gpc alone, and a division is ~30 instructions on the scalar unit,
+  // which at B=8 is a co-limit of this kernel
+  auto bp = [&](int& b, int& p) {
+    b = gpc / P;
+    p = gpc - b * P;
+  };
   float x = 0.f, y = 0.f;
 #ifdef LK_STAMPS
   const unsigned long long lk_r0 = lk_clock(true);
 #endif
   LK_STAMP(0);
-  load_coords(a.coords, a.coords_layout, b, p, P, x, y);
+  if (a.coords_layout == 0) {
+    x = a.coords[2L * gpc];
+    y = a.coords[2L * gpc + 1];
+  } else {
+    int b, p;
+    bp(b, p);
+    load_coords(a.coords, a.coords_layout, b, p, P, x, y);
+  }
 #ifdef LK_STAMPS
   asm volatile("" ::"v"(x), "v"(y));
 #endif
@@ -708,7 +723,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
       // lane's byte offset is (ti tw + tj) 64 + 16 rr = ti (64 tw) + 16 (lane & 15); lanes
       // without a tile row to fetch pass an offset above num_records (zeros, no access; the
       // fetched lanes' offsets lie in the map by the tests above)
-      const float* wb = a.pyr + lv.off + (long)((unsigned long long)(unsigned)gpc * (unsigned)lv.mapsz) +
+      const float* wb = a.lbase[k] + (long)((unsigned long long)(unsigned)gpc * (unsigned)lv.mapsz) +
                         ((long)tyo * lv.tw + txo) * 16;
       rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wb), (short)0, 0x7FFFFFFF, 0x00020000);
       off = ok ? __umul24((unsigned)ti, (unsigned)(64 * lv.tw)) + 16u * (unsigned)(lane & 15) : 0x80000000u;
@@ -724,7 +739,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
       // a raw buffer over this pixel's level map: lanes without a tile row to fetch pass an
       // out-of-range offset and get zeros (the map's zero padding) without a memory access.
       // (The map offset as one 32 x 32 -> 64-bit scalar product: mapsz < 2^31.)
-      const float* mapb = a.pyr + lv.off + (long)((unsigned long long)(unsigned)gpc * (unsigned)lv.mapsz);
+      const float* mapb = a.lbase[k] + (long)((unsigned long long)(unsigned)gpc * (unsigned)lv.mapsz);
       rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(mapb), (short)0, (int)(lv.mapsz * 4), 0x00020000);
       off = ok ? ((__umul24((unsigned)ty, (unsigned)lv.tw) + (unsigned)tx) * 64u + (unsigned)(rr * 16)) : 0x80000000u;
     }
@@ -856,6 +871,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
     for (int j = 4 * lane; j < ntap; j += 256)
       *reinterpret_cast<f32x4*>(orow + j) = *reinterpret_cast<const f32x4*>(st + j);
   } else if (col) {
+    int b, p;
+    bp(b, p);
     float* orow = a.out_layout == 0 ? a.out + (long)gp * a.out_ld + cbase
                                     : a.out + ((long)b * ntap + cbase) * P + p;
     const long ostep = a.out_layout == 0 ? 1 : P;
@@ -863,6 +880,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
     for (int iy = 0; iy < RD; ++iy) orow[iy * ostep] = val[iy];
   }
   if (a.flow && lane < 2) {
+    int b, p;
+    bp(b, p);
     const float g = lane == 0 ? (float)(p % a.W) : (float)(p / a.W);
     a.flow[(long)gp * a.flow_ld + lane] = (lane == 0 ? x : y) - g;
   }
@@ -1074,6 +1093,7 @@ int lookup_args(LookupArgs& a, const float* pyramid, int B, int H, int W, int L,
     a.prm[l] = f32x4{a.wm1[l], a.rw[l], a.hm1[l], a.rh[l]};
   }
   a.pyr = pyramid;
+  for (int l = 0; l < LK_MAXL; ++l) a.lbase[l] = pyramid + a.lv[l].off;
   a.B = B;
   a.H = H;
   a.W = W;
