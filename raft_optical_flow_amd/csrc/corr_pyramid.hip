@@ -311,32 +311,43 @@ __global__ __launch_bounds__(512, 2) void corr_build2_kernel(CorrBuildArgs a) {
     }
   }
   __syncthreads();
-  // level 0: tiles (2by + ti, 4bx + tj); the four tiles of a tile row are adjacent (256 B)
-  for (int idx = tid; idx < CB2_BM * 128; idx += 512) {
-    const int row = idx >> 7, o = idx & 127;
+  // level 0: tiles (2by + ti, 4bx + tj); the four tiles of a tile row are adjacent (256 B).
+  // One 16-B store per lane: a tile row's 4 floats (e = 4 tr .. 4 tr + 3) are 4 consecutive
+  // columns of the LDS tile (16-B aligned in the pyramid: offsets are multiples of 4 floats)
+  for (int idx = tid; idx < CB2_BM * 32; idx += 512) {
+    const int row = idx >> 5, o = (idx & 31) * 4;
     const int p1 = m0 + row;
     const int ti = o >> 6, tj = (o >> 4) & 3, e = o & 15;
     const int ty = 2 * by + ti, tx = 4 * bx + tj;
     if (p1 < a.P && ty < a.l0.th && tx < a.l0.tw) {
-      const int n = (ti * 4 + (e >> 2)) * 16 + tj * 4 + (e & 3);
-      a.pyr[a.l0.off + ((long)b * a.P + p1) * a.l0.mapsz + ((long)ty * a.l0.tw + tx) * 16 + e] = T[row * CB2_TLD + n];
+      const float* t = T + row * CB2_TLD + (ti * 4 + (e >> 2)) * 16 + tj * 4;
+      *reinterpret_cast<f32x4*>(a.pyr + a.l0.off + ((long)b * a.P + p1) * a.l0.mapsz + ((long)ty * a.l0.tw + tx) * 16 +
+                                e) = f32x4{t[0], t[1], t[2], t[3]};
     }
   }
   if (a.has_l1 && by < a.l1.th) {
-    // level 1: the block pooled 2x2 -> level-1 tiles (by, 2bx + tj), zeros beyond H1 x W1
-    for (int idx = tid; idx < CB2_BM * 32; idx += 512) {
-      const int row = idx >> 5, o = idx & 31;
+    // level 1: the block pooled 2x2 -> level-1 tiles (by, 2bx + tj), zeros beyond H1 x W1;
+    // one 16-B store per lane (a level-1 tile row)
+    for (int idx = tid; idx < CB2_BM * 8; idx += 512) {
+      const int row = idx >> 3, o = (idx & 7) * 4;
       const int p1 = m0 + row;
       const int tj = o >> 4, e = o & 15;
       const int tx1 = 2 * bx + tj;
       if (p1 >= a.P || tx1 >= a.l1.tw) continue;
-      const int yy = e >> 2, xx = tj * 4 + (e & 3);
-      float v = 0.f;
-      if (by * 4 + yy < a.l1.h && bx * 8 + xx < a.l1.w) {
-        const float* t = T + row * CB2_TLD + (2 * yy) * 16 + 2 * xx;
-        v = (((t[0] + t[1]) + t[16]) + t[17]) / 4.0f;  // avg_pool2d window order
+      const int yy = e >> 2;
+      f32x4 v4;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int xx = tj * 4 + c;
+        float v = 0.f;
+        if (by * 4 + yy < a.l1.h && bx * 8 + xx < a.l1.w) {
+          const float* t = T + row * CB2_TLD + (2 * yy) * 16 + 2 * xx;
+          v = (((t[0] + t[1]) + t[16]) + t[17]) / 4.0f;  // avg_pool2d window order
+        }
+        v4[c] = v;
       }
-      a.pyr[a.l1.off + ((long)b * a.P + p1) * a.l1.mapsz + ((long)by * a.l1.tw + tx1) * 16 + e] = v;
+      *reinterpret_cast<f32x4*>(a.pyr + a.l1.off + ((long)b * a.P + p1) * a.l1.mapsz + ((long)by * a.l1.tw + tx1) * 16 +
+                                e) = v4;
     }
   }
 }
@@ -1035,7 +1046,7 @@ extern "C" int raft_corr_build_prec(const float* fmap1, const float* fmap2, int 
   if (precision == RAFT_PREC_FP32) {
     dim3 grid(cdiv((int)P, CB_BM), cdiv(H, 8) * a.nbx, B);
     hipLaunchKernelGGL(corr_build_kernel<false>, grid, dim3(256), 0, s, a);
-  } else if (big) {
+  } else if (big && ((uintptr_t)pyramid & 15) == 0) {  // 16-B epilogue stores: an aligned pyramid
     dim3 grid(cdiv((int)P, CB2_BM), cdiv(H, 8) * cdiv(W, 16), B);
     hipLaunchKernelGGL(corr_build2_kernel, grid, dim3(512), 0, s, a);
   } else {
