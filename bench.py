@@ -11,22 +11,28 @@ GPUs with no data-path collective; weights are broadcast once over RCCL), so
 scaling is weak.  Rank 0 prints one JSON line.
 
 The line also carries
-  roofline      the corr-lookup kernel (the metric's "corr-lookup GB/s vs HBM
-                peak"): algorithmic bytes P*2904 per pair-iteration / its average
-                duration INSIDE the forward (HIP event pairs on its stream around each
-                of the 32 lookups of an eagerly enqueued forward); `traffic` = HBM
-                bytes per launch from the committed in-forward PMC summary
-                (profiles/r02_lookup_pmc.json, used only while corr_pyramid.hip is the
-                source it was taken on); with --alternate-corr (config 3) the
-                on-the-fly lookup's per-level launches against the fp32 VALU peak
-                (2*P*L*(2r+2)^2*C flops per iteration);
-  lookup_b8     the same kernel in a B=8 forward of the same geometry (SURVEY 8(d):
-                where the >=50% target is quoted; its own 2.2 GB pyramid and coords);
+  roofline      the forward's own lookup launch (the metric's "corr-lookup GB/s vs HBM
+                peak"): with the all-pairs RAFT-full loop that is raft_corr_lookup_conv
+                (the window lookup fused with the motion encoder's convc1 and convf1:
+                the 324-channel correlation rows never leave the CU), HBM-bound:
+                algorithmic bytes per pair-iteration = P * (L*(2r+2)^2*4 window reads +
+                8 coords + 4*(256 + 128) convc1 / convf1 outputs + 8 flow) over its
+                average duration IN the forward (HIP event pairs on the launch stream
+                around each of the 32 launches of an eagerly enqueued forward; the
+                rocprofv3 per-dispatch mean of the same kernel is committed under
+                profiles/); without the fused launch (fp32 mode) the lookup-only kernel
+                with SURVEY 8(d)'s P*2904 B; `traffic` = HBM bytes per launch from a
+                committed in-forward PMC summary taken on the current kernel source;
+                with --alternate-corr (config 3) the on-the-fly lookup against its peak;
+  lookup_b1, lookup_b8  the standalone lookup kernel (raft_corr_lookup, what CorrBlock.__call__
+                runs) at B=1 and B=8 (where the >=50% target is quoted),
+                cache-cold over rotating pyramids, P*2904 B per launch;
+  iteration     one refinement iteration's launches (lookup launch + update convs), replayed;
   update_gemm   the update block's main-stream convolutions of one iteration, timed
-                in-forward (MFMA-bound; fp32-equivalent peak per conv arithmetic:
+                as a replayed graph (MFMA-bound; fp32-equivalent peak per conv arithmetic:
                 f32 MFMA 157.3 TF, f16x3 = f16 MFMA / 3, f16 / bf16 2.5 PF);
   dominant_kernel  the step's dominant kernel, conv_halo_kernel<3,3,64> (convc2 and
-                the flow-head conv1), in-forward, with its committed MFMA-busy PMC
+                the flow-head conv1), with its committed MFMA-busy PMC
                 (profiles/r02_halo_pmc.json) while conv_halo.hip is unchanged;
   fp32_exact    with the default f16x3 conv arithmetic: the same run with exact
                 f32 MFMA convs (value, ms_per_step), rank 0, N = 1;
@@ -68,6 +74,38 @@ def alt_lookup_flops(P, levels=4, r=4, C=256):
     """alternate-corr lookup, 2*P*L*(2r+2)^2*C flops per iteration (the reference's
     integer-tap inner products, correlation_kernel.cu:43-114)."""
     return 2 * P * levels * (2 * r + 2) ** 2 * C
+
+
+def fused_lookup_bytes_per_pixel(levels=4, r=4, c1=256, f1=128):
+    """raft_corr_lookup_conv per query pixel: L*(2r+2)^2*4 window reads + 8 B coords + the convc1 and
+    convf1 output rows (4*(c1 + f1) B) + the 8-B flow row; the correlation rows stay in LDS."""
+    return levels * (2 * r + 2) ** 2 * 4 + 8 + 4 * (c1 + f1) + 8
+
+
+def inforward_launch_us(plan, name):
+    """Mean duration of the launches called `name` inside one eagerly enqueued forward of `plan`:
+    HIP event pairs on the launch stream around each such launch (the other launches run as in
+    the forward, so caches are in the forward's state)."""
+    from raft_optical_flow_amd import kernels as K
+    main = torch.cuda.current_stream()
+    side = plan.side_stream or torch.cuda.Stream(device=plan.device)
+    pairs = []
+    torch.cuda.synchronize()
+    for l in plan.launches:
+        if l is K.FORK:
+            side.wait_stream(main)
+        elif l is K.JOIN:
+            main.wait_stream(side)
+        elif not l.side and l.name == name:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(main)
+            l(main.cuda_stream)
+            b.record(main)
+            pairs.append((a, b))
+        else:
+            l(side.cuda_stream if l.side else main.cuda_stream)
+    torch.cuda.synchronize()
+    return sum(a.elapsed_time(b) for a, b in pairs) / len(pairs) * 1e3, len(pairs)
 
 
 def time_kernel_events(fn, reps):
@@ -280,19 +318,41 @@ def main():
     h8, w8 = H // 8, W // 8
     P = args.batch * h8 * w8
     pu = plan.pk.update
+    roof, lookup_b1 = None, None
     if not args.alternate_corr:
         # 16 pyramids: 16 x 28 MB of windows per rotation at B=1 (> the 256 MiB Infinity Cache)
-        roof = rotated_lookup(plan, args.batch, h8, w8, nrot=max(3, -(-16 // args.batch)), reps=4)
+        lookup_b1 = rotated_lookup(plan, args.batch, h8, w8, nrot=max(3, -(-16 // args.batch)), reps=4)
         pmc = load_pmc("r02_lookup_pmc.json", "corr_pyramid.hip")
         # the committed PMC pass is of config 2 (B=1, 440x1024) on the current kernel source
-        roof["traffic"] = pmc["hbm_bytes_per_launch"] if pmc and [args.batch, H, W] == pmc["shape_bhw"] else None
+        lookup_b1["traffic"] = (pmc["hbm_bytes_per_launch"] if pmc and [args.batch, H, W] == pmc["shape_bhw"]
+                                else None)
+        names = [getattr(l, "name", "") for l in plan.launches]
+        L_, r_ = plan.pk.levels, plan.pk.radius
+        if "raft_corr_lookup_conv" in names:
+            us, n = inforward_launch_us(plan, "raft_corr_lookup_conv")
+            alg = P * fused_lookup_bytes_per_pixel(L_, r_, pu.convc1.n, pu.convf1.n)
+            kname = "lookup_conv_kernel (raft_corr_lookup_conv: window lookup + convc1 + convf1, one launch)"
+            src = "lookup_conv.hip"
+        else:
+            lname = "raft_corr_lookup_convf1" if "raft_corr_lookup_convf1" in names else "raft_corr_lookup"
+            us, n = inforward_launch_us(plan, lname)
+            alg = P * lookup_bytes_per_pixel(L_, r_)
+            kname = f"corr_lookup_kernel ({lname})"
+            src = "corr_pyramid.hip"
+        roof = {"kernel": kname, "batch": args.batch, "bound": "hbm", "achieved": round(alg / us / 1e3, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / us / 1e3 / HBM_PEAK_GBS, 4),
+                "algorithmic_bytes_per_launch": alg, "launch_us": round(us, 2),
+                "timing": f"HIP event pairs around each of the {n} launches of an eagerly enqueued forward"}
+        fpmc = load_pmc("r03_lookup_conv_pmc.json", src)
+        roof["traffic"] = (fpmc["hbm_bytes_per_launch"] if fpmc and [args.batch, H, W] == fpmc["shape_bhw"]
+                           else None)
         if roof["traffic"] is not None:
-            roof["traffic_source"] = "profiles/r02_lookup_pmc.json (in-forward FETCH_SIZE/WRITE_SIZE, calibrated)"
+            roof["traffic_source"] = "profiles/r03_lookup_conv_pmc.json (in-forward FETCH_SIZE/WRITE_SIZE)"
     else:
         # alternate corr: FP32 VALU-bound, 2*P*L*(2r+2)^2*C flops over the L per-level launches
         nl = plan.pk.levels
         lk = [l for l in plan.launches[plan.loop_start:plan.loop_end]
-              if getattr(l, "name", None) == "raft_alt_corr_lookup_levels"]
+              if getattr(l, "name", None) in ("raft_alt_corr_lookup_levels", "raft_alt_corr_lookup_levels_prec")]
         t_it = time_kernel_events(lambda: lk[0](K.stream_handle()), 20)
         fl = alt_lookup_flops(P, nl, plan.pk.radius, plan.pk.fdim)
         # RAFT (r = 4, C = 256) runs the MFMA tile kernel (csrc/alt_corr.hip, f16x3 box GEMM) unless
@@ -316,16 +376,14 @@ def main():
     # the update block's main-stream convolutions of one (non-final) iteration, replayed as a graph
     # (their operands are L2 / MALL-resident in the forward as well: 7 MB activations, <= 2 MB weights)
     lk_idx = [i for i, l in enumerate(plan.launches) if getattr(l, "name", "") in
-              ("raft_corr_lookup", "raft_corr_lookup_convf1", "raft_alt_corr_lookup_levels")]
-    if not args.alternate_corr and plan.launches[lk_idx[0]].name == "raft_corr_lookup_convf1":
-        # the forward's lookup launch also runs the motion encoder's convf1 (raft_hip.h): its
-        # duration beside the lookup-only kernel's (cache-warm replays of the last iteration's)
-        fl1 = plan.launches[lk_idx[-1]]
-        roof["forward_launch"] = {
-            "kernel": "corr_lookup_kernel<4,4,true> (raft_corr_lookup_convf1: lookup + convf1)",
-            "launch_us": round(time_kernel_events(lambda: fl1(K.stream_handle()), 50) * 1e6, 2),
-            "timing": "HIP events around a hipGraph of 50 replays of the last iteration's launch (cache-warm)"}
+              ("raft_corr_lookup", "raft_corr_lookup_convf1", "raft_corr_lookup_conv", "raft_alt_corr_lookup_levels",
+               "raft_alt_corr_lookup_levels_prec")]
     per_it = len(lk_idx) // args.iters
+    # one whole (non-final) iteration: its lookup launch and every update launch up to the next lookup
+    it_all = [l for l in plan.launches[lk_idx[per_it]:lk_idx[2 * per_it]] if not isinstance(l, str)]
+    t_it = time_kernel_events(lambda: [l(K.stream_handle()) for l in it_all], 20)
+    iteration = {"launches": len(it_all), "iteration_us": round(t_it * 1e6, 1),
+                 "timing": "HIP events around a hipGraph of 20 replays of one iteration's launches"}
     it_convs = [plan.launches[i] for i in range(lk_idx[per_it] + 1, lk_idx[2 * per_it])
                 if getattr(plan.launches[i], "name", "") in ("raft_conv2d", "raft_conv2d_pair")
                 and not plan.launches[i].side]
@@ -382,7 +440,9 @@ def main():
                                    f"{'eager' if args.no_graph else 'hipGraph'}",
                        "global_batch": world * args.batch, "parallelism": f"frame-pair sharding x{world}"},
             "roofline": roof,
+            "lookup_b1": lookup_b1,
             "lookup_b8": lookup_b8,
+            "iteration": iteration,
             "update_gemm": update_roof,
             "dominant_kernel": dominant,
             "fp32_exact": exact,

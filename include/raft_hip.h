@@ -21,6 +21,8 @@
  *   raft_corr_build         <- CorrBlock.__init__ + CorrBlock.corr (core/corr.py:25-54, 96-127)
  *   raft_corr_lookup        <- CorrBlock.__call__ + bilinear_sampler (core/corr.py:56-94,
  *                                                      core/utils/utils.py:57-71)
+ *   raft_corr_lookup_conv   <- corr_fn(coords1) + BasicMotionEncoder.convc1 / convf1
+ *                              (core/raft.py:219, core/update.py:185-205)
  *   raft_conv2d             <- nn.Conv2d + fused activations / GRU gates of
  *                              core/update.py:6-325 and core/extractor.py:6-267
  *   raft_instnorm_*         <- nn.InstanceNorm2d in core/extractor.py (norm_fn='instance')
@@ -41,7 +43,7 @@
 extern "C" {
 #endif
 
-#define RAFT_HIP_ABI_VERSION 10
+#define RAFT_HIP_ABI_VERSION 11
 
 /* Negative return codes (argument errors, raised before any launch). */
 #define RAFT_E_INVALID (-1)   /* bad size / null pointer / unsupported shape */
@@ -52,6 +54,10 @@ typedef void* raft_stream_t;  /* hipStream_t; NULL = the legacy default stream *
 int raft_hip_abi_version(void);
 const char* raft_hip_arch(void);        /* offload arch the library was built for ("gfx950") */
 const char* raft_hip_last_error(void);  /* message of the last failure on this thread ("" if none) */
+/* first 16 hex digits of the sha256 of the sources the library was built from (csrc/Makefile
+ * SRC_HASH: the .hip files in SRCS order, csrc/*.hpp, include/raft_hip.h); the Python loader
+ * refuses a library whose hash differs from the sources beside it (a stale prebuilt .so) */
+const char* raft_hip_source_hash(void);
 
 /* ---------------------------------------------------------------------------
  * All-pairs correlation pyramid (CorrBlock)
@@ -114,6 +120,33 @@ int raft_convf1_flow(const float* coords, int coords_layout, int B, int H, int W
                      const float* f1_bias, int f1_n, int f1_k, int f1_precision, float* f1_out, int f1_out_ld,
                      int* f1_range_flag, raft_stream_t stream);
 
+/* The lookup fused with the motion encoder's first convs (RAFT-full: radius 4, 4 levels), ONE
+ * launch per iteration of the all-pairs loop (core/corr.py:56-94 + core/update.py:185-205):
+ *   c1_out rows [B*H*W][c1_out_ld] = relu(convc1(corr) + c1_bias), convc1 = the 1x1 324 -> 256 conv
+ *   over the lookup's 324 channels (channel order of raft_corr_lookup), in c1_precision
+ *   (RAFT_PREC_F16X3 / F16 / BF16 arithmetic of raft_conv2d); the correlation rows never
+ *   leave the work-group (LDS), so they are not an output;
+ *   f1_out, flow_out: as raft_corr_lookup_convf1 (convf1: exact fp32, f1_n = 128, f1_k = 7).
+ * coords: NHWC [B*H*W][2], 16-B aligned.  c1_weight: raft_lookup_conv_pack_weight's output for
+ * the split form (raft_conv2d_split_weight_prec, c1_precision) of convc1's packed weight
+ * [256][352].  range_flag: raised by a lookup tap above RAFT_RANGE_LIMIT (the split convc1
+ * input); c1_range_flag / f1_range_flag: by the convc1 / convf1 outputs (split convc2 / convf2
+ * inputs).  Returns RAFT_E_INVALID for any other radius / level count / channel count (the
+ * caller then runs raft_corr_lookup_convf1 + raft_conv2d). */
+int raft_corr_lookup_conv(const float* pyramid, int B, int H, int W, int num_levels, int radius,
+                          const float* coords, float* flow_out, int flow_ld, int* range_flag,
+                          const void* c1_weight, const float* c1_bias, int c1_n, int c1_precision,
+                          float* c1_out, int c1_out_ld, int* c1_range_flag, const float* f1_weight,
+                          const float* f1_bias, int f1_n, int f1_k, int f1_precision, float* f1_out,
+                          int f1_out_ld, int* f1_range_flag, raft_stream_t stream);
+/* convc1's split weight [n_pad][k_pad] (k_pad % 32 == 0) -> raft_corr_lookup_conv's fragment order:
+ * [k_pad/32][n/32][4][64] x 16 B, element (j, s, t, lane) = 8 halves of split row 32s + lane%32,
+ * K-step j, quad (t/2)*4 + 2*(lane/32) + t%2; out holds raft_lookup_conv_weight_floats(n, k_pad)
+ * floats (16-B aligned). */
+size_t raft_lookup_conv_weight_floats(int n, int k_pad);
+int raft_lookup_conv_pack_weight(const void* split_weight, int n_pad, int k_pad, int n, void* out,
+                                 raft_stream_t stream);
+
 /* ---------------------------------------------------------------------------
  * On-the-fly ("alternate") correlation — the alt_cuda_corr plugin.
  *
@@ -127,6 +160,15 @@ int raft_convf1_flow(const float* coords, int coords_layout, int B, int H, int W
 int raft_alt_corr_forward(const float* fmap1, const float* fmap2, const float* coords, float* corr,
                           int B, int H1, int W1, int H2, int W2, int C, int N, int radius, float scale_div,
                           raft_stream_t stream);
+/* Arithmetic of the alternate lookups: RAFT_PREC_FP32 = exact fp32 products on the VALU (the
+ * reference kernel's arithmetic; raft_alt_corr_forward, the plugin's entry point, always uses
+ * it); any other value = the fp32-accurate f16x3 box GEMM on MFMA where it applies (r = 4,
+ * C % 32 == 0, C <= 256; exact only while |fmap| < 65504: the RAFT forward's range guard covers
+ * it), exact fp32 elsewhere.  raft_alt_corr_lookup_nhwc / raft_alt_corr_lookup_levels below
+ * are the _prec forms with RAFT_PREC_F16X3. */
+int raft_alt_corr_forward_prec(const float* fmap1, const float* fmap2, const float* coords, float* corr,
+                               int B, int H1, int W1, int H2, int W2, int C, int N, int radius, float scale_div,
+                               int precision, raft_stream_t stream);
 
 /* Same computation, NHWC output: out rows [B*H1*W1][out_ld] at channel
  * offset already applied by the caller; coords_layout as raft_corr_lookup
@@ -136,6 +178,10 @@ int raft_alt_corr_lookup_nhwc(const float* fmap1, const float* fmap2, const floa
                               float coord_div, float* out, int out_ld, int B, int H1, int W1, int H2, int W2,
                               int C, int radius, float scale_div, float* flow_out, int flow_ld,
                               int* range_flag, raft_stream_t stream);
+int raft_alt_corr_lookup_nhwc_prec(const float* fmap1, const float* fmap2, const float* coords, int coords_layout,
+                                   float coord_div, float* out, int out_ld, int B, int H1, int W1, int H2, int W2,
+                                   int C, int radius, float scale_div, float* flow_out, int flow_ld,
+                                   int* range_flag, int precision, raft_stream_t stream);
 /* All L levels of AlternateCorrBlock.__call__ (core/corr.py:163-198, the L calls of
  * alt_cuda_corr.forward of :176-186) as one call: level l reads fmap2_levels[l] (NHWC,
  * h2s[l] x w2s[l]) with the coordinates divided by 2^l and writes output channels
@@ -147,6 +193,11 @@ int raft_alt_corr_lookup_levels(const float* fmap1, const float* const* fmap2_le
                                 const int* w2s, int L, const float* coords, int coords_layout, float* out,
                                 int out_ld, int B, int H1, int W1, int C, int radius, float scale_div,
                                 float* flow_out, int flow_ld, int* range_flag, raft_stream_t stream);
+int raft_alt_corr_lookup_levels_prec(const float* fmap1, const float* const* fmap2_levels, const int* h2s,
+                                     const int* w2s, int L, const float* coords, int coords_layout, float* out,
+                                     int out_ld, int B, int H1, int W1, int C, int radius, float scale_div,
+                                     float* flow_out, int flow_ld, int* range_flag, int precision,
+                                     raft_stream_t stream);
 
 /* Gradients of raft_alt_corr_forward (unscaled), replacing correlation_kernel.cu:122-256:
  * every output is written (no pre-zeroing) and bit-identical run to run.  fmap1_grad is
@@ -155,7 +206,7 @@ int raft_alt_corr_lookup_levels(const float* fmap1, const float* const* fmap2_le
  * of the reference's float atomics; coords_grad is the true gradient through the bilinear
  * weights (the reference leaves it zero, correlation_kernel.cu:307).  workspace: at least
  * raft_alt_corr_backward_workspace_floats(...) floats, 256-byte aligned.  C % 4 == 0,
- * C <= 1024, radius <= 4. */
+ * C <= 1024, radius <= 32 (the forward's range). */
 int raft_alt_corr_backward(const float* fmap1, const float* fmap2, const float* coords, const float* corr_grad,
                            float* fmap1_grad, float* fmap2_grad, float* coords_grad,
                            int B, int H1, int W1, int H2, int W2, int C, int N, int radius,
@@ -257,7 +308,8 @@ int raft_conv2d(const raft_conv2d_params* p, raft_stream_t stream);
  * raft_conv2d(p1).  When both are halo-kernel convs of one shape class and precision, their
  * tiles run side by side in ONE launch: the pair fills CUs that either alone leaves idle at
  * one frame pair, with no second stream (a cross-stream fork/join costs a graph ~7 us per
- * edge on ROCm).  Otherwise, or when one reads what the other writes, the two run in order. */
+ * edge on ROCm).  Otherwise, or when one reads what the other writes, or both write a common
+ * element (column ranges of their output rows meet), the two run in order. */
 int raft_conv2d_pair(const raft_conv2d_params* p0, const raft_conv2d_params* p1, raft_stream_t stream);
 /* fp32 packed weight [n_pad][k_pad] -> split form for RAFT_PREC_F16X3 / F16:
  * per row and 32-wide K-step, 32 f16 hi then 32 f16 lo (lo scaled by 2048);
@@ -315,7 +367,9 @@ int raft_bilinear_sample(const float* img, const float* coords, float* out, floa
                          int Ho, int Wo, raft_stream_t stream);
 /* forward_interpolate: flow [B][2][H][W] -> out [B][2][H][W]; every grid point takes the flow of
  * the nearest (fp64 Euclidean) forward-moved point (x + dx, y + dy) strictly inside
- * (0, W) x (0, H); ties -> the lowest source index; no valid point -> 0. */
+ * (0, W) x (0, H); ties -> the lowest source index; no valid point -> 0.  An all-pairs search,
+ * for the 1/8-resolution flow of the warm start: H*W <= RAFT_FI_MAX_POINTS (else RAFT_E_INVALID). */
+#define RAFT_FI_MAX_POINTS 65536
 int raft_forward_interpolate(const float* flow, float* out, int B, int H, int W, raft_stream_t stream);
 
 #ifdef __cplusplus

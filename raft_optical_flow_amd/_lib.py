@@ -29,7 +29,7 @@ PREC_F16 = 2     # single f16 product (mixed precision)
 PREC_BF16 = 3    # single bf16 product on v_mfma_f32_32x32x16_bf16 (bf16 mixed precision)
 PRECISIONS = {"fp32": PREC_FP32, "f16x3": PREC_F16X3, "f16": PREC_F16, "bf16": PREC_BF16}
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 RANGE_LIMIT = 32768.0  # RAFT_RANGE_LIMIT: |x| above it raises the f16x3 range guard
 
 EPI_LINEAR = 0
@@ -69,6 +69,7 @@ _PROTOS = {
     "raft_hip_abi_version": (c_int, []),
     "raft_hip_arch": (c_char_p, []),
     "raft_hip_last_error": (c_char_p, []),
+    "raft_hip_source_hash": (c_char_p, []),
     "raft_corr_pyramid_floats": (c_size_t, [c_int, c_int, c_int, c_int]),
     "raft_corr_build": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, P, P]),
     "raft_corr_build_prec": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, P, P]),
@@ -77,7 +78,17 @@ _PROTOS = {
     "raft_corr_lookup_convf1": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, c_int, c_int, P, c_int, P,
                                         P, P, c_int, c_int, c_int, P, c_int, P, P]),
     "raft_convf1_flow": (c_int, [P, c_int, c_int, c_int, c_int, P, P, c_int, c_int, c_int, P, c_int, P, P]),
+    "raft_corr_lookup_conv": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P, c_int, P, P, P, c_int, c_int, P,
+                                      c_int, P, P, P, c_int, c_int, c_int, P, c_int, P, P]),
+    "raft_lookup_conv_weight_floats": (c_size_t, [c_int, c_int]),
+    "raft_lookup_conv_pack_weight": (c_int, [P, c_int, c_int, c_int, P, P]),
     "raft_alt_corr_forward": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, P]),
+    "raft_alt_corr_forward_prec": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
+                                           c_int, P]),
+    "raft_alt_corr_lookup_levels_prec": (c_int, [P, P, P, P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int,
+                                                 c_int, ctypes.c_float, P, c_int, P, c_int, P]),
+    "raft_alt_corr_lookup_nhwc_prec": (c_int, [P, P, P, c_int, c_float, P, c_int, c_int, c_int, c_int, c_int, c_int,
+                                               c_int, c_int, c_float, P, c_int, P, c_int, P]),
     "raft_alt_corr_lookup_levels": (c_int, [P, P, P, P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, c_int, c_int,
                                             ctypes.c_float, P, c_int, P, P]),
     "raft_alt_corr_lookup_nhwc": (c_int, [P, P, P, c_int, c_float, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
@@ -136,8 +147,32 @@ def load():
             fn.argtypes = args
         if lib.raft_hip_abi_version() != ABI_VERSION:
             raise RaftHipError("libraft_hip.so ABI version mismatch")
+        want = source_hash()
+        got = lib.raft_hip_source_hash().decode()
+        if want is not None and got != want and os.environ.get("RAFT_SKIP_SRC_CHECK", "0") != "1":
+            raise RaftHipError(f"{LIB_PATH} was built from other sources (hash {got}, the sources here hash "
+                               f"{want}): rebuild it with `python __graft_entry__.py build`")
         _lib = lib
         return lib
+
+
+def source_hash() -> str | None:
+    """sha256[:16] of the HIP sources beside this package, as csrc/Makefile bakes into the library
+    (raft_hip_source_hash); None when the sources are not present."""
+    import glob
+    import hashlib
+    csrc = os.path.join(_HERE, "csrc")
+    mk = os.path.join(csrc, "Makefile")
+    hdr = os.path.join(os.path.dirname(_HERE), "include", "raft_hip.h")
+    if not (os.path.exists(mk) and os.path.exists(hdr)):
+        return None
+    srcs = next(l.split(":=", 1)[1].split() for l in open(mk) if l.startswith("SRCS :="))
+    files = [os.path.join(csrc, f) for f in srcs] + sorted(glob.glob(os.path.join(csrc, "*.hpp"))) + [hdr]
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def check(rc: int, what: str):

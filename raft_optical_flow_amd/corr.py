@@ -117,6 +117,9 @@ class AlternateCorrBlock:
         div = K.sqrt_c(self.dim)
         levels = list(self._f2[: self.num_levels])
         ptrs, hs, ws = K.alt_levels_args(levels)
-        _lib.call("raft_alt_corr_lookup_levels", f1.data_ptr(), ptrs, hs, ws, len(levels), coords.data_ptr(), 1,
-                  out.data_ptr(), out.shape[1], b, h, w, self.dim, r, div, None, 0, None, s)
+        # exact fp32 products, as the reference's kernel (set .precision = "f16x3" for the
+        # fp32-accurate split-f16 box GEMM on MFMA)
+        prec = _lib.PRECISIONS[getattr(self, "precision", "fp32")]
+        _lib.call("raft_alt_corr_lookup_levels_prec", f1.data_ptr(), ptrs, hs, ws, len(levels), coords.data_ptr(), 1,
+                  out.data_ptr(), out.shape[1], b, h, w, self.dim, r, div, None, 0, None, prec, s)
         return K.rows_to_nchw(K.Rows(out), b, h, w)

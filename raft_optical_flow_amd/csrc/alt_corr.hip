@@ -36,6 +36,7 @@ struct AltArgs {
   float* flow;
   int flow_ld;
   int* range_flag;  // f16x3 range guard (raft_hip.h), or null
+  int prec;         // RAFT_PREC_FP32: exact fp32 (VALU kernels); otherwise the f16x3 box GEMM where it applies
 };
 
 // One tap's fmap2 row slice for this lane's channel quads, read through a raw
@@ -735,7 +736,7 @@ int launch_alt(const AltArgs& a, raft_stream_t stream) {
     const char* e = getenv("RAFT_ALT_MFMA");
     return !(e && e[0] == '0');
   }();
-  if (mfma && a.r == 4 && a.C % 32 == 0 && a.C <= 256) {
+  if (mfma && a.prec != RAFT_PREC_FP32 && a.r == 4 && a.C % 32 == 0 && a.C <= 256) {
     const long tiles = (long)a.B * a.N * cdiv_l(a.H1, AT) * cdiv_l(a.W1, AT);
     AltLevels lv{};
     lv.f2[0] = a.f2;
@@ -804,6 +805,14 @@ static int alt_checks(const float* f1, const float* f2, const float* coords, con
 extern "C" int raft_alt_corr_forward(const float* fmap1, const float* fmap2, const float* coords, float* corr, int B,
                                      int H1, int W1, int H2, int W2, int C, int N, int radius, float scale_div,
                                      raft_stream_t stream) {
+  // the plugin's contract is the reference kernel's exact fp32 arithmetic
+  return raft_alt_corr_forward_prec(fmap1, fmap2, coords, corr, B, H1, W1, H2, W2, C, N, radius, scale_div,
+                                    RAFT_PREC_FP32, stream);
+}
+
+extern "C" int raft_alt_corr_forward_prec(const float* fmap1, const float* fmap2, const float* coords, float* corr,
+                                          int B, int H1, int W1, int H2, int W2, int C, int N, int radius,
+                                          float scale_div, int precision, raft_stream_t stream) {
   int rc = alt_checks(fmap1, fmap2, coords, corr, B, H1, W1, H2, W2, C, N, radius);
   if (rc) return rc;
   AltArgs a;
@@ -827,6 +836,7 @@ extern "C" int raft_alt_corr_forward(const float* fmap1, const float* fmap2, con
   a.flow = nullptr;
   a.flow_ld = 0;
   a.range_flag = nullptr;
+  a.prec = precision;
   return launch_alt(a, stream);
 }
 
@@ -834,6 +844,15 @@ extern "C" int raft_alt_corr_lookup_nhwc(const float* fmap1, const float* fmap2,
                                          int coords_layout, float coord_div, float* out, int out_ld, int B, int H1,
                                          int W1, int H2, int W2, int C, int radius, float scale_div, float* flow_out,
                                          int flow_ld, int* range_flag, raft_stream_t stream) {
+  return raft_alt_corr_lookup_nhwc_prec(fmap1, fmap2, coords, coords_layout, coord_div, out, out_ld, B, H1, W1, H2, W2,
+                                        C, radius, scale_div, flow_out, flow_ld, range_flag, RAFT_PREC_F16X3, stream);
+}
+
+extern "C" int raft_alt_corr_lookup_nhwc_prec(const float* fmap1, const float* fmap2, const float* coords,
+                                              int coords_layout, float coord_div, float* out, int out_ld, int B,
+                                              int H1, int W1, int H2, int W2, int C, int radius, float scale_div,
+                                              float* flow_out, int flow_ld, int* range_flag, int precision,
+                                              raft_stream_t stream) {
   int rc = alt_checks(fmap1, fmap2, coords, out, B, H1, W1, H2, W2, C, 1, radius);
   if (rc) return rc;
   RAFT_REQUIRE(coords_layout == 0 || coords_layout == 1, "raft_alt_corr_lookup_nhwc: bad coords_layout");
@@ -860,6 +879,7 @@ extern "C" int raft_alt_corr_lookup_nhwc(const float* fmap1, const float* fmap2,
   a.flow = flow_out;
   a.flow_ld = flow_ld;
   a.range_flag = range_flag;
+  a.prec = precision;
   return launch_alt(a, stream);
 }
 
@@ -867,6 +887,16 @@ extern "C" int raft_alt_corr_lookup_levels(const float* fmap1, const float* cons
                                            const int* w2s, int L, const float* coords, int coords_layout, float* out,
                                            int out_ld, int B, int H1, int W1, int C, int radius, float scale_div,
                                            float* flow_out, int flow_ld, int* range_flag, raft_stream_t stream) {
+  return raft_alt_corr_lookup_levels_prec(fmap1, fmap2_levels, h2s, w2s, L, coords, coords_layout, out, out_ld, B, H1,
+                                          W1, C, radius, scale_div, flow_out, flow_ld, range_flag, RAFT_PREC_F16X3,
+                                          stream);
+}
+
+extern "C" int raft_alt_corr_lookup_levels_prec(const float* fmap1, const float* const* fmap2_levels, const int* h2s,
+                                                const int* w2s, int L, const float* coords, int coords_layout,
+                                                float* out, int out_ld, int B, int H1, int W1, int C, int radius,
+                                                float scale_div, float* flow_out, int flow_ld, int* range_flag,
+                                                int precision, raft_stream_t stream) {
   RAFT_REQUIRE(fmap2_levels && h2s && w2s && L >= 1 && L <= AM_MAXL,
                "raft_alt_corr_lookup_levels: need 1..%d levels", AM_MAXL);
   const int rd2 = (2 * radius + 1) * (2 * radius + 1);
@@ -880,12 +910,13 @@ extern "C" int raft_alt_corr_lookup_levels(const float* fmap1, const float* cons
     const char* e = getenv("RAFT_ALT_MFMA");
     return !(e && e[0] == '0');
   }();
-  if (!(mfma && radius == 4 && C % 32 == 0 && C <= 256)) {
-    // one launch per level (raft_alt_corr_lookup_nhwc; the flow is written with level 0)
+  if (!(mfma && precision != RAFT_PREC_FP32 && radius == 4 && C % 32 == 0 && C <= 256)) {
+    // one launch per level (raft_alt_corr_lookup_nhwc_prec; the flow is written with level 0)
     for (int l = 0; l < L; ++l) {
-      int rc = raft_alt_corr_lookup_nhwc(fmap1, fmap2_levels[l], coords, coords_layout, (float)(1 << l),
-                                         out + (long)l * rd2, out_ld, B, H1, W1, h2s[l], w2s[l], C, radius, scale_div,
-                                         l == 0 ? flow_out : nullptr, flow_ld, range_flag, stream);
+      int rc = raft_alt_corr_lookup_nhwc_prec(fmap1, fmap2_levels[l], coords, coords_layout, (float)(1 << l),
+                                              out + (long)l * rd2, out_ld, B, H1, W1, h2s[l], w2s[l], C, radius,
+                                              scale_div, l == 0 ? flow_out : nullptr, flow_ld, range_flag, precision,
+                                              stream);
       if (rc) return rc;
     }
     return 0;
@@ -911,6 +942,7 @@ extern "C" int raft_alt_corr_lookup_levels(const float* fmap1, const float* cons
   a.flow = flow_out;
   a.flow_ld = flow_ld;
   a.range_flag = range_flag;
+  a.prec = precision;
   AltLevels lv{};
   for (int l = 0; l < L; ++l) {
     lv.f2[l] = fmap2_levels[l];

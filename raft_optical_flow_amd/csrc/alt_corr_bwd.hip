@@ -50,19 +50,21 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-// one wave per (b, p); loops over the N coordinate sets of the query pixel
+// one wave per (b, p); loops over the N coordinate sets of the query pixel.  Dynamic LDS: per
+// wave the (2r+2)^2 tap sums and tap gradients (any radius; blocks of 4 waves while that fits
+// 64 KB, else of one wave: r <= 32 takes <= 35 KB per wave)
 __global__ __launch_bounds__(256) void alt_bwd_query_kernel(BwdArgs a) {
-  __shared__ float sbuf[4][128], gbuf[4][128];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  extern __shared__ float bwd_lds[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
   const int P1 = a.H1 * a.W1;
-  const long bp = (long)blockIdx.x * 4 + wv;
+  const long bp = (long)blockIdx.x * wpb + wv;
   if (bp >= (long)a.B * P1) return;
   const int b = (int)(bp / P1), p = (int)(bp - (long)b * P1);
   const int r = a.r, rd = 2 * r + 1, wd = 2 * r + 2, ntaps = wd * wd;
   const float* f1row = a.f1 + bp * a.C;
   const float* f2b = a.f2 + (long)b * a.H2 * a.W2 * a.C;
-  float* s = sbuf[wv];
-  float* gt = gbuf[wv];
+  float* s = bwd_lds + (long)wv * 2 * ntaps;
+  float* gt = s + ntaps;
   // fmap1 gradient accumulators: lane owns channels 4*lane + 256*k
   constexpr int KMAX = 4;  // C <= 1024
   f32x4 acc[KMAX];
@@ -238,7 +240,7 @@ using namespace raft;
 
 extern "C" size_t raft_alt_corr_backward_workspace_floats(int B, int H1, int W1, int H2, int W2, int C, int N,
                                                           int radius) {
-  if (B <= 0 || H1 <= 0 || W1 <= 0 || H2 <= 0 || W2 <= 0 || C <= 0 || N <= 0 || radius < 0 || radius > 4) return 0;
+  if (B <= 0 || H1 <= 0 || W1 <= 0 || H2 <= 0 || W2 <= 0 || C <= 0 || N <= 0 || radius < 0 || radius > 32) return 0;
   WsLayout w;
   if (ws_layout((long)B * N * H1 * W1, (2 * radius + 2) * (2 * radius + 2), w)) return 0;
   return (w.total_bytes + 3) / 4;
@@ -252,7 +254,7 @@ extern "C" int raft_alt_corr_backward(const float* fmap1, const float* fmap2, co
   RAFT_REQUIRE(fmap1_grad && fmap2_grad && coords_grad, "raft_alt_corr_backward: null gradient pointer");
   RAFT_REQUIRE(B > 0 && H1 > 0 && W1 > 0 && H2 > 0 && W2 > 0 && N > 0, "raft_alt_corr_backward: bad sizes");
   RAFT_REQUIRE(C > 0 && C % 4 == 0 && C <= 1024, "raft_alt_corr_backward: C must be a multiple of 4, <= 1024");
-  RAFT_REQUIRE(radius >= 0 && radius <= 4, "raft_alt_corr_backward: radius must be 0..4 (got %d)", radius);
+  RAFT_REQUIRE(radius >= 0 && radius <= 32, "raft_alt_corr_backward: radius must be 0..32 (got %d)", radius);
   RAFT_REQUIRE(((((uintptr_t)fmap1) | ((uintptr_t)fmap2) | ((uintptr_t)fmap1_grad) | ((uintptr_t)fmap2_grad)) & 15) == 0,
                "raft_alt_corr_backward: fmaps and their gradients must be 16-byte aligned");
   const int wd = 2 * radius + 2;
@@ -290,7 +292,10 @@ extern "C" int raft_alt_corr_backward(const float* fmap1, const float* fmap2, co
   a.ncell = (int)ncell;
   a.Q = Q;
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(alt_bwd_query_kernel, dim3((unsigned)cdiv_l((long)B * H1 * W1, 4)), dim3(256), 0, s, a);
+  const size_t wave_lds = (size_t)2 * wd * wd * sizeof(float);
+  const int wpb = 4 * wave_lds <= 65536 ? 4 : 1;
+  hipLaunchKernelGGL(alt_bwd_query_kernel, dim3((unsigned)cdiv_l((long)B * H1 * W1, wpb)), dim3(64 * wpb),
+                     wpb * wave_lds, s, a);
   rc = check_launch("raft_alt_corr_backward(query)");
   if (rc) return rc;
   size_t sb = w.sort_bytes;

@@ -159,7 +159,12 @@ extern "C" int raft_bilinear_sample(const float* img, const float* coords, float
 extern "C" int raft_forward_interpolate(const float* flow, float* out, int B, int H, int W, raft_stream_t stream) {
   RAFT_REQUIRE(flow && out && B > 0 && H > 0 && W > 0 && B < 65536, "raft_forward_interpolate: bad arguments");
   RAFT_REQUIRE(flow != out, "raft_forward_interpolate: in-place is not supported");
-  RAFT_REQUIRE((long)H * W < (1L << 30), "raft_forward_interpolate: too many pixels");
+  // the search is all-pairs (every target scans every source: (H W)^2 fp64 distances per image);
+  // the RAFT warm start runs it at 1/8 resolution (Sintel: 55 x 128 = 7040 points, 5e7 pairs).
+  // Beyond 2^16 points one launch would run for seconds (a GPU watchdog risk): refused.
+  RAFT_REQUIRE((long)H * W <= RAFT_FI_MAX_POINTS,
+               "raft_forward_interpolate: %d x %d = %ld points exceeds %d (the all-pairs nearest search is "
+               "meant for 1/8-resolution flow)", H, W, (long)H * W, RAFT_FI_MAX_POINTS);
   dim3 grid((unsigned)cdiv_l((long)H * W, FI_T), (unsigned)B);
   hipLaunchKernelGGL(forward_interpolate_kernel, grid, dim3(FI_T), 0, as_stream(stream), flow, out, H, W);
   return check_launch("raft_forward_interpolate");

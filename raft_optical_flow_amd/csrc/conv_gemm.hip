@@ -842,6 +842,31 @@ bool overlaps(const void* a, long ra, int lda, const void* b, long rb, int ldb) 
   row_range(b, rb, ldb, b0, b1);
   return a0 < b1 && b0 < a1;
 }
+// could a row of output a (na channels per row) and a row of output b (nb) share an element?
+// Same ld: only if their column ranges meet (b's first column taken modulo ld relative to a's
+// rows, a wrap into the next row included); other lds: whenever their byte ranges meet.
+bool columns_meet(const void* a, long ra, int lda, int na, const void* b, long rb, int ldb, int nb) {
+  if (!overlaps(a, ra, lda, b, rb, ldb)) return false;
+  if (lda != ldb) return true;
+  const long d = ((long)((intptr_t)b - (intptr_t)a)) / 4;
+  if (((intptr_t)b - (intptr_t)a) % 4) return true;
+  long c = d % lda;
+  if (c < 0) c += lda;  // b's first column in a's row coordinates
+  return c < na || c + nb > lda;
+}
+// do the two convs write a common element? (a write-write race inside one launch)
+bool writes_overlap(const raft_conv2d_params& x, const raft_conv2d_params& y) {
+  const long rx = (long)x.batch * x.out_h * x.out_w, ry = (long)y.batch * y.out_h * y.out_w;
+  // the channels each output pointer receives: out gets all n (or n - split with out1), out1 n - split
+  const void* xo[2] = {x.out, x.out1};
+  const int xl[2] = {x.out_ld, x.out1_ld}, xn[2] = {x.n, x.n};
+  const void* yo[2] = {y.out, y.out1};
+  const int yl[2] = {y.out_ld, y.out1_ld}, yn[2] = {y.n, y.n};
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j)
+      if (xo[i] && yo[j] && columns_meet(xo[i], rx, xl[i], xn[i], yo[j], ry, yl[j], yn[j])) return true;
+  return false;
+}
 // does conv y read anything conv x writes?
 bool reads_output_of(const raft_conv2d_params& y, const raft_conv2d_params& x) {
   const long rin = (long)y.batch * y.in_h * y.in_w, rout = (long)x.batch * x.out_h * x.out_w;
@@ -904,8 +929,9 @@ extern "C" int raft_conv2d_pair(const raft_conv2d_params* p0, const raft_conv2d_
   if (rc) return rc;
   rc = conv_prepare(p1, a1, o1);
   if (rc) return rc;
-  // one launch only when neither reads what the other writes (otherwise: in order, as two calls)
-  const bool independent = !reads_output_of(*p1, *p0) && !reads_output_of(*p0, *p1);
+  // one launch only when neither reads what the other writes and no element is written by both
+  // (otherwise: in order, as two calls)
+  const bool independent = !reads_output_of(*p1, *p0) && !reads_output_of(*p0, *p1) && !writes_overlap(*p0, *p1);
   if (independent && !small_n(*p0) && !small_n(*p1) && conv_halo_launch_pair(o0, o1, as_stream(stream)) == 0)
     return check_launch("raft_conv2d_pair(halo)");
   rc = raft_conv2d(p0, stream);

@@ -158,47 +158,6 @@ __device__ __forceinline__ void wait_vm_n(int n) {
   }
 }
 
-// x - f16 half of hpk, exact in fp32 (v_fma_mix: the f16 operand widened in the ALU)
-__device__ __forceinline__ float sub_half_lo(unsigned hpk, float x) {
-  float r;
-  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hpk), "v"(x));
-  return r;
-}
-__device__ __forceinline__ float sub_half_hi(unsigned hpk, float x) {
-  float r;
-  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hpk), "v"(x));
-  return r;
-}
-
-using f2 = __attribute__((ext_vector_type(2))) float;
-using h2 = __attribute__((ext_vector_type(2))) _Float16;
-
-// 8 floats -> 8 f16 hi (+ 8 f16 lo = f16(x - hi)) : 4 VALU per 2 elements;
-// BF: 8 bf16 (round to nearest even) in the f16 container, no lo
-template <bool LO, bool BF = false>
-__device__ __forceinline__ void split8(const f32x4 x0, const f32x4 x1, h8& hi, h8& lo) {
-  if constexpr (BF) {
-    const h4 a = to_bf16x4(x0), b = to_bf16x4(x1);
-    hi = h8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-    return;
-  }
-  const float v[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-  unsigned hp[4], lp[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const h2 h = __builtin_convertvector((f2){v[2 * e], v[2 * e + 1]}, h2);
-    hp[e] = __builtin_bit_cast(unsigned, h);
-    if constexpr (LO) {
-      const float d0 = sub_half_lo(hp[e], v[2 * e]);
-      const float d1 = sub_half_hi(hp[e], v[2 * e + 1]);
-      lp[e] = __builtin_bit_cast(unsigned, __builtin_convertvector((f2){d0, d1}, h2));
-    }
-  }
-  hi = __builtin_bit_cast(h8, (__attribute__((ext_vector_type(4))) unsigned){hp[0], hp[1], hp[2], hp[3]});
-  if constexpr (LO)
-    lo = __builtin_bit_cast(h8, (__attribute__((ext_vector_type(4))) unsigned){lp[0], lp[1], lp[2], lp[3]});
-}
-
 template <int KH, int KW, int BNT, int PREC>
 __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
   using C = HaloCfg<KH, KW, BNT>;

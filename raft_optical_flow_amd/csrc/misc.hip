@@ -341,6 +341,11 @@ bool aligned16(const void* q) { return ((uintptr_t)q & 15) == 0; }
 using namespace raft;
 
 extern "C" int raft_hip_abi_version(void) { return RAFT_HIP_ABI_VERSION; }
+
+#ifndef RAFT_SRC_HASH
+#define RAFT_SRC_HASH "unknown"
+#endif
+extern "C" const char* raft_hip_source_hash(void) { return RAFT_SRC_HASH; }
 extern "C" const char* raft_hip_arch(void) { return "gfx950"; }
 extern "C" const char* raft_hip_last_error(void) { return last_error_buf(); }
 

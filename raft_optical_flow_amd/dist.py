@@ -51,9 +51,14 @@ def shard_indices(n_items: int, rank: int, world: int):
 
 
 def gather_flows(flow: torch.Tensor, dst: int = 0, group=None):
-    """Gather equally shaped per-rank flow batches to `dst` (list on dst, None elsewhere)."""
+    """Gather equally shaped per-rank flow batches to `dst` (list on dst, None elsewhere), on the
+    flows' device with RCCL; gloo (no gather of device tensors) goes through host copies."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    bufs = [torch.empty_like(flow) for _ in range(world)] if rank == dst else None
-    dist.gather(flow.contiguous(), bufs, dst=dst, group=group)
+    via_host = flow.is_cuda and dist.get_backend(group) == "gloo"
+    src = flow.detach().cpu() if via_host else flow.contiguous()
+    bufs = [torch.empty_like(src) for _ in range(world)] if rank == dst else None
+    dist.gather(src.contiguous(), bufs, dst=dst, group=group)
+    if bufs is not None and via_host:
+        bufs = [b.to(flow.device) for b in bufs]
     return bufs

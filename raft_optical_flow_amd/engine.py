@@ -371,11 +371,39 @@ def convf1_vec_weight(pu: PackedUpdate) -> torch.Tensor:
     return w
 
 
-def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool, convf1_done: bool = False):
+def convc1_fused(pk: PackedRaft) -> bool:
+    """Whether the all-pairs loop runs the lookup, convc1 and convf1 as ONE launch
+    (raft_corr_lookup_conv: RAFT-full's radius 4 / 4 levels, split-precision convs;
+    RAFT_FUSE_CONVC1=0 keeps lookup + convf1 and convc1 as two launches)."""
+    pu = pk.update
+    return (convf1_fused(pu) and pk.radius == 4 and pk.levels == 4 and pu.convc1.n == 256
+            and pu.convc1.cin == 324 and pu.convf1.n == 128
+            and pu.convc1.precision in (_lib.PREC_F16X3, _lib.PREC_F16, _lib.PREC_BF16)
+            and os.environ.get("RAFT_FUSE_CONVC1", "1") != "0")
+
+
+def convc1_frag_weight(pu: PackedUpdate) -> torch.Tensor:
+    """convc1's split weight in raft_corr_lookup_conv's fragment order (raft_hip.h), cached per precision."""
+    pc = pu.convc1
+    cached = getattr(pu, "_convc1_frag", None)
+    if cached is not None and cached[0] == pc.precision:
+        return cached[1]
+    split = pc.launch_weight()
+    n_pad, k_pad = split.shape
+    out = torch.empty(int(_lib.load().raft_lookup_conv_weight_floats(pc.n, k_pad)), device=split.device,
+                      dtype=torch.float32)
+    _lib.call("raft_lookup_conv_pack_weight", split.data_ptr(), n_pad, k_pad, pc.n, out.data_ptr(), K.stream_handle())
+    pu._convc1_frag = (pc.precision, out)
+    return out
+
+
+def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool, convf1_done: bool = False,
+                convc1_done: bool = False):
     """One BasicUpdateBlock / SmallUpdateBlock step (core/update.py:297-325 / :250-263)
     followed by coords1 += delta_flow (core/raft.py:232).  Assumes ub.corr and the
     flow slot of HX were filled by the lookup and plan_gru_context ran for this pair
-    (convf1_done: the lookup launch also wrote convf1's output, ub.flo1)."""
+    (convf1_done: the lookup launch also wrote convf1's output, ub.flo1; convc1_done: and
+    convc1's, ub.cor1)."""
     flow = Rows(ub.hx, ub.flow_off(pu), 2)
     cf = Rows(ub.cf)
     # RAFT-full: one stream; convc2 (corr branch) and convf2 (flow branch) are two 3x3 halo
@@ -394,7 +422,8 @@ def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool
     elif pair:
         if not convf1_done:
             _conv(L, pu.convf1, flow, B, h, w, Rows(ub.flo1), epilogue=_lib.EPI_RELU)
-        _conv(L, pu.convc1, Rows(ub.corr), B, h, w, Rows(ub.cor1), epilogue=_lib.EPI_RELU)
+        if not convc1_done:
+            _conv(L, pu.convc1, Rows(ub.corr), B, h, w, Rows(ub.cor1), epilogue=_lib.EPI_RELU)
         c2 = conv_params(pu.convc2, Rows(ub.cor1), B, h, w, cf.sub(0, 192), epilogue=_lib.EPI_RELU,
                          range_flag=_GUARD["flag"])
         f2 = conv_params(pu.convf2, Rows(ub.flo1), B, h, w, cf.sub(192, 64), epilogue=_lib.EPI_RELU,
@@ -540,9 +569,19 @@ class RaftPlan:
         if fuse_f1:
             f1w = convf1_vec_weight(pu)
             f1b = pu.convf1.bias.data_ptr() if pu.convf1.bias is not None else None
+        fuse_c1 = fuse_f1 and not alternate and convc1_fused(pk)
+        if fuse_c1:
+            c1w = convc1_frag_weight(pu)
+            c1b = pu.convc1.bias.data_ptr() if pu.convc1.bias is not None else None
         for it in range(iters):
             last = it == iters - 1
-            if fuse_f1 and not alternate:
+            if fuse_c1:
+                L.append(Launch("raft_corr_lookup_conv", self.pyramid.data_ptr(), B, h, w, lv, r, ub.coords.data_ptr(),
+                                ub.hx.data_ptr() + 4 * flow_slot, pu.ld, gflag, c1w.data_ptr(), c1b, pu.convc1.n,
+                                pu.convc1.precision, ub.cor1.data_ptr(), ub.cor1.shape[1], gflag, f1w.data_ptr(), f1b,
+                                pu.convf1.n, pu.convf1.kh, pu.convf1.precision, ub.flo1.data_ptr(),
+                                ub.flo1.shape[1], gflag, keep=(f1w, c1w)))
+            elif fuse_f1 and not alternate:
                 L.append(Launch("raft_corr_lookup_convf1", self.pyramid.data_ptr(), B, h, w, lv, r,
                                 ub.coords.data_ptr(), 0, ub.corr.data_ptr(), corr_ld, 0,
                                 ub.hx.data_ptr() + 4 * flow_slot, pu.ld, gflag, f1w.data_ptr(), f1b, pu.convf1.n,
@@ -554,15 +593,18 @@ class RaftPlan:
             else:
                 # every level in one call (one launch for RAFT's r = 4, C = 256: raft_hip.h)
                 arrs = K.alt_levels_args(self.f2levels)
-                L.append(Launch("raft_alt_corr_lookup_levels", fmap1.data_ptr(), *arrs, len(self.f2levels),
+                # exact fp32 products in "fp32" mode (the range guard's re-run), the f16x3 box GEMM otherwise
+                aprec = _lib.PREC_FP32 if pk.precision == _lib.PREC_FP32 else _lib.PREC_F16X3
+                L.append(Launch("raft_alt_corr_lookup_levels_prec", fmap1.data_ptr(), *arrs, len(self.f2levels),
                                 ub.coords.data_ptr(), 0, ub.corr.data_ptr(), corr_ld, B, h, w, C, r, div,
-                                ub.hx.data_ptr() + 4 * flow_slot, pu.ld, gflag, keep=arrs))
+                                ub.hx.data_ptr() + 4 * flow_slot, pu.ld, gflag, aprec, keep=arrs))
                 if fuse_f1:
                     L.append(Launch("raft_convf1_flow", ub.coords.data_ptr(), 0, B, h, w, f1w.data_ptr(), f1b,
                                     pu.convf1.n, pu.convf1.kh, pu.convf1.precision, ub.flo1.data_ptr(),
                                     ub.flo1.shape[1], gflag, keep=f1w))
             want_up = last or not test_mode
-            plan_update(L, pu, ub, B, h, w, with_mask=want_up and not pu.small, convf1_done=fuse_f1)
+            plan_update(L, pu, ub, B, h, w, with_mask=want_up and not pu.small, convf1_done=fuse_f1,
+                        convc1_done=fuse_c1)
             if want_up:
                 dst = self.flow_up[-1 if test_mode else it]
                 if pu.small:

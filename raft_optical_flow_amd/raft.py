@@ -22,15 +22,27 @@ evaluate.py's many KITTI sizes do not accumulate device memory.
 
 f16x3 range guard: the default fp32-accurate split arithmetic holds only while every
 conv input stays below 65504 in magnitude (include/raft_hip.h).  The convs and lookups
-whose outputs feed split convs raise a device flag above 2^15; forward() checks it and
-re-runs that forward on exact f32 MFMA with a warning (`model.range_guard = "raise"`
-raises FloatingPointError instead; "off" skips the check; env RAFT_RANGE_GUARD).
+whose outputs feed split convs raise a device flag above 2^15.  `model.range_guard`
+(env RAFT_RANGE_GUARD) chooses what happens then:
+  "fallback" (default)  the check is deferred so forwards queue back to back with no host
+                        sync: the flag is copied to pinned host memory behind the forward
+                        and read once that copy has completed (at a later forward() call, or
+                        at model.check_range_guard(), which waits).  A raised flag warns and
+                        re-runs that forward on exact f32 MFMA INTO the tensors it returned,
+                        so they hold the exact result once check_range_guard() returns
+                        (a reader before that point may have seen the inexact values; the
+                        re-run needs the input tensors unmodified in place, else it warns
+                        that it cannot correct them);
+  "sync"                forward() waits for its flag and returns the f32 re-run's result
+                        (the round-2 behaviour: one host sync per forward);
+  "raise"               as "sync", but raises FloatingPointError;
+  "off"                 no device checks at all.
 """
 from __future__ import annotations
 
 import os
 import warnings
-from collections import OrderedDict
+from collections import OrderedDict, deque
 
 import torch
 import torch.nn as nn
@@ -87,6 +99,7 @@ class RAFT(nn.Module):
         self.conv_precision = getattr(args, "conv_precision", None)
         self._packed = {}           # precision -> (weights key, PackedRaft)
         self._plans = OrderedDict()
+        self._pending = deque()     # deferred range-guard checks ("fallback"), oldest first
 
     def freeze_bn(self):
         for m in self.modules():
@@ -145,7 +158,8 @@ class RAFT(nn.Module):
         pk = self.packed(device, prec)
         # the stream layout knobs are read when a plan is built, so they are part of its key
         knobs = (os.environ.get("RAFT_CTX_SIDE", "1"), os.environ.get("RAFT_FLOW_SIDE", "1"),
-                 os.environ.get("RAFT_CONV_PAIR", "1"), os.environ.get("RAFT_FUSE_CONVF1", "1"))
+                 os.environ.get("RAFT_CONV_PAIR", "1"), os.environ.get("RAFT_FUSE_CONVF1", "1"),
+                 os.environ.get("RAFT_FUSE_CONVC1", "1"))
         guard = self.range_guard != "off"  # "off": no device-side checks either
         key = (batch, height, width, iters, bool(test_mode), bool(self.args.alternate_corr), bool(flow_init), prec,
                knobs, guard)
@@ -167,28 +181,87 @@ class RAFT(nn.Module):
             if self._plans[k] is not keep:
                 self._plans.pop(k).release()
 
+    # -- deferred range guard ------------------------------------------------
+    _MAX_PENDING = 2  # forwards whose flag may be unread: the third waits for the oldest
+
+    def check_range_guard(self, block=True):
+        """Resolve the deferred range-guard checks of earlier forwards ("fallback" mode): with
+        block=True wait for all of them, else only read those whose flag copy has completed.
+        A raised flag warns and re-runs that forward on exact f32 MFMA into its output tensors."""
+        while self._pending:
+            rec = self._pending[0]
+            if not block and len(self._pending) <= self._MAX_PENDING and not rec["event"].query():
+                break
+            rec["event"].synchronize()
+            self._pending.popleft()
+            if int(rec["flag"].item()):
+                self._guard_fallback(rec)
+
+    def _guard_fallback(self, rec):
+        msg = ("f16x3 range guard: an activation exceeded 2^15 in magnitude, outside the exact range "
+               "of the split-f16 conv arithmetic")
+        ins = [x for x in rec["inputs"] if x is not None]
+        if any(x._version != v for x, v in zip(ins, rec["versions"])):
+            warnings.warn(msg + "; the inputs of that forward were modified in place since, so its outputs "
+                          "cannot be recomputed and stay inexact", RuntimeWarning)
+            return
+        warnings.warn(msg + "; that forward was re-run with exact f32 MFMA convs into its output tensors",
+                      RuntimeWarning)
+        i1, i2, fi = rec["inputs"]
+        exact = self.forward(i1, i2, rec["iters"], fi, True, rec["test_mode"], _prec="fp32")
+        outs, new = rec["outputs"], exact
+        if isinstance(outs, tuple):
+            for o, n in zip(outs, new):
+                o.copy_(n)
+        else:
+            for o, n in zip(outs, new):
+                o.copy_(n)
+
     def forward(self, image1, image2, iters=12, flow_init=None, upsample=True, test_mode=False, _prec=None):
+        if image1.is_cuda and image1.device != torch.device("cuda", torch.cuda.current_device()):
+            # launches go to the current device's stream: make the images' device current
+            with torch.cuda.device(image1.device):
+                return self.forward(image1, image2, iters, flow_init, upsample, test_mode, _prec)
         if self.training:
             raise NotImplementedError("raft_optical_flow_amd.RAFT is an inference path: call model.eval() "
                                       "(training / BatchNorm batch statistics are out of scope)")
         K.require_device(image1, image2, flow_init)
         if image1.shape != image2.shape or image1.dim() != 4 or image1.shape[1] != 3:
             raise ValueError(f"images must both be [N, 3, H, W], got {tuple(image1.shape)} / {tuple(image2.shape)}")
+        if self._pending and _prec is None:
+            self.check_range_guard(block=False)  # earlier forwards whose flags have landed
         b, _, H, W = image1.shape
         pl = self.plan(b, H, W, iters, test_mode, flow_init is not None, image1.device, prec=_prec)
         pl.set_inputs(image1, image2, flow_init)
-        guard = pl.guarded and self.range_guard != "off"
+        mode = self.range_guard
+        guard = pl.guarded and mode != "off"
         if guard:
             pl.range_flag.zero_()
         if self.hip_graph and (pl.graph is not None or pl.runs > 0):
             pl.replay()
         else:
             pl.run()
-        if guard and int(pl.range_flag.item()):
-            msg = ("f16x3 range guard: an activation exceeded 2^15 in magnitude, outside the exact range "
-                   "of the split-f16 conv arithmetic")
-            if self.range_guard == "raise":
-                raise FloatingPointError(msg)
-            warnings.warn(msg + "; this forward was re-run with exact f32 MFMA convs", RuntimeWarning)
-            return self.forward(image1, image2, iters, flow_init, upsample, test_mode, _prec="fp32")
-        return pl.outputs(clone=True)
+        outs = pl.outputs(clone=True)
+        if not guard:
+            return outs
+        if mode in ("sync", "raise"):
+            if int(pl.range_flag.item()):
+                msg = ("f16x3 range guard: an activation exceeded 2^15 in magnitude, outside the exact range "
+                       "of the split-f16 conv arithmetic")
+                if mode == "raise":
+                    raise FloatingPointError(msg)
+                warnings.warn(msg + "; this forward was re-run with exact f32 MFMA convs", RuntimeWarning)
+                return self.forward(image1, image2, iters, flow_init, upsample, test_mode, _prec="fp32")
+            return outs
+        # "fallback": the flag travels to pinned host memory behind the forward; read later
+        flag = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        flag.copy_(pl.range_flag, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        ins = (image1, image2, flow_init)
+        self._pending.append({"event": ev, "flag": flag, "inputs": ins, "outputs": outs, "iters": iters,
+                              "test_mode": test_mode,
+                              "versions": [x._version for x in ins if x is not None]})
+        if len(self._pending) > self._MAX_PENDING:
+            self.check_range_guard(block=False)
+        return outs

@@ -11,6 +11,7 @@
 
 Every helper computes on the GPU through the HIP kernels of libraft_hip.so; a CPU tensor is
 copied to the current GPU and the result copied back (there is no host computation path).
+Kernels run on the tensor's own device (its current stream), whatever device is current.
 """
 from __future__ import annotations
 
@@ -24,6 +25,20 @@ def _lib():
 
 def _stream():
     return torch.cuda.current_stream().cuda_stream
+
+
+def _on_device(fn):
+    """Run fn(x, ...) with x's GPU current (so launches take that device's current stream);
+    CPU inputs go to the current GPU first (inside fn)."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrapped(x, *args, **kw):
+        if torch.is_tensor(x) and x.is_cuda:
+            with torch.cuda.device(x.device):
+                return fn(x, *args, **kw)
+        return fn(x, *args, **kw)
+    return wrapped
 
 
 def _on_gpu(x: torch.Tensor) -> torch.Tensor:
@@ -46,6 +61,12 @@ class InputPadder:
         self._pad = [pw // 2, pw - pw // 2, top, ph - top]
 
     def _pad_one(self, x: torch.Tensor) -> torch.Tensor:
+        if x.is_cuda:
+            with torch.cuda.device(x.device):
+                return self._pad_dev(x)
+        return self._pad_dev(x)
+
+    def _pad_dev(self, x: torch.Tensor) -> torch.Tensor:
         left, right, top, bottom = self._pad
         src = x
         x = _on_gpu(x).float().contiguous()
@@ -64,6 +85,7 @@ class InputPadder:
         return x[..., top:h - bottom, left:w - right]
 
 
+@_on_device
 def forward_interpolate(flow):
     """Warm-start flow for the next frame pair (evaluate.py:37-41): each pixel takes the flow of
     the nearest point the flow moves a pixel to, over the points that land strictly inside the
@@ -82,6 +104,7 @@ def forward_interpolate(flow):
     return out.to(flow.device)
 
 
+@_on_device
 def bilinear_sampler(img, coords, mode="bilinear", mask=False):
     """Sample img [N, C, H, W] at pixel coordinates coords [N, Ho, Wo, 2] (x, y): bilinear,
     corners outside the image read 0 (grid_sample align_corners=True).  With mask=True also
@@ -108,6 +131,7 @@ def coords_grid(batch, ht, wd, device):
     return torch.stack([x, y], 0)[None].repeat(batch, 1, 1, 1)
 
 
+@_on_device
 def upflow8(flow, mode="bilinear"):
     """8 * bilinear(align_corners=True) x8 upsampling (raft_upflow8)."""
     from .. import kernels as K

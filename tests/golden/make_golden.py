@@ -232,6 +232,27 @@ def gen_bf16():
 
 
 @torch.no_grad()
+def gen_bf16_config5():
+    """Config 5 at its real size: 1080x1920 (a multiple of 8: no padding), iters=32, the reference
+    with mixed_precision=True under CPU bf16 autocast (as gen_bf16); flow_low and every 8th row of
+    flow_up are stored (plus the whole field's sum and absolute sum)."""
+    rraft, *_ = ref_modules()
+    saved = rraft.autocast
+    rraft.autocast = lambda enabled=True: torch.autocast("cpu", dtype=torch.bfloat16, enabled=enabled)
+    try:
+        i1, i2 = seeded_images(1, 1080, 1920, seed=5)
+        m = rraft.RAFT(argparse.Namespace(small=False, mixed_precision=True, alternate_corr=False, dropout=0))
+        m.load_state_dict(seeded_state_dict(m, 0))
+        m.eval()
+        low, up = m(i1, i2, iters=32, test_mode=True)
+        low, up = low.float(), up.float()
+        save("raft_full_rand_b1_1080x1920_i32_bf16.npz", iters=32, seed=0, img_seed=5, flow_low=low,
+             flow_up_rows8=up[:, :, ::8], flow_up_sum=up.double().sum(), flow_up_abs=up.double().abs().sum())
+    finally:
+        rraft.autocast = saved
+
+
+@torch.no_grad()
 def gen_raft_small_demo():
     """Config 1: raft-small.pth on demo-frames 0016 -> 0017, iters=12 (reference demo.py path)."""
     from PIL import Image
@@ -265,7 +286,7 @@ if __name__ == "__main__":
     a = ap.parse_args()
     jobs = {"lookup": gen_lookup, "update": gen_update_and_upsample, "enc": gen_encoders,
             "e2e": lambda: gen_raft_e2e(a.full_size), "demo": gen_raft_small_demo,
-            "config4": gen_config4, "bf16": gen_bf16, "caller": gen_caller, "bigr": gen_lookup_big_radius}
+            "config4": gen_config4, "bf16": gen_bf16, "bf16big": gen_bf16_config5, "caller": gen_caller, "bigr": gen_lookup_big_radius}
     for k, f in jobs.items():
         if not a.only or k in a.only.split(","):
             f()

@@ -226,21 +226,30 @@ def test_bf16_band_vs_reference_autocast():
     assert epe_f < 0.15
 
 
-def test_bf16_1080x1920_property():
-    """Config 5 geometry: 1080x1920 (no padding), B=1, iters=32, bf16: finite, and mean EPE
-    against the same run in the fp32-accurate f16x3 mode <= 0.25 px (random-init flows
-    reach |flow| ~ 20 px; bf16 vs fp32 measured at 128x192: 0.11 px for the reference)."""
+def test_bf16_1080x1920_vs_reference_autocast():
+    """Config 5 at its real size: 1080x1920 (no padding), B=1, iters=32, conv_precision="bf16",
+    against the reference run at the same size under CPU bf16 autocast
+    (tests/golden/make_golden.py gen_bf16_config5): flow_low everywhere and every 8th row of
+    flow_up, plus the field's sum / absolute sum.  Two bf16 runs differ by where they round (the
+    reference's autocast rounds conv inputs and outputs, the HIP path rounds conv operands and
+    keeps fp32 activations), so the band is that of the 128x192 case, not bit equality."""
+    g = load_golden("raft_full_rand_b1_1080x1920_i32_bf16.npz")
     from raft_optical_flow_amd.init import seeded_images
-    i1, i2 = seeded_images(1, 1080, 1920, seed=5)
-    i1, i2 = i1.to(DEV), i2.to(DEV)
+    i1, i2 = seeded_images(1, 1080, 1920, seed=int(g["img_seed"]))
     with torch.no_grad():
-        mb = make_model(0, precision="bf16")
-        _, upb = mb(i1, i2, iters=32, test_mode=True)
-        del mb
-        torch.cuda.empty_cache()
-        mf = make_model(0, precision="f16x3")
-        _, upf = mf(i1, i2, iters=32, test_mode=True)
-    assert torch.isfinite(upb).all() and torch.isfinite(upf).all()
-    epe = float(((upb.double() - upf.double()) ** 2).sum(1).sqrt().mean())
-    print(f"1080x1920 bf16 vs f16x3: mean EPE {epe:.3g}, max |flow| {float(upf.abs().max()):.3g}")
-    assert epe < 0.25
+        m = make_model(int(g["seed"]), precision="bf16")
+        low, up = m(i1.to(DEV), i2.to(DEV), iters=int(g["iters"]), test_mode=True)
+    assert torch.isfinite(up).all()
+    lo = low.cpu().double().numpy()
+    u8 = up[:, :, ::8].cpu().double().numpy()
+    dl = np.abs(lo - g["flow_low"])
+    du = np.abs(u8 - g["flow_up_rows8"])
+    epe = np.sqrt(((u8 - g["flow_up_rows8"]) ** 2).sum(1)).mean()
+    mag = float(np.abs(g["flow_up_rows8"]).max())
+    rel_abs = abs(float(up.double().abs().sum()) - float(g["flow_up_abs"])) / float(g["flow_up_abs"])
+    print(f"1080x1920 bf16 vs reference bf16: flow_low max {dl.max():.3g} mean {dl.mean():.3g}; flow_up rows8 "
+          f"max {du.max():.3g} mean {du.mean():.3g}, mean EPE {epe:.3g} (max |flow| {mag:.3g}); "
+          f"|flow| sum rel {rel_abs:.3g}")
+    assert dl.max() < 0.5 and dl.mean() < 0.05
+    assert du.max() < 1.0 and du.mean() < 0.1 and epe < 0.15
+    assert rel_abs < 0.02

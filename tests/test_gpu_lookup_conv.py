@@ -1,0 +1,145 @@
+"""GPU parity of raft_corr_lookup_conv: the correlation lookup fused with the motion encoder's
+convc1 (1x1, 324 -> 256, relu) and convf1 (7x7, 2 -> 128, relu) in one launch
+(core/corr.py:56-94, core/update.py:185-205).
+
+convc1 is checked against an fp64 torch conv of the plain lookup's correlation rows
+(raft_corr_lookup, itself pinned to the reference's goldens), with the operands rounded to the
+conv precision's operand type in the one-product modes; tolerances as the conv GEMM tests:
+1e-4 x max|ref| (f16x3), 5e-3 x (f16), 3e-2 x (bf16).  convf1 and the flow output must equal the
+unfused kernels' bit for bit (same FMA order)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+TOL = {"f16x3": 1e-4, "f16": 5e-3, "bf16": 3e-2}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from raft_optical_flow_amd import _lib
+    _lib.load()
+
+
+def t(x):
+    return torch.from_numpy(np.ascontiguousarray(x)).float().to(DEV)
+
+
+def _case(B, h, w, prec, coord_sigma=3.0, fscale=1.0, seed=5, C=64):
+    from raft_optical_flow_amd import _lib
+    from raft_optical_flow_amd import kernels as K
+    p = _lib.PRECISIONS[prec]
+    rng = np.random.default_rng(seed)
+    L, r = 4, 4
+    f1 = rng.standard_normal((B, C, h, w)).astype(np.float32) * fscale
+    f2 = rng.standard_normal((B, C, h, w)).astype(np.float32) * fscale
+    r1, r2 = K.nchw_to_rows(t(f1)), K.nchw_to_rows(t(f2))
+    pyr = torch.empty(K.pyramid_floats(B, h, w, L), device=DEV)
+    _lib.call("raft_corr_build", r1.data_ptr(), r2.data_ptr(), C, B, h, w, C, L, K.sqrt_c(C), pyr.data_ptr(),
+              K.stream_handle())
+    ys, xs = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    grid = np.stack([xs, ys], -1)[None].astype(np.float32)
+    coords = (grid + rng.normal(0, coord_sigma, (B, h, w, 2))).astype(np.float32)
+    cr = t(coords.reshape(-1, 2))
+    P, ntap = B * h * w, 324
+    # convc1 weights, packed as the engine does (engine.convc1_frag_weight)
+    wc = (rng.standard_normal((256, ntap)) * 0.05).astype(np.float32)
+    bc = (rng.standard_normal(256) * 0.1).astype(np.float32)
+    pc = K.pack_conv(torch.from_numpy(wc)[:, :, None, None], torch.from_numpy(bc), 1, 0, device=DEV)
+    pc.precision = p
+    split = pc.launch_weight()
+    n_pad, k_pad = split.shape
+    frag = torch.empty(int(_lib.load().raft_lookup_conv_weight_floats(256, k_pad)), device=DEV)
+    _lib.call("raft_lookup_conv_pack_weight", split.data_ptr(), n_pad, k_pad, 256, frag.data_ptr(), K.stream_handle())
+    # convf1 weights [n/32][49][2][32], rounded as the engine does in the one-product modes
+    wf = (rng.standard_normal((128, 2, 7, 7)) * 0.1).astype(np.float32)
+    bf = (rng.standard_normal(128) * 0.1).astype(np.float32)
+    rnd = {"f16": torch.float16, "bf16": torch.bfloat16}.get(prec)
+    wq = torch.from_numpy(wf)
+    if rnd is not None:
+        wq = wq.to(rnd).float()
+    wv = wq.reshape(4, 32, 2, 49).permute(0, 3, 2, 1).contiguous().to(DEV)
+    # unfused: lookup (+flow), convf1 alone
+    corr = torch.full((P, ntap), -7.0, device=DEV)
+    flow_a = torch.zeros(P, 4, device=DEV)
+    _lib.call("raft_corr_lookup", pyr.data_ptr(), B, h, w, L, r, cr.data_ptr(), 0, corr.data_ptr(), ntap, 0,
+              flow_a.data_ptr(), 4, None, K.stream_handle())
+    f1_a = torch.full((P, 132), -7.0, device=DEV)
+    _lib.call("raft_convf1_flow", cr.data_ptr(), 0, B, h, w, wv.data_ptr(), t(bf).data_ptr(), 128, 7, p,
+              f1_a.data_ptr(), 132, None, K.stream_handle())
+    # fused
+    c1 = torch.full((P, 260), -7.0, device=DEV)
+    f1_b = torch.full((P, 132), -7.0, device=DEV)
+    flow_b = torch.zeros(P, 4, device=DEV)
+    flags = torch.zeros(3, dtype=torch.int32, device=DEV)
+    fp = flags.data_ptr()
+    _lib.call("raft_corr_lookup_conv", pyr.data_ptr(), B, h, w, L, r, cr.data_ptr(), flow_b.data_ptr(), 4, fp,
+              frag.data_ptr(), pc.bias.data_ptr(), 256, p, c1.data_ptr(), 260, fp + 4, wv.data_ptr(),
+              t(bf).data_ptr(), 128, 7, p, f1_b.data_ptr(), 132, fp + 8, K.stream_handle())
+    torch.cuda.synchronize()
+    # convc1 reference: fp64 on the plain lookup's rows (operands rounded in one-product modes)
+    cin = corr.cpu().double()
+    wref = torch.from_numpy(wc).double()
+    if rnd is not None:
+        cin = cin.to(rnd).double()
+        wref = wref.to(rnd).double()
+    ref = torch.relu(cin @ wref.T + torch.from_numpy(bc).double())
+    return dict(c1=c1, ref=ref, f1_a=f1_a, f1_b=f1_b, flow_a=flow_a, flow_b=flow_b, flags=flags.cpu().tolist(),
+                corr=corr)
+
+
+@pytest.mark.parametrize("B,h,w", [(1, 55, 128), (2, 17, 21), (1, 16, 40)])
+@pytest.mark.parametrize("prec", ["f16x3", "f16", "bf16"])
+def test_lookup_conv_equals_lookup_then_convs(B, h, w, prec):
+    """Config 2's 1/8-res grid (2x16 tiles, last tile row half), ragged tiles in both axes."""
+    d = _case(B, h, w, prec)
+    got = d["c1"][:, :256].cpu().double()
+    scale = float(d["ref"].abs().max())
+    err = float((got - d["ref"]).abs().max())
+    assert err <= TOL[prec] * max(1.0, scale), (err, scale)
+    assert bool((d["c1"][:, 256:] == -7.0).all())  # nothing past n channels of a row
+    assert torch.equal(d["f1_a"], d["f1_b"])
+    assert torch.equal(d["flow_a"], d["flow_b"])
+    assert d["flags"] == [0, 0, 0]
+
+
+def test_lookup_conv_far_out_of_bounds():
+    """Coordinates spread far past the map (zero taps, windows off every level)."""
+    d = _case(1, 19, 35, "f16x3", coord_sigma=40.0, seed=9)
+    got = d["c1"][:, :256].cpu().double()
+    scale = float(d["ref"].abs().max())
+    assert float((got - d["ref"]).abs().max()) <= 1e-4 * max(1.0, scale)
+    assert torch.equal(d["f1_a"], d["f1_b"])
+
+
+def test_lookup_conv_range_guard():
+    """Correlation taps beyond the f16x3 split range raise the lookup's flag."""
+    d = _case(1, 16, 24, "f16x3", fscale=200.0, seed=3)
+    assert float(d["corr"].abs().max()) > 32768
+    assert d["flags"][0] == 1
+
+
+def test_raft_fused_lookup_conv_matches_unfused(monkeypatch):
+    """RAFT-full forward with the fused launch vs RAFT_FUSE_CONVC1=0 (lookup + convf1, then convc1
+    as a halo conv): the same flow within the f16x3 end-to-end noise."""
+    import argparse
+    from raft_optical_flow_amd import RAFT
+    from raft_optical_flow_amd.init import seeded_state_dict, smooth_images
+    m = RAFT(argparse.Namespace(small=False, mixed_precision=False, alternate_corr=False))
+    m.load_state_dict(seeded_state_dict(m, 0))
+    m.to(DEV).eval()
+    i1, i2 = smooth_images(1, 128, 192, seed=3)
+    i1, i2 = i1.to(DEV), i2.to(DEV)
+    with torch.no_grad():
+        lo_a, up_a = m(i1, i2, iters=12, test_mode=True)
+        names = m._plans[next(iter(m._plans))].kernel_names()
+        monkeypatch.setenv("RAFT_FUSE_CONVC1", "0")
+        lo_b, up_b = m(i1, i2, iters=12, test_mode=True)
+    assert names.count("raft_corr_lookup_conv") == 12
+    assert float((up_a - up_b).abs().max()) < 1e-3
+    assert float((lo_a - lo_b).abs().max()) < 1e-3

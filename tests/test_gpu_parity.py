@@ -449,6 +449,8 @@ def _alt_bwd_case(seed, B, H1, W1, H2, W2, C, N, r, spread):
     dict(seed=3, B=1, H1=6, W1=7, H2=6, W2=7, C=32, N=1, r=2, spread=2.0),
     dict(seed=4, B=2, H1=9, W1=13, H2=5, W2=7, C=96, N=2, r=4, spread=3.0),    # pooled level, N = 2
     dict(seed=5, B=1, H1=8, W1=8, H2=8, W2=8, C=260, N=1, r=3, spread=9.0),    # far out of bounds, C > 256
+    dict(seed=6, B=1, H1=10, W1=12, H2=10, W2=12, C=64, N=1, r=6, spread=3.0),  # r = 6: 196 taps (4-wave blocks)
+    dict(seed=7, B=1, H1=5, W1=6, H2=9, W2=11, C=32, N=1, r=23, spread=2.0),   # r = 23: 2304 taps (1-wave blocks)
 ])
 def test_alt_cuda_corr_backward_vs_autograd(case):
     """alt_cuda_corr.backward against autograd (fp64) through the differentiable restatement
@@ -830,6 +832,14 @@ def test_f16x3_range_guard_falls_back_to_fp32():
         fm = ref_m.fnet(i1)
         assert float(fm.abs().max()) > 65504.0
         rlow, rup = ref_m(i1, i2, iters=4, test_mode=True)
+        # "fallback" (default): the check is deferred; check_range_guard() resolves it and the
+        # returned tensors then hold the exact-f32 re-run's result
+        low, up = m(i1, i2, iters=4, test_mode=True)
+        with pytest.warns(RuntimeWarning, match="range guard"):
+            m.check_range_guard()
+        assert maxabs(low, rlow) == 0.0 and maxabs(up, rup) == 0.0
+        # "sync": forward() itself waits for the flag and returns the re-run's result
+        m.range_guard = "sync"
         with pytest.warns(RuntimeWarning, match="range guard"):
             low, up = m(i1, i2, iters=4, test_mode=True)
         assert maxabs(low, rlow) == 0.0 and maxabs(up, rup) == 0.0
@@ -841,6 +851,40 @@ def test_f16x3_range_guard_falls_back_to_fp32():
             warnings.simplefilter("error")
             low_off, up_off = m(i1, i2, iters=4, test_mode=True)
     assert not bool(torch.isfinite(up_off).all()) or maxabs(up_off, rup) > 1e-3
+
+
+def test_range_guard_deferred_forwards_queue_without_host_sync():
+    """"fallback" mode: back-to-back forwards enqueue without waiting for the GPU (the flag is read
+    once its copy has landed): behind a ~50 ms spin kernel, two forward() calls return while the
+    stream is still busy; the deferred checks resolve quietly in range, and a forward whose inputs
+    were modified in place before a raised flag is read warns that it cannot be corrected."""
+    import warnings
+    g = load_golden("raft_full_rand_b1_128x192_i32.npz")
+    m, _ = make_model(False, 0)
+    i1, i2 = t(g["image1"]), t(g["image2"])
+    with torch.no_grad(), warnings.catch_warnings():
+        warnings.simplefilter("error")
+        for _ in range(2):  # eager run, then the graph capture (which synchronises)
+            m(i1, i2, iters=4, test_mode=True)
+        m.check_range_guard()
+        s = torch.cuda.current_stream()
+        torch.cuda._sleep(int(1e8))
+        a = m(i1, i2, iters=4, test_mode=True)
+        b = m(i1, i2, iters=4, test_mode=True)
+        busy = not s.query()
+        m.check_range_guard()
+    assert busy, "forward() synchronised with the device"
+    assert not m._pending
+    assert maxabs(a[1], b[1]) == 0.0
+    # a raised flag with modified inputs: warned, not corrected
+    with torch.no_grad():
+        m.fnet.conv2.weight.mul_(20000.0)
+        m.fnet.conv2.bias.mul_(20000.0)
+        j1 = i1.clone()
+        m(j1, i2, iters=4, test_mode=True)
+        j1.add_(1.0)
+        with pytest.warns(RuntimeWarning, match="cannot be recomputed"):
+            m.check_range_guard()
 
 
 def test_range_guard_quiet_in_range():

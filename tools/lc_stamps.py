@@ -1,0 +1,50 @@
+"""Phase stamps of the fused lookup + convc1 + convf1 kernel (a -DLC_STAMPS variant):
+
+    make -C raft_optical_flow_amd/csrc variant NAME=lcst DEFS=-DLC_STAMPS
+    RAFT_HIP_LIB=variants/lcst/libraft_hip.so python tools/lc_stamps.py
+
+Runs config 2 forwards eagerly, then replays the last iteration's fused launch alone once and
+prints per-wave cycle means of each phase and the launch's wall span (100 MHz realtime)."""
+import argparse
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from raft_optical_flow_amd import RAFT, _lib  # noqa: E402
+from raft_optical_flow_amd import kernels as K  # noqa: E402
+from raft_optical_flow_amd.init import seeded_images, seeded_state_dict  # noqa: E402
+
+dev = torch.device("cuda:0")
+m = RAFT(argparse.Namespace(small=False, mixed_precision=False, alternate_corr=False))
+m.load_state_dict(seeded_state_dict(m, 0))
+m.to(dev).eval()
+m.hip_graph = False
+i1, i2 = seeded_images(1, 440, 1024, seed=1)
+with torch.no_grad():
+    for _ in range(2):
+        m(i1.to(dev), i2.to(dev), iters=32, test_mode=True)
+pl = next(iter(m._plans.values()))
+lk = [l for l in pl.launches if getattr(l, "name", "") == "raft_corr_lookup_conv"]
+lib = _lib.load()
+lib.raft_debug_lcstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+for rep in range(3):
+    torch.cuda.synchronize()
+    lk[-1](K.stream_handle())
+    torch.cuda.synchronize()
+nwg = 224
+buf = np.zeros(nwg * 8 * 16, dtype=np.uint64)
+lib.raft_debug_lcstamps(buf.ctypes.data, buf.size)
+s = buf.reshape(nwg * 8, 16).astype(np.int64)
+r0, r1, t = s[:, 0], s[:, 1], s[:, 2:12]
+names = ["issue loads", "axis entries", "vmcnt16+flowpatch+sync", "convf1", "wait tiles", "taps x4",
+         "sync A", "GEMM", "epilogues"]
+d = np.diff(t, axis=1)
+for k, n in enumerate(names):
+    print(f"  {n:26s} mean {d[:, k].mean():8.0f} cyc  max {d[:, k].max():8.0f}")
+print(f"  total per wave mean {(t[:, 9] - t[:, 0]).mean():.0f} cycles")
+print(f"  launch span (realtime 100 MHz): {(r1.max() - r0.min()) / 100:.2f} us; wave mean {(r1 - r0).mean() / 100:.2f} us;"
+      f" start spread {(r0.max() - r0.min()) / 100:.2f} us")
