@@ -123,22 +123,24 @@ int raft_convf1_flow(const float* coords, int coords_layout, int B, int H, int W
 /* The lookup fused with the motion encoder's first convs (RAFT-full: radius 4, 4 levels), ONE
  * launch per iteration of the all-pairs loop (core/corr.py:56-94 + core/update.py:185-205):
  *   c1_out rows [B*H*W][c1_out_ld] = relu(convc1(corr) + c1_bias), convc1 = the 1x1 324 -> 256 conv
- *   over the lookup's 324 channels (channel order of raft_corr_lookup), in c1_precision
- *   (RAFT_PREC_F16X3 / F16 / BF16 arithmetic of raft_conv2d); the correlation rows never
+ *   over the lookup's 324 channels (channel order of raft_corr_lookup); the correlation rows never
  *   leave the work-group (LDS), so they are not an output;
- *   f1_out, flow_out: as raft_corr_lookup_convf1 (convf1: exact fp32, f1_n = 128, f1_k = 7).
- * coords: NHWC [B*H*W][2], 16-B aligned.  c1_weight: raft_lookup_conv_pack_weight's output for
- * the split form (raft_conv2d_split_weight_prec, c1_precision) of convc1's packed weight
- * [256][352].  range_flag: raised by a lookup tap above RAFT_RANGE_LIMIT (the split convc1
- * input); c1_range_flag / f1_range_flag: by the convc1 / convf1 outputs (split convc2 / convf2
- * inputs).  Returns RAFT_E_INVALID for any other radius / level count / channel count (the
- * caller then runs raft_corr_lookup_convf1 + raft_conv2d). */
+ *   f1_out rows [B*H*W][f1_out_ld] = relu(convf1(flow) + f1_bias), convf1 the 7x7 2 -> 128 conv of
+ *   flow = coords - coords_grid (zero padding), f1_k = 7;
+ *   flow_out (optional): as raft_corr_lookup.
+ * Both convs in `precision` (RAFT_PREC_F16X3 / F16 / BF16: the arithmetic of raft_conv2d).
+ * coords: NHWC [B*H*W][2].  c1_weight / f1_weight: raft_lookup_conv_pack_weight's output for the
+ * split form (raft_conv2d_split_weight_prec, `precision`) of the conv's packed weight (convc1
+ * [256][352] RAFT_CONV_VEC, convf1 [128][128] RAFT_CONV_GATHER), 16-B aligned.  range_flag: raised
+ * by a lookup tap above RAFT_RANGE_LIMIT (the split convc1 input); c1_range_flag / f1_range_flag:
+ * by the convc1 / convf1 outputs (split convc2 / convf2 inputs).  Returns RAFT_E_INVALID for any
+ * other radius / level count / channel count (the caller then runs raft_corr_lookup_convf1 +
+ * raft_conv2d). */
 int raft_corr_lookup_conv(const float* pyramid, int B, int H, int W, int num_levels, int radius,
-                          const float* coords, float* flow_out, int flow_ld, int* range_flag,
-                          const void* c1_weight, const float* c1_bias, int c1_n, int c1_precision,
-                          float* c1_out, int c1_out_ld, int* c1_range_flag, const float* f1_weight,
-                          const float* f1_bias, int f1_n, int f1_k, int f1_precision, float* f1_out,
-                          int f1_out_ld, int* f1_range_flag, raft_stream_t stream);
+                          const float* coords, float* flow_out, int flow_ld, int* range_flag, int precision,
+                          const void* c1_weight, const float* c1_bias, int c1_n, float* c1_out, int c1_out_ld,
+                          int* c1_range_flag, const void* f1_weight, const float* f1_bias, int f1_n, int f1_k,
+                          float* f1_out, int f1_out_ld, int* f1_range_flag, raft_stream_t stream);
 /* convc1's split weight [n_pad][k_pad] (k_pad % 32 == 0) -> raft_corr_lookup_conv's fragment order:
  * [k_pad/32][n/32][4][64] x 16 B, element (j, s, t, lane) = 8 halves of split row 32s + lane%32,
  * K-step j, quad (t/2)*4 + 2*(lane/32) + t%2; out holds raft_lookup_conv_weight_floats(n, k_pad)
@@ -287,6 +289,14 @@ typedef struct raft_conv2d_params {
   int precision;                            /* RAFT_PREC_* (weight format follows it) */
   int* range_flag;                          /* optional (NULL = off): set to 1 when an output
                                                exceeds RAFT_RANGE_LIMIT in magnitude */
+  float* stats_part; int stats_ld;          /* optional (NULL = off): InstanceNorm partial statistics
+                                               of the output, see raft_conv2d_stats_slots */
+  const float* in_norm; int in_norm_relu;   /* optional (NULL = off): the conv reads
+                                               act((seg0 - mean[b][c]) * rstd[b][c]) instead of seg 0,
+                                               in_norm = [batch][in0_c][2] {mean, rstd} (the output of
+                                               raft_instnorm_stats / _merge), act = relu if
+                                               in_norm_relu; zero padding stays zero.  Only where
+                                               raft_conv2d_in_norm_ok says so. */
 } raft_conv2d_params;
 
 /* f16x3 range guard.  RAFT_PREC_F16X3 splits every activation x as hi = f16(x), which is
@@ -299,6 +309,22 @@ typedef struct raft_conv2d_params {
  * epilogues (sigmoid / tanh blends of |h| <= 1); neither do convs whose outputs only feed
  * fp32 consumers (the raw convs of an InstanceNorm encoder, the flow head's first conv). */
 #define RAFT_RANGE_LIMIT 32768.0f
+
+/* InstanceNorm statistics from the conv epilogue (core/extractor.py norm_fn='instance': the
+ * raw conv output's per-(image, channel) mean and variance without a pass over it).  With
+ * p->stats_part set, every wave of the conv writes, per output channel n, the (count, mean, M2)
+ * of its <= 32 output pixels (M2 = sum of squared deviations from that mean) as 4 floats at
+ * stats_part[((slot * stats_ld) + n) * 4 ..], slot = image * slots_per_image + s, s <
+ * slots_per_image; raft_instnorm_merge combines them (Chan's formula in double, fixed order).
+ * Only for convs with the linear epilogue (alpha 1, no add0) that run on the halo or stem kernel:
+ * raft_conv2d_stats_slots returns slots_per_image for such a conv and 0 otherwise (raft_conv2d
+ * then rejects stats_part). */
+int raft_conv2d_stats_slots(const raft_conv2d_params* p);
+/* 1 when the conv can apply its input's InstanceNorm in its loaders (in_norm above: the halo
+ * kernel's 3x3 convs over <= 256 channels), else 0. */
+int raft_conv2d_in_norm_ok(const raft_conv2d_params* p);
+int raft_instnorm_merge(const float* part, int slots_per_image, int B, int C, int stats_ld, float eps,
+                        float* stats, raft_stream_t stream);
 
 /* Packed weight geometry for a conv (n_pad, k_pad in floats per row). */
 int raft_conv2d_packed_shape(int mode, int n, int kh, int kw, int cin, int* n_pad, int* k_pad);

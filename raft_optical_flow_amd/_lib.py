@@ -61,6 +61,8 @@ class ConvParams(ctypes.Structure):
         ("add0", P), ("add0_ld", c_int),
         ("precision", c_int),
         ("range_flag", P),
+        ("stats_part", P), ("stats_ld", c_int),
+        ("in_norm", P), ("in_norm_relu", c_int),
     ]
 
 
@@ -78,8 +80,8 @@ _PROTOS = {
     "raft_corr_lookup_convf1": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, c_int, c_int, P, c_int, P,
                                         P, P, c_int, c_int, c_int, P, c_int, P, P]),
     "raft_convf1_flow": (c_int, [P, c_int, c_int, c_int, c_int, P, P, c_int, c_int, c_int, P, c_int, P, P]),
-    "raft_corr_lookup_conv": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P, c_int, P, P, P, c_int, c_int, P,
-                                      c_int, P, P, P, c_int, c_int, c_int, P, c_int, P, P]),
+    "raft_corr_lookup_conv": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P, c_int, P, c_int, P, P, c_int, P,
+                                      c_int, P, P, P, c_int, c_int, P, c_int, P, P]),
     "raft_lookup_conv_weight_floats": (c_size_t, [c_int, c_int]),
     "raft_lookup_conv_pack_weight": (c_int, [P, c_int, c_int, c_int, P, P]),
     "raft_alt_corr_forward": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, P]),
@@ -101,6 +103,9 @@ _PROTOS = {
                                          ctypes.POINTER(c_int)]),
     "raft_conv2d": (c_int, [ctypes.POINTER(ConvParams), P]),
     "raft_conv2d_pair": (c_int, [ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), P]),
+    "raft_conv2d_stats_slots": (c_int, [ctypes.POINTER(ConvParams)]),
+    "raft_conv2d_in_norm_ok": (c_int, [ctypes.POINTER(ConvParams)]),
+    "raft_instnorm_merge": (c_int, [P, c_int, c_int, c_int, c_int, c_float, P, P]),
     "raft_conv2d_split_weight": (c_int, [P, P, c_int, c_int, P]),
     "raft_conv2d_split_weight_prec": (c_int, [P, P, c_int, c_int, c_int, P]),
     "raft_instnorm_workspace_floats": (c_size_t, [c_int, c_int, c_int]),

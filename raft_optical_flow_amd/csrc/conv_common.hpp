@@ -216,6 +216,33 @@ __device__ __forceinline__ void tile_epilogue(const raft_conv2d_params& p, const
     if (ncol && rows[r] >= 0) dst[eidx(rows[r], ld, col)] = v[r];
 }
 
+// InstanceNorm partial statistics of one wave's 32x32 accumulator tile (raft_conv2d_stats_slots):
+// for column n, (count, mean, M2) of v = acc + bias over the wave's valid rows; lanes n and n + 32
+// hold 16 rows each.  M2 is taken around the wave's own mean (well conditioned in fp32).
+__device__ __forceinline__ void tile_stats(const raft_conv2d_params& p, const int (&rows)[16], int n,
+                                           const f32x16& acc, long slot) {
+  const bool ncol = n < p.n;
+  const float bias = p.bias ? p.bias[ncol ? n : 0] : 0.f;
+  float s = 0.f, c = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    s += rows[r] >= 0 ? acc[r] + bias : 0.f;
+    c += rows[r] >= 0 ? 1.f : 0.f;
+  }
+  s += __shfl_xor(s, 32);
+  c += __shfl_xor(c, 32);
+  const float mean = c > 0.f ? s / c : 0.f;
+  float m2 = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float d = acc[r] + bias - mean;
+    m2 += rows[r] >= 0 ? d * d : 0.f;
+  }
+  m2 += __shfl_xor(m2, 32);
+  if (ncol && (threadIdx.x & 32) == 0)
+    *reinterpret_cast<f32x4*>(p.stats_part + (slot * p.stats_ld + n) * 4) = f32x4{c, mean, m2, 0.f};
+}
+
 constexpr unsigned OFF_INVALID = 0x80000000u;  // > num_records of every buffer (host-checked)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, unsigned bytes) {
@@ -240,5 +267,11 @@ struct HaloOperands {
 int conv_halo_launch(const HaloOperands& o, hipStream_t s);
 // two independent convs of one shape class in one launch; 1 (nothing launched) if they do not qualify
 int conv_halo_launch_pair(const HaloOperands& o0, const HaloOperands& o1, hipStream_t s);
+// conv_stem.hip: the encoders' 7x7 / stride-2 stem over 3 channels; 1 (nothing launched) otherwise
+int conv_stem_launch(const raft_conv2d_params& p, int k_pad, hipStream_t s);
+// tile-statistics slots per image of a conv on the halo / stem kernel (raft_conv2d_stats_slots), 0 if none
+int conv_halo_stats_slots(const HaloOperands& o);
+bool conv_halo_norm_ok(const HaloOperands& o);
+int conv_stem_stats_slots(const raft_conv2d_params& p, int k_pad);
 
 }  // namespace raft

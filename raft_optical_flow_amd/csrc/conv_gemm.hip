@@ -911,7 +911,16 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
       hipLaunchKernelGGL(conv_smalln_kernel<4>, grid, dim3(256), 0, s, a);
     return check_launch("raft_conv2d(small n)");
   }
+  if (p.in_norm) RAFT_REQUIRE(raft_conv2d_in_norm_ok(pp), "raft_conv2d: in_norm needs a halo-kernel 3x3 conv");
+  if (p.stats_part) {
+    // InstanceNorm partials come from the halo / stem epilogues only (raft_conv2d_stats_slots)
+    RAFT_REQUIRE(raft_conv2d_stats_slots(pp) > 0,
+                 "raft_conv2d: stats_part needs a linear-epilogue conv on the halo or stem kernel");
+    RAFT_REQUIRE(p.stats_ld >= p.n && ((uintptr_t)p.stats_part & 15) == 0,
+                 "raft_conv2d: stats_ld >= n and a 16-B aligned stats_part");
+  }
   if (p.mode == RAFT_CONV_VEC && conv_halo_launch(o, s) == 0) return check_launch("raft_conv2d(halo)");
+  if (p.mode == RAFT_CONV_GATHER && conv_stem_launch(p, o.k_pad, s) == 0) return check_launch("raft_conv2d(stem)");
   a.gn = n_pad / BN;
   const long tiles = (long)cdiv(a.M, BM) * a.gn;
   RAFT_REQUIRE(tiles < (1L << 31), "raft_conv2d: too many tiles");
@@ -922,6 +931,23 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
   return check_launch("raft_conv2d");
 }
 
+extern "C" int raft_conv2d_in_norm_ok(const raft_conv2d_params* pp) {
+  ConvArgs a;
+  HaloOperands o;
+  if (!pp || conv_prepare(pp, a, o)) return 0;
+  return pp->mode == RAFT_CONV_VEC && pp->n > 4 && conv_halo_norm_ok(o) ? 1 : 0;
+}
+
+extern "C" int raft_conv2d_stats_slots(const raft_conv2d_params* pp) {
+  ConvArgs a;
+  HaloOperands o;
+  if (!pp || conv_prepare(pp, a, o)) return 0;
+  const raft_conv2d_params& p = *pp;
+  if (p.epilogue != RAFT_EPI_LINEAR || p.alpha != 1.0f || p.add0 || (p.n <= 4 && p.mode == RAFT_CONV_VEC)) return 0;
+  if (p.mode == RAFT_CONV_VEC) return conv_halo_stats_slots(o);
+  return conv_stem_stats_slots(p, o.k_pad);
+}
+
 extern "C" int raft_conv2d_pair(const raft_conv2d_params* p0, const raft_conv2d_params* p1, raft_stream_t stream) {
   ConvArgs a0, a1;
   HaloOperands o0, o1;
@@ -929,6 +955,8 @@ extern "C" int raft_conv2d_pair(const raft_conv2d_params* p0, const raft_conv2d_
   if (rc) return rc;
   rc = conv_prepare(p1, a1, o1);
   if (rc) return rc;
+  RAFT_REQUIRE(!p0->stats_part && !p1->stats_part && !p0->in_norm && !p1->in_norm,
+               "raft_conv2d_pair: no stats_part / in_norm (use raft_conv2d)");
   // one launch only when neither reads what the other writes and no element is written by both
   // (otherwise: in order, as two calls)
   const bool independent = !reads_output_of(*p1, *p0) && !reads_output_of(*p0, *p1) && !writes_overlap(*p0, *p1);

@@ -158,7 +158,10 @@ __device__ __forceinline__ void wait_vm_n(int n) {
   }
 }
 
-template <int KH, int KW, int BNT, int PREC>
+// ENC: the encoder features (InstanceNorm partial statistics in the epilogue, the input's
+// InstanceNorm applied by the 3x3 loaders); separate instantiations, so the update block's convs
+// compile exactly as without them
+template <int KH, int KW, int BNT, int PREC, bool ENC = false>
 __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
   using C = HaloCfg<KH, KW, BNT>;
   constexpr int T = C::T, U = C::U, D = C::D, PW = C::PW, NPIX = C::NPIX, PI = C::PI, PA = C::PA, SB = C::SB;
@@ -184,7 +187,10 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
   static_assert(D >= 2 && C::LDS_B + C::LDS_A <= C::LB, "LDS budget");
   static_assert(NWP >= 1 && NBI % NWP == 0, "a wave's weight pieces lie in one K-step");
   static_assert(U % 2 == 0 && (T == 1 || T >= U), "fragment parity; at most one chunk start per load set");
-  __shared__ __attribute__((aligned(1024))) char smem[C::LDS_B + C::LDS_A];
+  // (+ the input InstanceNorm table of the 3x3 convs: {mean, 1/std} of <= 256 channels)
+  constexpr int NORM_BYTES = (ENC && KH == 3 && KW == 3 && D == 3) ? 256 * 8 : 0;
+  static_assert(C::LDS_B + C::LDS_A + NORM_BYTES <= C::LB, "LDS budget with the norm table");
+  __shared__ __attribute__((aligned(1024))) char smem[C::LDS_B + C::LDS_A + NORM_BYTES];
 
 #ifdef STAMPS
   const unsigned long long r_entry = hstamp_real(), c_entry = hstamp_now();
@@ -229,6 +235,17 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
 #pragma unroll
     for (int k = 0; k < NWP; ++k) dma16(rs_w, dst + k * 1024, in ? wvoff[k] : OFF_INVALID, soff);
   };
+
+  // the input's InstanceNorm (raft_conv2d_params.in_norm: relu((x - mean) / std) applied as the
+  // loaders split the patch): this image's table into LDS, one barrier for every wave
+  float* norm_tab = reinterpret_cast<float*>(smem + C::LDS_B + C::LDS_A);
+  if constexpr (NORM_BYTES > 0) {
+    if (p.in_norm) {
+      if (loader)
+        for (int i = 64 * lw + lane; i < 2 * p.in0_c; i += 256) norm_tab[i] = p.in_norm[(long)b * 2 * p.in0_c + i];
+      __syncthreads();
+    }
+  }
 
   if (loader) {
     // ---- loader waves ------------------------------------------------------
@@ -328,13 +345,30 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
             dst[i][q] = buf_load4(s0 ? rs0 : rs1, voff, 0);
           }
       };
+      const bool nrm = NORM_BYTES > 0 && p.in_norm != nullptr;
       auto store_patch = [&](int c, const Staged& src) {
         char* base = smem + C::LDS_B + (c % PA) * (PI * 1024);
+        const bool s0 = 32 * c < in0_c;  // (the norm applies to segment 0)
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
           if (tlds[i] >= 0) {
             h8 hi, lo;
-            split8<X3, BF>(src[i][0], src[i][1], hi, lo);
+            if (nrm && s0) {
+              // channels 32c + 8g .. +7: (x - mean) * rstd, relu; padding (no pixel, or past in0_c) stays 0
+              const int ch = 32 * c + (int)tg8[i];
+              float e[8] = {src[i][0][0], src[i][0][1], src[i][0][2], src[i][0][3],
+                            src[i][1][0], src[i][1][1], src[i][1][2], src[i][1][3]};
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const bool ok = tpix[i] != OFF_INVALID && ch + j < in0_c;
+                const float2 mr = reinterpret_cast<const float2*>(norm_tab)[ok ? ch + j : 0];
+                const float v = (e[j] - mr.x) * mr.y;
+                e[j] = ok ? (p.in_norm_relu ? fmaxf(v, 0.f) : v) : 0.f;
+              }
+              split8<X3, BF>(f32x4{e[0], e[1], e[2], e[3]}, f32x4{e[4], e[5], e[6], e[7]}, hi, lo);
+            } else {
+              split8<X3, BF>(src[i][0], src[i][1], hi, lo);
+            }
             *reinterpret_cast<h8*>(base + tlds[i]) = hi;
             if constexpr (X3) *reinterpret_cast<h8*>(base + (tlds[i] ^ 64)) = lo;
           }
@@ -619,6 +653,12 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
   }
 #pragma unroll
   for (int sb = 0; sb < NSUB; ++sb) tile_epilogue(p, rows, n0 + sb * 32 + m, acc[sb]);
+  if constexpr (ENC) {
+    if (p.stats_part) {  // InstanceNorm partials of the raw output (slot: spatial tile x 4 + wave)
+#pragma unroll
+      for (int sb = 0; sb < NSUB; ++sb) tile_stats(p, rows, n0 + sb * 32 + m, acc[sb], (long)st * 4 + w);
+    }
+  }
 #ifdef STAMPS
   {
     const unsigned long long c_exit = hstamp_now(), r_exit = hstamp_real();
@@ -639,6 +679,16 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
 
 template <int KH, int KW, int PREC>
 void launch_halo_p(const HaloLaunch& l, int bn, dim3 grid, hipStream_t s) {
+  const raft_conv2d_params& p = l.a[0].p;
+  if constexpr ((KH == 1 && KW == 1) || (KH == 3 && KW == 3)) {
+    if (p.stats_part || p.in_norm) {  // (one conv per launch: raft_conv2d_pair takes neither)
+      if (bn == 64)
+        hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 64, PREC, true>), grid, dim3(512), 0, s, l);
+      else
+        hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 32, PREC, true>), grid, dim3(512), 0, s, l);
+      return;
+    }
+  }
   if (bn == 64)
     hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 64, PREC>), grid, dim3(512), 0, s, l);
   else
@@ -708,6 +758,21 @@ extern "C" int raft_debug_hstamps(unsigned long long* host, int n) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_hstamp), sizeof(unsigned long long) * (size_t)n);
 }
 #endif
+
+// whether the conv takes its input InstanceNorm in the loaders (raft_conv2d_params.in_norm): the
+// 3x3 convs' split-patch path (D = 3 for both N-tile widths), <= 256 input channels
+bool conv_halo_norm_ok(const HaloOperands& o) {
+  HaloArgs a;
+  if (!halo_enabled() || !halo_problem(o, a)) return false;
+  const raft_conv2d_params& p = o.p;
+  return p.kh == 3 && p.kw == 3 && p.in0_c <= 256 && HaloCfg<3, 3, 64>::D == 3 && HaloCfg<3, 3, 32>::D == 3;
+}
+
+int conv_halo_stats_slots(const HaloOperands& o) {
+  HaloArgs a;
+  if (!halo_enabled() || !halo_problem(o, a)) return 0;
+  return a.tx_n * a.ty_n * 4;
+}
 
 // Launches the halo kernel when the conv is one it covers; returns 1 without launching
 // otherwise.  Arguments are already validated by raft_conv2d.

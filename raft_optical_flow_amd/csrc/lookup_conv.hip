@@ -4,22 +4,29 @@
 //   cor  = relu(convc1(corr))   1x1, 324 -> 256             core/update.py:185,202
 //   flo  = relu(convf1(flow))   7x7, 2 -> 128               core/update.py:186,205
 //
-// in ONE launch, with the 324-channel correlation rows never leaving the CU: a
-// work-group owns a 2x16 tile of query pixels, gathers their windows from the
-// tiled pyramid (the lookup of corr_pyramid.hip, four pixels per wave), writes
-// the interpolated taps split into f16 hi | lo straight into an LDS A operand
-// (32 rows x 352 K), and contracts it with convc1's weight on MFMA — the weight
-// read straight from L2 into registers in MFMA-fragment order (no LDS ring: each
-// of the 8 waves owns 32 of the 256 output channels, so no two waves read the
-// same weight bytes).  convf1 runs on the VALU of the same work-group while the
-// gather's tile loads are in flight.
+// in ONE launch, with the 324-channel correlation rows never leaving the CU.  A work-group
+// (8 waves) owns a 2x16 tile of query pixels:
 //
-// Before (round 2): the lookup + convf1 launch wrote 9.1 MB of correlation rows
-// per iteration at B=1, and convc1 (its own halo-conv launch) read them back.
+//   1. every wave issues the window tiles of its four pixels (all levels, one 16-B load per
+//      lane each: the lookup of corr_pyramid.hip) and, behind them, the coords of convf1's
+//      8x22 flow patch;
+//   2. while they fly: the per-axis sampling entries (the reference's grid_sample arithmetic);
+//   3. per pixel: the tiles go to a double-buffered LDS patch, the lane's nine taps are
+//      interpolated and written, split into f16 hi | lo (the conv precision's operand format),
+//      straight into the convc1 A operand in LDS (32 rows x 352 K); meanwhile the flow patch
+//      becomes convf1's im2col A operand (32 rows x 128 K);
+//   4. both convs on MFMA: each wave owns 32 of convc1's 256 outputs (and waves 0-3 32 of
+//      convf1's 128); the weights come straight from L2 into registers in MFMA-fragment order
+//      (raft_lookup_conv_pack_weight), so no two waves read the same weight bytes and no LDS
+//      ring is needed;
+//   5. epilogues: bias + relu, range guard, NHWC rows.
 //
-// Arithmetic: the taps are the lookup kernel's (the reference's grid_sample
-// arithmetic); convc1 runs in the conv precision (f16x3: hi*hi + lo*hi + hi*lo,
-// fp32 accumulation; f16 / bf16: one product); convf1 in exact fp32 FMAs.
+// Before (round 2): the lookup + convf1 launch wrote 9.1 MB of correlation rows per iteration
+// at B=1 and convc1 (its own halo-conv launch) read them back.
+//
+// Arithmetic: the taps are the lookup kernel's; convc1 and convf1 run in the conv precision
+// (f16x3: hi*hi + lo*hi + hi*(2048 lo)/2048, fp32 accumulation, the halo kernel's split;
+// f16 / bf16: one product), as every other conv of the update block.
 #include "lookup_common.hpp"
 
 namespace raft {
@@ -30,33 +37,36 @@ constexpr int LC_R = 4, LC_L = 4, LC_RD = 9;              // RAFT-full: radius 4
 constexpr int LC_NTAP = LC_L * LC_RD * LC_RD;             // 324 correlation channels
 constexpr int LC_KS = (LC_NTAP + 31) / 32;                // 11 K-steps of 32 (K = 352)
 constexpr int LC_N = 256;                                 // convc1 outputs: 8 waves x 32
-constexpr int LC_F1N = 128;                               // convf1 outputs: 8 waves x 16
+constexpr int LC_F1N = 128;                               // convf1 outputs: waves 0-3 x 32
 constexpr int LC_F1K = 7, LC_F1KK = 49;
+constexpr int LC_F1KS = (2 * LC_F1KK + 31) / 32;          // convf1: K = 98 -> 4 K-steps (128)
 constexpr int LC_FPH = LC_TH + LC_F1K - 1, LC_FPW = LC_TW + LC_F1K - 1;  // 8 x 22 flow patch
 constexpr int LC_PX = 4;                                  // query pixels per wave
 
 // LDS (bytes)
-constexpr int LC_A_BYTES = LC_KS * LC_M * 128;                       // A operand: 45056
-constexpr int LC_W1_BYTES = LC_F1N * LC_F1KK * 2 * 4;                // convf1 weights: 50176
+constexpr int LC_A_BYTES = LC_KS * LC_M * 128;                       // convc1 A operand: 45056
+constexpr int LC_A1_BYTES = LC_F1KS * LC_M * 128;                    // convf1 A operand: 16384
 constexpr int LC_FL_BYTES = LC_FPH * LC_FPW * 8;                     // flow patch: 1408
 constexpr int LC_PATCH_FLOATS = 16 * patch_rs<4>();                  // one pixel's window patch
-constexpr int LC_PATCH_BYTES = 8 * LC_PATCH_FLOATS * 4;              // 34816
+constexpr int LC_PATCH_BYTES = 8 * 2 * LC_PATCH_FLOATS * 4;          // two per wave: 69632
 constexpr int LC_YT_BYTES = 8 * LC_PX * LC_L * LC_RD * 16;           // y-entries: 18432
-constexpr int LC_OFF_W1 = LC_A_BYTES, LC_OFF_FL = LC_OFF_W1 + LC_W1_BYTES, LC_OFF_PATCH = LC_OFF_FL + LC_FL_BYTES,
+constexpr int LC_OFF_A1 = LC_A_BYTES, LC_OFF_FL = LC_OFF_A1 + LC_A1_BYTES, LC_OFF_PATCH = LC_OFF_FL + LC_FL_BYTES,
               LC_OFF_YT = LC_OFF_PATCH + LC_PATCH_BYTES, LC_LDS = LC_OFF_YT + LC_YT_BYTES;
 static_assert(LC_LDS <= 160 * 1024, "LDS budget");
-static_assert(LC_PATCH_FLOATS >= 4 * LC_KS * 8, "the staging row fits a consumed patch");
 
 struct LookupConvArgs {
-  LookupArgs a;        // pyramid geometry, coords (NHWC), flow output, lookup range flag
-  const h8* wfrag;     // convc1 weight, fragment order [KS][8][4][64] x 16 B (raft_lookup_conv_pack_weight)
-  const float* bias;   // convc1 bias [256] or null
-  float* out;          // convc1 output rows (relu), [B*H*W][out_ld]
+  LookupArgs a;         // pyramid geometry, coords (NHWC), flow output, lookup range flag
+  const h8* wfrag;      // convc1 weight, fragment order [11][8][4][64] x 16 B (raft_lookup_conv_pack_weight)
+  const float* bias;    // convc1 bias [256] or null
+  float* out;           // convc1 output rows (relu), [B*H*W][out_ld]
   int out_ld;
-  int* out_flag;       // range guard of the convc1 output (feeds the split convc2), or null
-  FlowConvArgs f;      // convf1 (n = 128, k = 7)
-  int tx_n, ty_n;      // pixel tiles per image row / column
-  int ntiles;
+  int* out_flag;        // range guard of the convc1 output (feeds the split convc2), or null
+  const h8* f1frag;     // convf1 weight, fragment order [4][4][4][64] x 16 B
+  const float* f1bias;  // [128] or null
+  float* f1out;
+  int f1out_ld;
+  int* f1flag;
+  int tx_n, ty_n;       // pixel tiles per image row / column
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -65,8 +75,15 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, void* lds, unsigned voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+// f16 / bf16 hi (and f16x3 lo = f16(x - hi), unscaled, as split8) of one activation
+template <bool X3, bool BF>
+__device__ __forceinline__ void split1(float x, _Float16& hi, _Float16& lo) {
+  if constexpr (BF) {
+    hi = __builtin_bit_cast(_Float16, (__bf16)x);
+  } else {
+    hi = (_Float16)x;
+    if constexpr (X3) lo = (_Float16)(x - (float)hi);
+  }
 }
 
 #ifdef LC_STAMPS  // dev-only phase timing (tools/lc_stamps.py with a -DLC_STAMPS variant)
@@ -103,7 +120,6 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
   constexpr int R = LC_R, RD = LC_RD, WD = 2 * R + 2, RS = patch_rs<4>();
   __shared__ __attribute__((aligned(1024))) char smem[LC_LDS];
   const LookupArgs& a = g.a;
-  const FlowConvArgs& f = g.f;
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
@@ -112,76 +128,47 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
   const int y0 = (sr / g.tx_n) * LC_TH, x0 = (sr % g.tx_n) * LC_TW;
   const int H = a.H, W = a.W, P = H * W;
 
-  // ---- 1. loads, in the order they are waited for ------------------------------------------
-  // (a) convf1's weights -> LDS by DMA (49 KiB pieces over the 8 waves)
-  {
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(f.w), (short)0,
-                                                                        LC_W1_BYTES, 0x00020000);
-    for (int pc = wv; pc < LC_W1_BYTES / 1024; pc += 8)
-      dma16(rs, smem + LC_OFF_W1 + pc * 1024, (unsigned)(pc * 1024 + lane * 16));
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  // (b) the coords of convf1's 8x22 flow patch (zero padded), threads 0 .. 175
-  const int fi = threadIdx.x;
-  const int fyy = y0 - 3 + fi / LC_FPW, fxx = x0 - 3 + fi % LC_FPW;
-  const bool fin = fi < LC_FPH * LC_FPW && (unsigned)fyy < (unsigned)H && (unsigned)fxx < (unsigned)W;
-  f32x2 fc = {0.f, 0.f};
-  if (fin) fc = *reinterpret_cast<const f32x2*>(a.coords + 2L * ((long)b * P + fyy * W + fxx));
-  // (c) convc1's weight fragments of K-steps 0 and 1 (this wave's 32 output channels)
-  h8 wb[3][NT];
-  auto load_w = [&](int j, h8 (&dst)[NT]) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) dst[t] = g.wfrag[((j * 8 + wv) * 4 + t) * 64 + lane];
-  };
-  load_w(0, wb[0]);
-  load_w(1, wb[1]);
-  __builtin_amdgcn_sched_barrier(0);  // (a) .. (c) are issued before the tile loads: vmcnt(16) below
-  // (d) the windows of this wave's four query pixels, every level, one 16-B load per lane each
+  // ---- 1. the window tiles of this wave's four query pixels (the critical path) --------------
   const int ti = lane >> 4, tj = (lane >> 2) & 3, rr = lane & 3;
   const int lrow = ti * 4 + rr;
+  // per-level map geometry in registers up front (re-read from the kernel arguments inside the
+  // pixel loop, each read is a scalar-cache round trip)
+  int lth[LC_L], ltw[LC_L];
+  unsigned lmsz[LC_L];
+  const float* lbs[LC_L];
+#pragma unroll
+  for (int l = 0; l < LC_L; ++l) {
+    lth[l] = a.lv[l].th;
+    ltw[l] = a.lv[l].tw;
+    lmsz[l] = (unsigned)a.lv[l].mapsz;
+    lbs[l] = a.lbase[l];
+  }
   float px_x[LC_PX], px_y[LC_PX];
   int px_gp[LC_PX];
   bool px_ok[LC_PX];
-  f32x4 v[LC_PX][LC_L];
+  // the four pixels' coords, every load issued before the first is used (uniform: scalar loads)
 #pragma unroll
   for (int k = 0; k < LC_PX; ++k) {
-    const int m = LC_PX * wv + k;
-    const int yy = y0 + (m >> 4), xx = x0 + (m & 15);
+    const int mk = LC_PX * wv + k;
+    const int yy = y0 + (mk >> 4), xx = x0 + (mk & 15);
     const bool ok = yy < H && xx < W;
-    const int gp = ok ? b * P + yy * W + xx : b * P;
     px_ok[k] = ok;
-    px_gp[k] = gp;
-    const float x = a.coords[2L * gp], y = a.coords[2L * gp + 1];
-    px_x[k] = x;
-    px_y[k] = y;
-    const int xf = __builtin_amdgcn_readfirstlane((int)floorf(x));
-    const int yf = __builtin_amdgcn_readfirstlane((int)floorf(y));
+    px_gp[k] = ok ? b * P + yy * W + xx : b * P;
+  }
+  {
+    // one round trip: lane k < 4 loads pixel k's x and y (two 4-B loads), then lane reads
+    int gk = px_gp[0];
 #pragma unroll
-    for (int l = 0; l < LC_L; ++l) {
-      const int wx0 = (xf >> l) - R, wy0 = (yf >> l) - R;
-      const int tyo = wy0 >> 2, txo = wx0 >> 2;
-      const int ntx = ((wx0 + WD - 1) >> 2) - txo + 1;
-      const Level& lv = a.lv[l];
-      // (the scalar-interval window test of corr_lookup_kernel<..., SCAL>)
-      const int rlo = max(wy0, 0), rhi = min(wy0 + WD, 4 * lv.th);
-      const int clo = max(txo, 0), chi = min(txo + ntx, lv.tw);
-      const int rb = __builtin_amdgcn_readfirstlane(rlo - 4 * tyo), cb = __builtin_amdgcn_readfirstlane(clo - txo);
-      const bool tok = ok && ((unsigned)(lrow - rb) < (unsigned)max(rhi - rlo, 0)) &&
-                       ((unsigned)(tj - cb) < (unsigned)max(chi - clo, 0));
-      const float* wbase = a.lbase[l] + (long)((unsigned long long)(unsigned)gp * (unsigned)lv.mapsz) +
-                           ((long)tyo * lv.tw + txo) * 16;
-      const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wbase), (short)0, 0x7FFFFFFF, 0x00020000);
-      const unsigned off = tok ? __umul24((unsigned)ti, (unsigned)(64 * lv.tw)) + 16u * (unsigned)(lane & 15)
-                               : 0x80000000u;
-      v[k][l] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    for (int k = 1; k < LC_PX; ++k) gk = (lane & 3) == k ? px_gp[k] : gk;
+    const float cx = a.coords[2L * gk], cy = a.coords[2L * gk + 1];
+#pragma unroll
+    for (int k = 0; k < LC_PX; ++k) {
+      px_x[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cx), k));
+      px_y[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cy), k));
     }
   }
-
-  LC_STAMP(1);
-  // ---- 2. while the tiles fly: the per-axis sampling entries of the four pixels ------------
-  // lane (l, ix) = (lane / 9, lane % 9), lanes 0 .. 35: x-entry ix kept in registers, y-entry
-  // ix through LDS (the reference's arithmetic, see axis_entry)
+  // the small loads the waits below need before the tiles (loads return in order):
+  // this lane's level constants, the coords of convf1's 8x22 flow patch (threads 0 .. 175), the biases
   const bool col = lane < LC_L * RD;
   int lq = 0;
 #pragma unroll
@@ -189,6 +176,46 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
   const int l = col ? lq : 0;
   const int ix = lane - l * RD;
   const f32x4 prm = a.prm[l];
+  const int fi = threadIdx.x;
+  const int fyy = y0 - 3 + fi / LC_FPW, fxx = x0 - 3 + fi % LC_FPW;
+  const bool fin = fi < LC_FPH * LC_FPW && (unsigned)fyy < (unsigned)H && (unsigned)fxx < (unsigned)W;
+  f32x2 fc = {0.f, 0.f};
+  if (fin) fc = *reinterpret_cast<const f32x2*>(a.coords + 2L * ((long)b * P + fyy * W + fxx));
+  const int m = lane & 31, h = lane >> 5;
+  const float c1b = g.bias ? g.bias[32 * wv + m] : 0.f;
+  const float f1b = (wv < 4 && g.f1bias) ? g.f1bias[32 * wv + m] : 0.f;
+
+  __builtin_amdgcn_sched_barrier(0);
+  f32x4 v[LC_PX][LC_L];
+#pragma unroll
+  for (int k = 0; k < LC_PX; ++k) {
+    const bool ok = px_ok[k];
+    const int gp = px_gp[k];
+    const int xf = __builtin_amdgcn_readfirstlane((int)floorf(px_x[k]));
+    const int yf = __builtin_amdgcn_readfirstlane((int)floorf(px_y[k]));
+#pragma unroll
+    for (int l = 0; l < LC_L; ++l) {
+      const int wx0 = (xf >> l) - R, wy0 = (yf >> l) - R;
+      const int tyo = wy0 >> 2, txo = wx0 >> 2;
+      const int ntx = ((wx0 + WD - 1) >> 2) - txo + 1;
+      // (the scalar-interval window test of corr_lookup_kernel<..., SCAL>)
+      const int rlo = max(wy0, 0), rhi = min(wy0 + WD, 4 * lth[l]);
+      const int clo = max(txo, 0), chi = min(txo + ntx, ltw[l]);
+      const int rb = __builtin_amdgcn_readfirstlane(rlo - 4 * tyo), cb = __builtin_amdgcn_readfirstlane(clo - txo);
+      const bool tok = ok && ((unsigned)(lrow - rb) < (unsigned)max(rhi - rlo, 0)) &&
+                       ((unsigned)(tj - cb) < (unsigned)max(chi - clo, 0));
+      const float* wbase = lbs[l] + (long)((unsigned long long)(unsigned)gp * lmsz[l]) + ((long)tyo * ltw[l] + txo) * 16;
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wbase), (short)0, 0x7FFFFFFF, 0x00020000);
+      const unsigned off = tok ? __umul24((unsigned)ti, (unsigned)(64 * ltw[l])) + 16u * (unsigned)(lane & 15)
+                               : 0x80000000u;
+      v[k][l] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    }
+  }
+  LC_STAMP(1);
+  // ---- 2. while the tiles fly: the per-axis sampling entries of the four pixels ------------
+  // lane (l, ix) = (lane / 9, lane % 9), lanes 0 .. 35: x-entry ix kept in registers, y-entry
+  // ix through LDS (the reference's arithmetic, see axis_entry)
   int4* ytab = reinterpret_cast<int4*>(smem + LC_OFF_YT) + wv * LC_PX * LC_L * RD;
   int xw[LC_PX], xi[LC_PX];
   float xt[LC_PX];
@@ -205,72 +232,43 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
     onp[k] = xw[k] >= 0 && yw >= 0;
     if (col) ytab[k * LC_L * RD + lane] = int4{yw >= 0 ? yw * RS * 4 : yw, __float_as_int(yt), __float_as_int(1.0f - yt), yi};
   }
-
-  LC_STAMP(2);
-  // ---- 3. convf1 on the VALU (weights + flow patch: the loads of (a), (b)) ------------------
-  __builtin_amdgcn_s_waitcnt(0x0F70 | (LC_PX * LC_L & 15) | ((LC_PX * LC_L >> 4) << 14));  // vmcnt(16): all but the tiles
+  // the flow patch (coords - grid, zero padded)
   float2* fl = reinterpret_cast<float2*>(smem + LC_OFF_FL);
   if (fi < LC_FPH * LC_FPW) {
     float2 fv = {0.f, 0.f};
     if (fin) {
-      fv.x = round_operand(fc[0] - (float)fxx, f.rnd);
-      fv.y = round_operand(fc[1] - (float)fyy, f.rnd);
+      fv.x = fc[0] - (float)fxx;
+      fv.y = fc[1] - (float)fyy;
     }
     fl[fi] = fv;
   }
-  __syncthreads();  // the DMA'd weights and the flow patch are visible
-  LC_STAMP(3);
-  const int fh = lane >> 5, fm = lane & 31;
-  const int fc0 = 16 * wv + 8 * fh;  // this lane's 8 convf1 channels
-  float f1acc[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) f1acc[j] = 0.f;
-  {
-    const float* wl = reinterpret_cast<const float*>(smem + LC_OFF_W1) + (fc0 >> 5) * LC_F1KK * 2 * 32 + (fc0 & 31);
-    const int fpy = fm >> 4, fpx = fm & 15;
-#pragma unroll 1
-    for (int dy = 0; dy < LC_F1K; ++dy) {
-      const float2* row = fl + (fpy + dy) * LC_FPW + fpx;
-      const float* wr = wl + dy * LC_F1K * 2 * 32;
-#pragma unroll
-      for (int dx = 0; dx < LC_F1K; ++dx) {
-        const float2 fv = row[dx];
-        const f32x4 w0a = *reinterpret_cast<const f32x4*>(wr + dx * 64);
-        const f32x4 w0b = *reinterpret_cast<const f32x4*>(wr + dx * 64 + 4);
-        const f32x4 w1a = *reinterpret_cast<const f32x4*>(wr + dx * 64 + 32);
-        const f32x4 w1b = *reinterpret_cast<const f32x4*>(wr + dx * 64 + 36);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          f1acc[j] = fmaf(fv.x, w0a[j], f1acc[j]);
-          f1acc[4 + j] = fmaf(fv.x, w0b[j], f1acc[4 + j]);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          f1acc[j] = fmaf(fv.y, w1a[j], f1acc[j]);
-          f1acc[4 + j] = fmaf(fv.y, w1b[j], f1acc[4 + j]);
-        }
-      }
-    }
-  }
+  LC_STAMP(2);
 
-  // ---- 4. the taps of each pixel -> split rows of the A operand -----------------------------
-#ifdef LC_STAMPS
-  asm volatile("" ::"v"(f1acc[0]), "v"(f1acc[7]));
-#endif
-  LC_STAMP(4);
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the tiles have landed
-  LC_STAMP(5);
-  float* patch = reinterpret_cast<float*>(smem + LC_OFF_PATCH) + wv * LC_PATCH_FLOATS;
+  // ---- 3. the taps of each pixel -> split rows of convc1's A operand ------------------------
+  // The K stream of step 4, in registers: convc1's 11 K-steps (all waves) then convf1's 4 (waves
+  // 0-3), prefetched PF steps ahead; the first PF steps are issued here, behind the tiles, so they
+  // land during the taps.
+  constexpr int PF = 3;
+  h8 wb[PF + 1][NT];
+  auto load_w = [&](int j, h8 (&dst)[NT]) {
+    const h8* wf = j < LC_KS ? g.wfrag + ((j * (LC_N / 32) + wv) * 4) * 64
+                             : g.f1frag + (((j - LC_KS) * (LC_F1N / 32) + wv) * 4) * 64;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) dst[t] = wf[t * 64 + lane];
+  };
+#pragma unroll
+  for (int j = 0; j < PF; ++j) load_w(j, wb[j]);
   char* Abase = smem;
   bool big = false;
-#pragma unroll
-  for (int k = 0; k < LC_PX; ++k) {
-    const int m = LC_PX * wv + k;
-#pragma unroll
-    for (int lv_ = 0; lv_ < LC_L; ++lv_) *reinterpret_cast<f32x4*>(&patch[pidx<4>(lrow, tj * 4, lv_)]) = v[k][lv_];
-    wave_sync();
+  auto patch_of = [&](int k) {
+    return reinterpret_cast<float*>(smem + LC_OFF_PATCH) + (wv * 2 + (k & 1)) * LC_PATCH_FLOATS;
+  };
+  // this lane's nine output channels c = l*81 + ix*9 + iy
+  const int cbase = l * RD * RD + ix * RD;
+  // the nine taps of pixel k from its staged patch
+  auto taps = [&](int k, float (&val)[RD]) {
+    const float* patch = patch_of(k);
     const int4* yt = ytab + k * LC_L * RD;
-    float val[RD];
     const float ex = 1.0f - xt[k];
     const int xwk = xw[k];
     // the common case: every entry of the wave is finite and on the patch
@@ -324,127 +322,157 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
         }
       }
     }
+  };
+  // pixel k's taps, split, straight into its row of the A operand (2-B writes); lanes 36 .. 63
+  // write the row's zero K padding (channels 324 .. 351)
+  auto write_row = [&](int k, const float (&val)[RD]) {
+    const int mk = LC_PX * wv + k;
+    const int sw = (mk >> 1) & 7;
     if (col) {
 #pragma unroll
-      for (int iy = 0; iy < RD; ++iy) big |= fabsf(val[iy]) > RAFT_RANGE_LIMIT;
-    }
-    // the pixel's 324 taps through the (consumed) patch as an fp32 row, then 8-channel
-    // chunks split into f16 hi | lo quads of the A operand's K-step blocks
-    wave_sync();
-    if (col) {
-#pragma unroll
-      for (int iy = 0; iy < RD; ++iy) patch[l * RD * RD + ix * RD + iy] = px_ok[k] ? val[iy] : 0.f;
-    }
-    wave_sync();
-    if (lane < 4 * LC_KS) {
-      const int c = 8 * lane;
-      f32x4 q0 = *reinterpret_cast<const f32x4*>(patch + c);
-      f32x4 q1 = *reinterpret_cast<const f32x4*>(patch + c + 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        q0[e] = c + e < LC_NTAP ? q0[e] : 0.f;
-        q1[e] = c + 4 + e < LC_NTAP ? q1[e] : 0.f;
+      for (int iy = 0; iy < RD; ++iy) {
+        const float vv = px_ok[k] ? val[iy] : 0.f;
+        big |= fabsf(vv) > RAFT_RANGE_LIMIT;
+        const int c = cbase + iy;
+        const int j = c >> 5, kk = c & 31;
+        _Float16 hi, lo;
+        split1<X3, BF>(vv, hi, lo);
+        char* rb = Abase + j * (LC_M * 128) + mk * 128;
+        *reinterpret_cast<_Float16*>(rb + (((kk >> 3) ^ sw) << 4) + 2 * (kk & 7)) = hi;
+        if constexpr (X3) *reinterpret_cast<_Float16*>(rb + (((4 + (kk >> 3)) ^ sw) << 4) + 2 * (kk & 7)) = lo;
       }
-      h8 hi, lo;
-      split8<X3, BF>(q0, q1, hi, lo);
-      const int j = lane >> 2, qd = lane & 3, sw = (m >> 1) & 7;
-      char* row = Abase + j * (LC_M * 128) + m * 128;
-      *reinterpret_cast<h8*>(row + ((qd ^ sw) << 4)) = hi;
-      if constexpr (X3) *reinterpret_cast<h8*>(row + (((4 + qd) ^ sw) << 4)) = lo;
+    } else if (lane - LC_L * RD < 32 * LC_KS - LC_NTAP) {
+      const int c = LC_NTAP + lane - LC_L * RD;
+      const int j = c >> 5, kk = c & 31;
+      char* rb = Abase + j * (LC_M * 128) + mk * 128;
+      *reinterpret_cast<_Float16*>(rb + (((kk >> 3) ^ sw) << 4) + 2 * (kk & 7)) = (_Float16)0.f;
+      if constexpr (X3) *reinterpret_cast<_Float16*>(rb + (((4 + (kk >> 3)) ^ sw) << 4) + 2 * (kk & 7)) = (_Float16)0.f;
     }
     if (a.flow && lane < 2 && px_ok[k]) {
       const int p = px_gp[k] - b * P;
       const float gcoord = lane == 0 ? (float)(p % W) : (float)(p / W);
       a.flow[(long)px_gp[k] * a.flow_ld + lane] = (lane == 0 ? px_x[k] : px_y[k]) - gcoord;
     }
-    wave_sync();  // the chunk reads are done before the next pixel's patch lands
+  };
+  // two pixels per round: both patches staged, one wave sync, both pixels' taps interleaved
+#pragma unroll
+  for (int k = 0; k < LC_PX; k += 2) {
+#pragma unroll
+    for (int lv_ = 0; lv_ < LC_L; ++lv_) {
+      *reinterpret_cast<f32x4*>(&patch_of(k)[pidx<4>(lrow, tj * 4, lv_)]) = v[k][lv_];
+      *reinterpret_cast<f32x4*>(&patch_of(k + 1)[pidx<4>(lrow, tj * 4, lv_)]) = v[k + 1][lv_];
+    }
+    wave_sync();
+    float va[RD], vb[RD];
+    taps(k, va);
+    taps(k + 1, vb);
+    write_row(k, va);
+    write_row(k + 1, vb);
+    wave_sync();  // (the patches are read before the next round overwrites them)
   }
   if (a.range_flag && big) *a.range_flag = 1;
-  LC_STAMP(6);
-  __syncthreads();  // every A row is in LDS
-  LC_STAMP(7);
-
-  // ---- 5. convc1: [32 x 352] x [352 x 32] per wave on MFMA, weights from L2 ------------------
-  const int m = lane & 31, h = lane >> 5;
-  const int sw = (m >> 1) & 7;
-  f32x16 acc = {}, accx = {};
+  LC_STAMP(3);
+  __syncthreads();  // the flow patch is visible
+  // convf1's im2col A operand: row mm, K = 2 (dy*7 + dx) + ci (the GATHER packing), 8 K per thread
+  {
+    const int mm = threadIdx.x >> 4, q = threadIdx.x & 15;
+    const int py = mm >> 4, px = mm & 15;
+    float e[8];
 #pragma unroll
-  for (int j = 0; j < LC_KS; ++j) {
-    if (j + 2 < LC_KS) load_w(j + 2, wb[(j + 2) % 3]);
-    const char* row = Abase + j * (LC_M * 128) + m * 128;
+    for (int i = 0; i < 8; ++i) {
+      const int k = 8 * q + i, t = k >> 1;
+      const int dy = t / LC_F1K, dx = t - dy * LC_F1K;
+      const float2 fv = fl[(py + (k < 2 * LC_F1KK ? dy : 0)) * LC_FPW + px + (k < 2 * LC_F1KK ? dx : 0)];
+      e[i] = k < 2 * LC_F1KK ? ((k & 1) ? fv.y : fv.x) : 0.f;
+    }
+    h8 hi, lo;
+    split8<X3, BF>(f32x4{e[0], e[1], e[2], e[3]}, f32x4{e[4], e[5], e[6], e[7]}, hi, lo);
+    const int j = q >> 2, qd = q & 3, sw = (mm >> 1) & 7;
+    char* row = smem + LC_OFF_A1 + j * (LC_M * 128) + mm * 128;
+    *reinterpret_cast<h8*>(row + ((qd ^ sw) << 4)) = hi;
+    if constexpr (X3) *reinterpret_cast<h8*>(row + (((4 + qd) ^ sw) << 4)) = lo;
+  }
+  __syncthreads();  // every A row is in LDS
+  LC_STAMP(4);
+
+  // ---- 4. convc1 (all waves, 32 outputs each) then convf1 (waves 0-3) on MFMA: one K stream ----
+  const int sw = (m >> 1) & 7;
+  auto kstep = [&](const char* A, const h8 (&B)[NT], f32x16& c, f32x16& cx) {
+    const char* row = A + m * 128;
     h8 ah[2], al[2];
 #pragma unroll
     for (int qq = 0; qq < 2; ++qq) {
       ah[qq] = *reinterpret_cast<const h8*>(row + (((2 * h + qq) ^ sw) << 4));
       if constexpr (X3) al[qq] = *reinterpret_cast<const h8*>(row + (((4 + 2 * h + qq) ^ sw) << 4));
     }
-    const h8(&B)[NT] = wb[j % 3];
 #pragma unroll
     for (int qq = 0; qq < 2; ++qq) {
       if constexpr (BF) {
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8, ah[qq]), __builtin_bit_cast(bf8, B[qq]),
-                                                      acc, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8, ah[qq]), __builtin_bit_cast(bf8, B[qq]), c,
+                                                    0, 0, 0);
       } else {
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[qq], B[qq], acc, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[qq], B[qq], c, 0, 0, 0);
       }
       if constexpr (X3) {
-        accx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[qq], B[2 + qq], accx, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[qq], B[qq], acc, 0, 0, 0);
+        cx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[qq], B[2 + qq], cx, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[qq], B[qq], c, 0, 0, 0);
       }
+    }
+  };
+  f32x16 acc = {}, accx = {}, facc = {}, faccx = {};
+  const bool f1w = wv < LC_F1N / 32;  // (wave-uniform)
+#pragma unroll
+  for (int j = 0; j < LC_KS; ++j) {
+    // (the K stream continues into convf1's steps on waves 0-3)
+    if (j + PF < LC_KS || f1w) load_w(j + PF, wb[(j + PF) % (PF + 1)]);
+    kstep(Abase + j * (LC_M * 128), wb[j % (PF + 1)], acc, accx);
+  }
+  if (f1w) {
+#pragma unroll
+    for (int j = LC_KS; j < LC_KS + LC_F1KS; ++j) {
+      if (j + PF < LC_KS + LC_F1KS) load_w(j + PF, wb[(j + PF) % (PF + 1)]);
+      kstep(smem + LC_OFF_A1 + (j - LC_KS) * (LC_M * 128), wb[j % (PF + 1)], facc, faccx);
     }
   }
   if constexpr (X3) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] += accx[r] * (1.0f / SPLIT_SCALE);
+    for (int r = 0; r < 16; ++r) {
+      acc[r] += accx[r] * (1.0f / SPLIT_SCALE);
+      facc[r] += faccx[r] * (1.0f / SPLIT_SCALE);
+    }
   }
-
 #ifdef LC_STAMPS
-  asm volatile("" ::"v"(acc[0]), "v"(acc[15]));
+  asm volatile("" ::"v"(acc[0]), "v"(acc[15]), "v"(facc[0]));
 #endif
-  LC_STAMP(8);
-  // ---- 6. epilogues: convc1 (bias, relu) and convf1 -----------------------------------------
-  {
-    const int n = 32 * wv + m;
-    const float bias = g.bias ? g.bias[n] : 0.f;
+  LC_STAMP(5);
+
+  // ---- 5. epilogues: bias, relu, range guard, NHWC rows ----------------------------------------
+  auto store = [&](const f32x16& c, float bias, float* out, int ld, int n, int* flag) {
     bool obig = false;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int mm = (r & 3) + 8 * (r >> 2) + 4 * h;
       const int yy = y0 + (mm >> 4), xx = x0 + (mm & 15);
-      const float o = fmaxf(acc[r] + bias, 0.f);
+      const float o = fmaxf(c[r] + bias, 0.f);
       if (yy < H && xx < W) {
         obig |= o > RAFT_RANGE_LIMIT;
-        g.out[((long)b * P + yy * W + xx) * g.out_ld + n] = o;
+        out[((long)b * P + yy * W + xx) * ld + n] = o;
       }
     }
-    if (g.out_flag && obig) *g.out_flag = 1;
-  }
-  {
-    const int oy = y0 + (fm >> 4), ox = x0 + (fm & 15);
-    if (oy < H && ox < W) {
-      float o[8];
-      bool fbig = false;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        o[j] = fmaxf(f1acc[j] + (f.bias ? f.bias[fc0 + j] : 0.f), 0.f);
-        fbig |= o[j] > RAFT_RANGE_LIMIT;
-      }
-      if (f.range_flag && fbig) *f.range_flag = 1;
-      float* dst = f.out + ((long)b * P + oy * W + ox) * f.out_ld + fc0;
-      *reinterpret_cast<f32x4*>(dst) = f32x4{o[0], o[1], o[2], o[3]};
-      *reinterpret_cast<f32x4*>(dst + 4) = f32x4{o[4], o[5], o[6], o[7]};
-    }
-  }
+    if (flag && obig) *flag = 1;
+  };
+  store(acc, c1b, g.out, g.out_ld, 32 * wv + m, g.out_flag);
+  if (wv < LC_F1N / 32) store(facc, f1b, g.f1out, g.f1out_ld, 32 * wv + m, g.f1flag);
 #ifdef LC_STAMPS
   __builtin_amdgcn_s_waitcnt(0);
-  LC_STAMP(9);
+  LC_STAMP(6);
   const unsigned long long lc_r1 = lc_real();
   const unsigned wid = blockIdx.x * 8 + wv;
   if (lane == 0 && wid < 16384) {
     unsigned long long* gs = g_lcstamp + wid * 16;
     gs[0] = lc_r0;
     gs[1] = lc_r1;
-    for (int k = 0; k < 10; ++k) gs[2 + k] = lc_t[k];
+    for (int k = 0; k < 7; ++k) gs[2 + k] = lc_t[k];
   }
 #endif
 }
@@ -473,9 +501,9 @@ extern "C" int raft_debug_lcstamps(unsigned long long* host, int n) {
 }
 #endif
 
-extern "C" size_t raft_lookup_conv_weight_floats(int n, int cin) {
-  if (n <= 0 || n % 32 || cin <= 0) return 0;
-  return (size_t)((cin + 31) / 32) * (size_t)n * 32;
+extern "C" size_t raft_lookup_conv_weight_floats(int n, int k_pad) {
+  if (n <= 0 || n % 32 || k_pad <= 0) return 0;
+  return (size_t)((k_pad + 31) / 32) * (size_t)n * 32;
 }
 
 extern "C" int raft_lookup_conv_pack_weight(const void* split_weight, int n_pad, int k_pad, int n, void* out,
@@ -491,41 +519,44 @@ extern "C" int raft_lookup_conv_pack_weight(const void* split_weight, int n_pad,
 }
 
 extern "C" int raft_corr_lookup_conv(const float* pyramid, int B, int H, int W, int L, int radius, const float* coords,
-                                     float* flow_out, int flow_ld, int* range_flag, const void* c1_weight,
-                                     const float* c1_bias, int c1_n, int c1_precision, float* c1_out, int c1_out_ld,
-                                     int* c1_range_flag, const float* f1_weight, const float* f1_bias, int f1_n,
-                                     int f1_k, int f1_precision, float* f1_out, int f1_out_ld, int* f1_range_flag,
+                                     float* flow_out, int flow_ld, int* range_flag, int precision,
+                                     const void* c1_weight, const float* c1_bias, int c1_n, float* c1_out,
+                                     int c1_out_ld, int* c1_range_flag, const void* f1_weight, const float* f1_bias,
+                                     int f1_n, int f1_k, float* f1_out, int f1_out_ld, int* f1_range_flag,
                                      raft_stream_t stream) {
   RAFT_REQUIRE(L == LC_L && radius == LC_R, "raft_corr_lookup_conv: radius 4 and 4 levels only (got %d, %d)", radius,
                L);
-  RAFT_REQUIRE(c1_n == LC_N && f1_n == LC_F1N, "raft_corr_lookup_conv: convc1 256 / convf1 128 outputs only");
-  RAFT_REQUIRE(c1_precision == RAFT_PREC_F16X3 || c1_precision == RAFT_PREC_F16 || c1_precision == RAFT_PREC_BF16,
-               "raft_corr_lookup_conv: convc1 precision must be F16X3, F16 or BF16 (got %d)", c1_precision);
-  RAFT_REQUIRE(c1_weight && c1_out && c1_out_ld >= c1_n, "raft_corr_lookup_conv: bad convc1 arguments");
-  RAFT_REQUIRE((((uintptr_t)c1_weight | (uintptr_t)coords) & 15) == 0 && ((uintptr_t)coords & 7) == 0,
-               "raft_corr_lookup_conv: 16-B aligned weight / coords");
+  RAFT_REQUIRE(c1_n == LC_N && f1_n == LC_F1N && f1_k == LC_F1K,
+               "raft_corr_lookup_conv: convc1 256 / convf1 128 outputs, convf1 7x7 only");
+  RAFT_REQUIRE(precision == RAFT_PREC_F16X3 || precision == RAFT_PREC_F16 || precision == RAFT_PREC_BF16,
+               "raft_corr_lookup_conv: precision must be F16X3, F16 or BF16 (got %d)", precision);
+  RAFT_REQUIRE(c1_weight && c1_out && c1_out_ld >= c1_n && f1_weight && f1_out && f1_out_ld >= f1_n,
+               "raft_corr_lookup_conv: bad conv arguments");
+  RAFT_REQUIRE((((uintptr_t)c1_weight | (uintptr_t)f1_weight) & 15) == 0 && ((uintptr_t)coords & 7) == 0,
+               "raft_corr_lookup_conv: 16-B aligned weights, 8-B aligned coords");
   LookupConvArgs g;
-  // (the lookup's own output is never written: out = the convc1 rows, checked as a dummy)
+  // (the lookup's own output is never written: out = the convc1 rows, checked as a stand-in)
   int rc = lookup_args(g.a, pyramid, B, H, W, L, radius, coords, 0, c1_out, LC_NTAP, 0, flow_out, flow_ld, range_flag);
-  if (rc) return rc;
-  rc = flowconv_args(g.f, "raft_corr_lookup_conv", B, H, W, f1_weight, f1_bias, f1_n, f1_k, f1_precision, f1_out,
-                     f1_out_ld, f1_range_flag);
   if (rc) return rc;
   g.wfrag = reinterpret_cast<const h8*>(c1_weight);
   g.bias = c1_bias;
   g.out = c1_out;
   g.out_ld = c1_out_ld;
   g.out_flag = c1_range_flag;
+  g.f1frag = reinterpret_cast<const h8*>(f1_weight);
+  g.f1bias = f1_bias;
+  g.f1out = f1_out;
+  g.f1out_ld = f1_out_ld;
+  g.f1flag = f1_range_flag;
   g.tx_n = cdiv(W, LC_TW);
   g.ty_n = cdiv(H, LC_TH);
   const long nt = (long)B * g.tx_n * g.ty_n;
   RAFT_REQUIRE(nt < (1L << 31), "raft_corr_lookup_conv: grid too large");
-  g.ntiles = (int)nt;
   hipStream_t s = as_stream(stream);
   const dim3 grid((unsigned)nt);
-  if (c1_precision == RAFT_PREC_F16X3)
+  if (precision == RAFT_PREC_F16X3)
     hipLaunchKernelGGL(lookup_conv_kernel<RAFT_PREC_F16X3>, grid, dim3(512), 0, s, g);
-  else if (c1_precision == RAFT_PREC_F16)
+  else if (precision == RAFT_PREC_F16)
     hipLaunchKernelGGL(lookup_conv_kernel<RAFT_PREC_F16>, grid, dim3(512), 0, s, g);
   else
     hipLaunchKernelGGL(lookup_conv_kernel<RAFT_PREC_BF16>, grid, dim3(512), 0, s, g);

@@ -333,6 +333,48 @@ __global__ __launch_bounds__(256) void instnorm_apply4_kernel(const float* x, in
   }
 }
 
+// Chan's parallel merge of (count, mean, M2) partials, in double
+__device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, double nb, double meanb, double m2b) {
+  if (nb <= 0.0) return;
+  const double nn = n + nb;
+  const double d = meanb - mean;
+  mean += d * (nb / nn);
+  m2 += m2b + d * d * (n * nb / nn);
+  n = nn;
+}
+
+// raft_instnorm_merge: one 256-thread block per (channel, image); thread t merges slots t, t+256, ...
+// in order, then a fixed-order LDS tree (deterministic); stats = {mean, 1/sqrt(M2/n + eps)}
+__global__ __launch_bounds__(256) void instnorm_merge_kernel(const float* part, int slots, int C, int ld, float eps,
+                                                             float* stats) {
+  __shared__ double red[3][256];
+  const int c = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  for (int k = t; k < slots; k += 256) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(part + (((long)b * slots + k) * ld + c) * 4);
+    chan_merge(n, mean, m2, (double)v[0], (double)v[1], (double)v[2]);
+  }
+  red[0][t] = n;
+  red[1][t] = mean;
+  red[2][t] = m2;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) {
+      double n0 = red[0][t], m0 = red[1][t], q0 = red[2][t];
+      chan_merge(n0, m0, q0, red[0][t + w], red[1][t + w], red[2][t + w]);
+      red[0][t] = n0;
+      red[1][t] = m0;
+      red[2][t] = q0;
+    }
+    __syncthreads();
+  }
+  if (t != 0) return;
+  const double nn = red[0][0];
+  const double var = nn > 0.0 ? red[2][0] / nn : 0.0;
+  stats[2 * (b * C + c)] = (float)red[1][0];
+  stats[2 * (b * C + c) + 1] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
 bool aligned16(const void* q) { return ((uintptr_t)q & 15) == 0; }
 
 }  // namespace
@@ -429,6 +471,16 @@ extern "C" int raft_instnorm_stats(const float* x, int ld, int B, int HW, int C,
   hipLaunchKernelGGL(instnorm_finalize_kernel, dim3(C, B), dim3(256), 0, s, x, ld, HW, C, nchunk, workspace, eps,
                      stats, B);
   return check_launch("raft_instnorm_stats(finalize)");
+}
+
+extern "C" int raft_instnorm_merge(const float* part, int slots_per_image, int B, int C, int stats_ld, float eps,
+                                   float* stats, raft_stream_t stream) {
+  RAFT_REQUIRE(part && stats && slots_per_image > 0 && B > 0 && C > 0 && stats_ld >= C && B < 65536,
+               "raft_instnorm_merge: bad arguments");
+  RAFT_REQUIRE(aligned16(part), "raft_instnorm_merge: part must be 16-byte aligned");
+  hipLaunchKernelGGL(instnorm_merge_kernel, dim3(C, B), dim3(256), 0, as_stream(stream), part, slots_per_image, C,
+                     stats_ld, eps, stats);
+  return check_launch("raft_instnorm_merge");
 }
 
 extern "C" int raft_instnorm_apply(const float* x, int ld, const float* stats, const float* resid, int resid_ld,

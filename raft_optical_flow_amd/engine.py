@@ -186,6 +186,42 @@ def _in_stats(L, A: Arena, x: Rows, n_img, hw):
     return st
 
 
+def _conv_in(L, A: Arena, pc: PackedConv, src: Rows, n_img, h, w, out: Rows, src_norm=None):
+    """A conv whose raw output feeds an InstanceNorm; returns that norm's statistics.  On the halo /
+    stem kernel the conv's epilogue writes per-wave (count, mean, M2) partials and one merge launch
+    replaces raft_instnorm_stats' pass over the output (raft_conv2d_stats_slots; RAFT_EPI_STATS=0:
+    always the separate pass).  src_norm: src is a raw conv output whose relu(InstanceNorm) the conv
+    applies in its loaders (the statistics; the caller checked _norm_in_loader).  (The raw conv
+    outputs of an InstanceNorm encoder feed the fp32 statistics and normalisation only: no range
+    guard, raft_hip.h.)"""
+    import ctypes
+    p = conv_params(pc, src, n_img, h, w, out)
+    if src_norm is not None:
+        p.in_norm, p.in_norm_relu = src_norm.data_ptr(), 1
+    slots = int(_lib.load().raft_conv2d_stats_slots(ctypes.byref(p)))
+    ho, wo = K.conv_out_hw(pc, h, w)
+    if slots > 0 and os.environ.get("RAFT_EPI_STATS", "1") != "0":
+        part = A.flat(n_img * slots * out.c * 4)
+        p.stats_part, p.stats_ld = part.data_ptr(), out.c
+        L.append(conv_launch(p))
+        st = A.flat(2 * n_img * out.c)
+        L.append(Launch("raft_instnorm_merge", part.data_ptr(), slots, n_img, out.c, out.c, 1e-5, st.data_ptr()))
+        return st
+    L.append(conv_launch(p))
+    return _in_stats(L, A, out, n_img, ho * wo)
+
+
+def _norm_in_loader(pc: PackedConv, src: Rows, n_img, h, w) -> bool:
+    """Whether the conv of pc over src can apply src's relu(InstanceNorm) in its loaders
+    (raft_conv2d_in_norm_ok; RAFT_IN_NORM=0: never), which saves the normalised copy's pass."""
+    import ctypes
+    if os.environ.get("RAFT_IN_NORM", "1") == "0":
+        return False
+    p = conv_params(pc, src, n_img, h, w, src)   # (only checked, never launched)
+    p.in_norm, p.in_norm_relu = src.ptr, 1
+    return bool(_lib.load().raft_conv2d_in_norm_ok(ctypes.byref(p)))
+
+
 def _in_apply(L, A: Arena, x: Rows, st, n_img, hw, mode, resid: Rows | None = None, rst=None) -> Rows:
     out = Rows(A.rows(n_img * hw, x.c))
     L.append(Launch("raft_instnorm_apply", x.ptr, x.ld, st.data_ptr(), resid.ptr if resid else None,
@@ -211,8 +247,7 @@ def plan_encoder_trunk(L, A: Arena, pe: PackedEncoder, x: Rows, n_img, h, w):
         # (the raw conv outputs of an InstanceNorm encoder feed the fp32 statistics and the
         # normalisation, whose outputs are bounded by sqrt(H*W): no range guard, raft_hip.h)
         t = Rows(A.rows(n_img * ho * wo, pe.stem.n))
-        _conv(L, pe.stem, x, n_img, h, w, t, range_flag=None)
-        st = _in_stats(L, A, t, n_img, ho * wo)
+        st = _conv_in(L, A, pe.stem, x, n_img, h, w, t)
         x = _in_apply(L, A, t, st, n_img, ho * wo, 1)
     else:
         t = Rows(A.rows(n_img * ho * wo, pe.stem.n))
@@ -234,15 +269,16 @@ def _plan_residual(L, A, pe, d, x: Rows, n, h, w):
     npx = n * ho * wo
     if pe.norm == "instance":
         t1 = Rows(A.rows(npx, c1.n))
-        _conv(L, c1, x, n, h, w, t1, range_flag=None)
-        y1 = _in_apply(L, A, t1, _in_stats(L, A, t1, n, ho * wo), n, ho * wo, 1)
+        st1 = _conv_in(L, A, c1, x, n, h, w, t1)
         t2 = Rows(A.rows(npx, c2.n))
-        _conv(L, c2, y1, n, ho, wo, t2, range_flag=None)
-        st2 = _in_stats(L, A, t2, n, ho * wo)
+        if _norm_in_loader(c2, t1, n, ho, wo):
+            st2 = _conv_in(L, A, c2, t1, n, ho, wo, t2, src_norm=st1)
+        else:
+            y1 = _in_apply(L, A, t1, st1, n, ho * wo, 1)
+            st2 = _conv_in(L, A, c2, y1, n, ho, wo, t2)
         if ds is not None:
             t3 = Rows(A.rows(npx, ds.n))
-            _conv(L, ds, x, n, h, w, t3, range_flag=None)
-            out = _in_apply(L, A, t2, st2, n, ho * wo, 2, resid=t3, rst=_in_stats(L, A, t3, n, ho * wo))
+            out = _in_apply(L, A, t2, st2, n, ho * wo, 2, resid=t3, rst=_conv_in(L, A, ds, x, n, h, w, t3))
         else:
             out = _in_apply(L, A, t2, st2, n, ho * wo, 2, resid=x)
         return out, ho, wo
@@ -264,18 +300,18 @@ def _plan_bottleneck(L, A, pe, d, x: Rows, n, h, w):
     ho, wo = K.conv_out_hw(c2, h, w)
     if pe.norm == "instance":
         t1 = Rows(A.rows(n * h * w, c1.n))
-        _conv(L, c1, x, n, h, w, t1, range_flag=None)
-        y1 = _in_apply(L, A, t1, _in_stats(L, A, t1, n, h * w), n, h * w, 1)
+        st1 = _conv_in(L, A, c1, x, n, h, w, t1)
         t2 = Rows(A.rows(n * ho * wo, c2.n))
-        _conv(L, c2, y1, n, h, w, t2, range_flag=None)
-        y2 = _in_apply(L, A, t2, _in_stats(L, A, t2, n, ho * wo), n, ho * wo, 1)
+        if _norm_in_loader(c2, t1, n, h, w):
+            st2 = _conv_in(L, A, c2, t1, n, h, w, t2, src_norm=st1)
+        else:
+            st2 = _conv_in(L, A, c2, _in_apply(L, A, t1, st1, n, h * w, 1), n, h, w, t2)
+        y2 = _in_apply(L, A, t2, st2, n, ho * wo, 1)
         t3 = Rows(A.rows(n * ho * wo, c3.n))
-        _conv(L, c3, y2, n, ho, wo, t3, range_flag=None)
-        st3 = _in_stats(L, A, t3, n, ho * wo)
+        st3 = _conv_in(L, A, c3, y2, n, ho, wo, t3)
         if ds is not None:
             t4 = Rows(A.rows(n * ho * wo, ds.n))
-            _conv(L, ds, x, n, h, w, t4, range_flag=None)
-            out = _in_apply(L, A, t3, st3, n, ho * wo, 2, resid=t4, rst=_in_stats(L, A, t4, n, ho * wo))
+            out = _in_apply(L, A, t3, st3, n, ho * wo, 2, resid=t4, rst=_conv_in(L, A, ds, x, n, h, w, t4))
         else:
             out = _in_apply(L, A, t3, st3, n, ho * wo, 2, resid=x)
         return out, ho, wo
@@ -377,15 +413,16 @@ def convc1_fused(pk: PackedRaft) -> bool:
     RAFT_FUSE_CONVC1=0 keeps lookup + convf1 and convc1 as two launches)."""
     pu = pk.update
     return (convf1_fused(pu) and pk.radius == 4 and pk.levels == 4 and pu.convc1.n == 256
-            and pu.convc1.cin == 324 and pu.convf1.n == 128
+            and pu.convc1.cin == 324 and pu.convf1.n == 128 and pu.convf1.weight.shape == (128, 128)
             and pu.convc1.precision in (_lib.PREC_F16X3, _lib.PREC_F16, _lib.PREC_BF16)
+            and pu.convf1.precision == pu.convc1.precision
             and os.environ.get("RAFT_FUSE_CONVC1", "1") != "0")
 
 
-def convc1_frag_weight(pu: PackedUpdate) -> torch.Tensor:
-    """convc1's split weight in raft_corr_lookup_conv's fragment order (raft_hip.h), cached per precision."""
-    pc = pu.convc1
-    cached = getattr(pu, "_convc1_frag", None)
+def frag_weight(pc) -> torch.Tensor:
+    """A conv's split weight in raft_corr_lookup_conv's fragment order (raft_hip.h), cached on the
+    PackedConv per precision."""
+    cached = getattr(pc, "_frag", None)
     if cached is not None and cached[0] == pc.precision:
         return cached[1]
     split = pc.launch_weight()
@@ -393,7 +430,7 @@ def convc1_frag_weight(pu: PackedUpdate) -> torch.Tensor:
     out = torch.empty(int(_lib.load().raft_lookup_conv_weight_floats(pc.n, k_pad)), device=split.device,
                       dtype=torch.float32)
     _lib.call("raft_lookup_conv_pack_weight", split.data_ptr(), n_pad, k_pad, pc.n, out.data_ptr(), K.stream_handle())
-    pu._convc1_frag = (pc.precision, out)
+    pc._frag = (pc.precision, out)
     return out
 
 
@@ -571,16 +608,16 @@ class RaftPlan:
             f1b = pu.convf1.bias.data_ptr() if pu.convf1.bias is not None else None
         fuse_c1 = fuse_f1 and not alternate and convc1_fused(pk)
         if fuse_c1:
-            c1w = convc1_frag_weight(pu)
+            c1w, f1w_frag = frag_weight(pu.convc1), frag_weight(pu.convf1)
             c1b = pu.convc1.bias.data_ptr() if pu.convc1.bias is not None else None
         for it in range(iters):
             last = it == iters - 1
             if fuse_c1:
                 L.append(Launch("raft_corr_lookup_conv", self.pyramid.data_ptr(), B, h, w, lv, r, ub.coords.data_ptr(),
-                                ub.hx.data_ptr() + 4 * flow_slot, pu.ld, gflag, c1w.data_ptr(), c1b, pu.convc1.n,
-                                pu.convc1.precision, ub.cor1.data_ptr(), ub.cor1.shape[1], gflag, f1w.data_ptr(), f1b,
-                                pu.convf1.n, pu.convf1.kh, pu.convf1.precision, ub.flo1.data_ptr(),
-                                ub.flo1.shape[1], gflag, keep=(f1w, c1w)))
+                                ub.hx.data_ptr() + 4 * flow_slot, pu.ld, gflag, pu.convc1.precision, c1w.data_ptr(),
+                                c1b, pu.convc1.n, ub.cor1.data_ptr(), ub.cor1.shape[1], gflag, f1w_frag.data_ptr(), f1b,
+                                pu.convf1.n, pu.convf1.kh, ub.flo1.data_ptr(), ub.flo1.shape[1], gflag,
+                                keep=(f1w_frag, c1w)))
             elif fuse_f1 and not alternate:
                 L.append(Launch("raft_corr_lookup_convf1", self.pyramid.data_ptr(), B, h, w, lv, r,
                                 ub.coords.data_ptr(), 0, ub.corr.data_ptr(), corr_ld, 0,

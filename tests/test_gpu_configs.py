@@ -207,7 +207,8 @@ def test_bf16_band_vs_reference_autocast():
     """conv_precision="bf16": encoders and update block on v_mfma_f32_32x32x16_bf16 (fp32
     accumulate; corr volume and lookup stay fp32-accurate, as the reference keeps them
     outside autocast).  Band against the reference run under CPU bf16 autocast (whose
-    own drift from fp32 is max 0.27 / mean 0.072 px here) and against the fp32 reference."""
+    own drift from fp32 is max 0.27 / mean 0.072 px here) and against the fp32 reference; the band
+    is the measured difference plus margin."""
     gb = load_golden("raft_full_rand_b1_128x192_i32_bf16.npz")
     gf = load_golden("raft_full_rand_b1_128x192_i32.npz")
     from raft_optical_flow_amd.init import seeded_images
@@ -222,8 +223,9 @@ def test_bf16_band_vs_reference_autocast():
     epe_ref_bf = np.sqrt(((gb["flow_up"] - gf["flow_up"]) ** 2).sum(1)).mean()
     print(f"bf16 vs ref-bf16: max {db.max():.3g} mean {db.mean():.3g}; mean EPE vs fp32 {epe_f:.3g} "
           f"(reference bf16 vs fp32: {epe_ref_bf:.3g})")
-    assert db.max() < 1.0 and db.mean() < 0.15
-    assert epe_f < 0.15
+    # measured (round 3): max 0.281, mean 0.0611, mean EPE vs fp32 0.0546
+    assert db.max() < 0.45 and db.mean() < 0.09
+    assert epe_f < 0.09
 
 
 def test_bf16_1080x1920_vs_reference_autocast():
@@ -250,6 +252,8 @@ def test_bf16_1080x1920_vs_reference_autocast():
     print(f"1080x1920 bf16 vs reference bf16: flow_low max {dl.max():.3g} mean {dl.mean():.3g}; flow_up rows8 "
           f"max {du.max():.3g} mean {du.mean():.3g}, mean EPE {epe:.3g} (max |flow| {mag:.3g}); "
           f"|flow| sum rel {rel_abs:.3g}")
-    assert dl.max() < 0.5 and dl.mean() < 0.05
-    assert du.max() < 1.0 and du.mean() < 0.1 and epe < 0.15
-    assert rel_abs < 0.02
+    # measured (round 3): flow_low max 0.117 mean 0.0169; rows8 max 0.31 mean 0.0581, EPE 0.0907;
+    # |flow| sum 8e-4 relative
+    assert dl.max() < 0.25 and dl.mean() < 0.03
+    assert du.max() < 0.5 and du.mean() < 0.09 and epe < 0.13
+    assert rel_abs < 0.005

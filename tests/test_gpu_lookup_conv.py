@@ -5,8 +5,9 @@ convc1 (1x1, 324 -> 256, relu) and convf1 (7x7, 2 -> 128, relu) in one launch
 convc1 is checked against an fp64 torch conv of the plain lookup's correlation rows
 (raft_corr_lookup, itself pinned to the reference's goldens), with the operands rounded to the
 conv precision's operand type in the one-product modes; tolerances as the conv GEMM tests:
-1e-4 x max|ref| (f16x3), 5e-3 x (f16), 3e-2 x (bf16).  convf1 and the flow output must equal the
-unfused kernels' bit for bit (same FMA order)."""
+1e-4 x max|ref| (f16x3), 5e-3 x (f16), 3e-2 x (bf16).  convf1 (on MFMA in the conv precision, an
+im2col of the flow patch) likewise against an fp64 conv of the same operands; the flow output
+equals the plain lookup's bit for bit."""
 import numpy as np
 import pytest
 import torch
@@ -56,31 +57,30 @@ def _case(B, h, w, prec, coord_sigma=3.0, fscale=1.0, seed=5, C=64):
     n_pad, k_pad = split.shape
     frag = torch.empty(int(_lib.load().raft_lookup_conv_weight_floats(256, k_pad)), device=DEV)
     _lib.call("raft_lookup_conv_pack_weight", split.data_ptr(), n_pad, k_pad, 256, frag.data_ptr(), K.stream_handle())
-    # convf1 weights [n/32][49][2][32], rounded as the engine does in the one-product modes
+    # convf1 weights, packed as the engine does (GATHER mode, K = 2 (dy*7 + dx) + ci)
     wf = (rng.standard_normal((128, 2, 7, 7)) * 0.1).astype(np.float32)
     bf = (rng.standard_normal(128) * 0.1).astype(np.float32)
     rnd = {"f16": torch.float16, "bf16": torch.bfloat16}.get(prec)
-    wq = torch.from_numpy(wf)
-    if rnd is not None:
-        wq = wq.to(rnd).float()
-    wv = wq.reshape(4, 32, 2, 49).permute(0, 3, 2, 1).contiguous().to(DEV)
+    pf = K.pack_conv(torch.from_numpy(wf), torch.from_numpy(bf), 1, 3, mode=_lib.RAFT_CONV_GATHER, device=DEV)
+    pf.precision = p
+    fsplit = pf.launch_weight()
+    fnp, fkp = fsplit.shape
+    ffrag = torch.empty(int(_lib.load().raft_lookup_conv_weight_floats(128, fkp)), device=DEV)
+    _lib.call("raft_lookup_conv_pack_weight", fsplit.data_ptr(), fnp, fkp, 128, ffrag.data_ptr(), K.stream_handle())
     # unfused: lookup (+flow), convf1 alone
     corr = torch.full((P, ntap), -7.0, device=DEV)
     flow_a = torch.zeros(P, 4, device=DEV)
     _lib.call("raft_corr_lookup", pyr.data_ptr(), B, h, w, L, r, cr.data_ptr(), 0, corr.data_ptr(), ntap, 0,
               flow_a.data_ptr(), 4, None, K.stream_handle())
-    f1_a = torch.full((P, 132), -7.0, device=DEV)
-    _lib.call("raft_convf1_flow", cr.data_ptr(), 0, B, h, w, wv.data_ptr(), t(bf).data_ptr(), 128, 7, p,
-              f1_a.data_ptr(), 132, None, K.stream_handle())
     # fused
     c1 = torch.full((P, 260), -7.0, device=DEV)
     f1_b = torch.full((P, 132), -7.0, device=DEV)
     flow_b = torch.zeros(P, 4, device=DEV)
     flags = torch.zeros(3, dtype=torch.int32, device=DEV)
     fp = flags.data_ptr()
-    _lib.call("raft_corr_lookup_conv", pyr.data_ptr(), B, h, w, L, r, cr.data_ptr(), flow_b.data_ptr(), 4, fp,
-              frag.data_ptr(), pc.bias.data_ptr(), 256, p, c1.data_ptr(), 260, fp + 4, wv.data_ptr(),
-              t(bf).data_ptr(), 128, 7, p, f1_b.data_ptr(), 132, fp + 8, K.stream_handle())
+    _lib.call("raft_corr_lookup_conv", pyr.data_ptr(), B, h, w, L, r, cr.data_ptr(), flow_b.data_ptr(), 4, fp, p,
+              frag.data_ptr(), pc.bias.data_ptr(), 256, c1.data_ptr(), 260, fp + 4, ffrag.data_ptr(),
+              pf.bias.data_ptr(), 128, 7, f1_b.data_ptr(), 132, fp + 8, K.stream_handle())
     torch.cuda.synchronize()
     # convc1 reference: fp64 on the plain lookup's rows (operands rounded in one-product modes)
     cin = corr.cpu().double()
@@ -89,7 +89,15 @@ def _case(B, h, w, prec, coord_sigma=3.0, fscale=1.0, seed=5, C=64):
         cin = cin.to(rnd).double()
         wref = wref.to(rnd).double()
     ref = torch.relu(cin @ wref.T + torch.from_numpy(bc).double())
-    return dict(c1=c1, ref=ref, f1_a=f1_a, f1_b=f1_b, flow_a=flow_a, flow_b=flow_b, flags=flags.cpu().tolist(),
+    # convf1 reference: fp64 conv of flow = coords - grid (zero padded), operands rounded likewise
+    flow = torch.from_numpy(coords - grid).permute(0, 3, 1, 2).double()
+    wfr = torch.from_numpy(wf).double()
+    if rnd is not None:
+        flow = flow.to(rnd).double()
+        wfr = wfr.to(rnd).double()
+    fref = torch.relu(F.conv2d(flow, wfr, torch.from_numpy(bf).double(), padding=3))
+    fref = fref.permute(0, 2, 3, 1).reshape(P, 128)
+    return dict(c1=c1, ref=ref, f1=f1_b, fref=fref, flow_a=flow_a, flow_b=flow_b, flags=flags.cpu().tolist(),
                 corr=corr)
 
 
@@ -103,7 +111,11 @@ def test_lookup_conv_equals_lookup_then_convs(B, h, w, prec):
     err = float((got - d["ref"]).abs().max())
     assert err <= TOL[prec] * max(1.0, scale), (err, scale)
     assert bool((d["c1"][:, 256:] == -7.0).all())  # nothing past n channels of a row
-    assert torch.equal(d["f1_a"], d["f1_b"])
+    fgot = d["f1"][:, :128].cpu().double()
+    fscale = float(d["fref"].abs().max())
+    ferr = float((fgot - d["fref"]).abs().max())
+    assert ferr <= TOL[prec] * max(1.0, fscale), (ferr, fscale)
+    assert bool((d["f1"][:, 128:] == -7.0).all())
     assert torch.equal(d["flow_a"], d["flow_b"])
     assert d["flags"] == [0, 0, 0]
 
@@ -114,7 +126,8 @@ def test_lookup_conv_far_out_of_bounds():
     got = d["c1"][:, :256].cpu().double()
     scale = float(d["ref"].abs().max())
     assert float((got - d["ref"]).abs().max()) <= 1e-4 * max(1.0, scale)
-    assert torch.equal(d["f1_a"], d["f1_b"])
+    fscale = float(d["fref"].abs().max())
+    assert float((d["f1"][:, :128].cpu().double() - d["fref"]).abs().max()) <= 1e-4 * max(1.0, fscale)
 
 
 def test_lookup_conv_range_guard():

@@ -52,6 +52,96 @@ def make_model(small, seed=0, alternate=False, precision=None):
 # ----------------------------------------------------------------------------- instance norm
 
 
+@pytest.mark.parametrize("case", [
+    dict(cin=64, cout=64, k=3, stride=1, pad=1, H=37, W=53, B=2, mode=None),   # halo 3x3, ragged tiles
+    dict(cin=96, cout=96, k=1, stride=1, pad=0, H=20, W=33, B=2, mode=None),   # halo 1x1
+    dict(cin=3, cout=64, k=7, stride=2, pad=3, H=90, W=150, B=2, mode="gather"),  # the stem
+])
+@pytest.mark.parametrize("prec", ["f16x3", "bf16"])
+def test_conv_epilogue_instnorm_stats(case, prec):
+    """InstanceNorm statistics from the conv epilogue (raft_conv2d_stats_slots + raft_instnorm_merge):
+    per-(image, channel) mean and 1/sqrt(var + eps) of the conv output against fp64 over the
+    output the same launch wrote; run twice, bit-identical (fixed merge order)."""
+    import ctypes
+    from raft_optical_flow_amd import _lib
+    from raft_optical_flow_amd import kernels as K
+    g = torch.Generator().manual_seed(case["cin"] + case["k"])
+    B, H, W = case["B"], case["H"], case["W"]
+    x = torch.randn(B, case["cin"], H, W, generator=g) + 0.5
+    w = torch.randn(case["cout"], case["cin"], case["k"], case["k"], generator=g) / np.sqrt(case["cin"] * case["k"] ** 2)
+    b = torch.randn(case["cout"], generator=g) * 3.0   # an offset the M2 form must not lose precision to
+    mode = _lib.RAFT_CONV_GATHER if case["mode"] == "gather" else None
+    pc = K.pack_conv(w, b, case["stride"], case["pad"], mode=mode, device=DEV)
+    pc.precision = _lib.PRECISIONS[prec]
+    src = K.Rows(K.nchw_to_rows(x.to(DEV)))
+    ho, wo = K.conv_out_hw(pc, H, W)
+    out = K.Rows(torch.empty(B * ho * wo, case["cout"], device=DEV))
+    p = K.conv_params(pc, src, B, H, W, out)
+    slots = _lib.load().raft_conv2d_stats_slots(ctypes.byref(p))
+    assert slots > 0
+    part = torch.full((B * slots * case["cout"] * 4,), float("nan"), device=DEV)
+    p.stats_part, p.stats_ld = part.data_ptr(), case["cout"]
+    got = []
+    for _ in range(2):
+        K.conv_launch(p)(K.stream_handle())
+        st = torch.empty(2 * B * case["cout"], device=DEV)
+        _lib.call("raft_instnorm_merge", part.data_ptr(), slots, B, case["cout"], case["cout"], 1e-5, st.data_ptr(),
+                  K.stream_handle())
+        got.append(st.view(B, case["cout"], 2).cpu())
+    assert torch.equal(got[0], got[1])
+    y = out.t.view(B, ho * wo, case["cout"]).cpu().double()
+    mean = y.mean(1)
+    rstd = 1.0 / torch.sqrt(y.var(1, unbiased=False) + 1e-5)
+    assert float((got[0][..., 0].double() - mean).abs().max()) < 1e-5 * max(1.0, float(mean.abs().max()))
+    assert float(((got[0][..., 1].double() - rstd) / rstd).abs().max()) < 1e-5
+
+
+@pytest.mark.parametrize("cin,cout,H,W,B,relu", [(64, 64, 37, 53, 2, 1), (128, 96, 23, 30, 1, 0), (96, 96, 16, 16, 1, 1)])
+@pytest.mark.parametrize("prec", ["f16x3", "bf16"])
+def test_conv_in_norm_loader(cin, cout, H, W, B, relu, prec):
+    """raft_conv2d_params.in_norm: the 3x3 halo conv reads act((x - mean) * rstd) of its raw input
+    (the residual blocks' conv2 over conv1's un-normalised output), zero padding staying zero;
+    against torch fp64 of conv(act(instance_norm(x)))."""
+    import ctypes
+    from raft_optical_flow_amd import _lib
+    from raft_optical_flow_amd import kernels as K
+    g = torch.Generator().manual_seed(cin + H)
+    x = torch.randn(B, cin, H, W, generator=g) * 2.0 + 1.5
+    w = torch.randn(cout, cin, 3, 3, generator=g) / np.sqrt(cin * 9)
+    b = torch.randn(cout, generator=g) * 0.1
+    mean = x.double().mean((2, 3))
+    rstd = 1.0 / torch.sqrt(x.double().var((2, 3), unbiased=False) + 1e-5)
+    xn = (x.double() - mean[:, :, None, None]) * rstd[:, :, None, None]
+    if relu:
+        xn = torch.relu(xn)
+    ref = F.conv2d(xn, w.double(), b.double(), 1, 1)
+    pc = K.pack_conv(w, b, 1, 1, device=DEV)
+    pc.precision = _lib.PRECISIONS[prec]
+    src = K.Rows(K.nchw_to_rows(x.to(DEV)))
+    out = K.Rows(torch.full((B * H * W, cout + 4), -7.0, device=DEV), 0, cout)
+    st = torch.stack([mean, rstd], -1).float().contiguous().to(DEV)   # [B][cin][2]
+    p = K.conv_params(pc, src, B, H, W, out)
+    p.in_norm, p.in_norm_relu = st.data_ptr(), relu
+    assert _lib.load().raft_conv2d_in_norm_ok(ctypes.byref(p)) == 1
+    K.conv_launch(p)(K.stream_handle())
+    y = K.rows_to_nchw(out, B, H, W)
+    assert maxabs(y, ref) < CONV_TOL[prec] * max(1.0, float(ref.abs().max()))
+    assert bool((out.t[:, cout:] == -7.0).all())
+
+
+def test_encoders_in_norm_matches_apply_pass(monkeypatch):
+    """The encoders with the loaders' InstanceNorm (default) vs the separate normalised copy
+    (RAFT_IN_NORM=0): the same features to 1e-4 of their scale."""
+    m, _ = make_model(False)
+    g = torch.Generator().manual_seed(11)
+    img = (torch.rand(2, 3, 96, 128, generator=g) * 255).to(DEV)
+    with torch.no_grad():
+        a = m.fnet(img)
+        monkeypatch.setenv("RAFT_IN_NORM", "0")
+        b = m.fnet(img)
+    assert maxabs(a, b) < 1e-4 * max(1.0, float(b.abs().max()))
+
+
 @pytest.mark.parametrize("B,HW,C,ld", [(2, 220 * 512, 64, 64), (3, 1000, 96, 100), (1, 77, 6, 6), (2, 513, 300, 300)])
 def test_instnorm_stats_vs_fp64(B, HW, C, ld):
     """raft_instnorm_stats (one launch: chunk partials, the last block of each image finalizes):
@@ -539,6 +629,31 @@ def test_conv2d_vs_torch_fp64(cin, cout, kh, kw, stride, pad, H, W, B, prec):
     y = K.rows_to_nchw(out, B, ho, wo)
     err = maxabs(y, ref)
     assert err < CONV_TOL[prec] * max(1.0, float(ref.abs().max())), err
+
+
+@pytest.mark.parametrize("prec", ["f16x3", "bf16"])
+def test_conv_stem_full_size_relu(prec):
+    """The encoders' 7x7 / stride-2 stem (conv_stem.hip) at config 2's size (440x1024 -> 220x512:
+    896 tiles per image, more than one per work-group) with the relu epilogue and the range guard,
+    against torch fp64."""
+    from raft_optical_flow_amd import kernels as K
+    from raft_optical_flow_amd import _lib
+    g = torch.Generator().manual_seed(7)
+    B, H, W = 2, 440, 1024
+    x = torch.rand(B, 3, H, W, generator=g) * 2 - 1
+    w = torch.randn(64, 3, 7, 7, generator=g) / np.sqrt(147)
+    b = torch.randn(64, generator=g) * 0.1
+    ref = torch.relu(F.conv2d(x.double(), w.double(), b.double(), 2, 3))
+    pc = K.pack_conv(w, b, 2, 3, device=DEV)
+    pc.precision = _lib.PRECISIONS[prec]
+    src = K.Rows(K.nchw_to_rows(x.to(DEV)))
+    out = K.Rows(torch.full((B * 220 * 512, 68), -7.0, device=DEV), 0, 64)
+    flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+    K.conv2d_rows(pc, src, B, H, W, out, epilogue=_lib.EPI_RELU, range_flag=flag)
+    y = K.rows_to_nchw(out, B, 220, 512)
+    assert maxabs(y, ref) < CONV_TOL[prec] * max(1.0, float(ref.abs().max()))
+    assert bool((out.t[:, 64:] == -7.0).all())
+    assert int(flag.item()) == 0
 
 
 def test_conv2d_split_weight_layout():

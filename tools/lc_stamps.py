@@ -39,12 +39,12 @@ nwg = 224
 buf = np.zeros(nwg * 8 * 16, dtype=np.uint64)
 lib.raft_debug_lcstamps(buf.ctypes.data, buf.size)
 s = buf.reshape(nwg * 8, 16).astype(np.int64)
-r0, r1, t = s[:, 0], s[:, 1], s[:, 2:12]
-names = ["issue loads", "axis entries", "vmcnt16+flowpatch+sync", "convf1", "wait tiles", "taps x4",
-         "sync A", "GEMM", "epilogues"]
+r0, r1, t = s[:, 0], s[:, 1], s[:, 2:9]
+names = ["issue loads", "axis entries + flow patch", "taps x4 (tile wait incl.)", "sync + convf1 A + sync",
+         "GEMMs", "epilogues"]
 d = np.diff(t, axis=1)
 for k, n in enumerate(names):
     print(f"  {n:26s} mean {d[:, k].mean():8.0f} cyc  max {d[:, k].max():8.0f}")
-print(f"  total per wave mean {(t[:, 9] - t[:, 0]).mean():.0f} cycles")
+print(f"  total per wave mean {(t[:, 6] - t[:, 0]).mean():.0f} cycles")
 print(f"  launch span (realtime 100 MHz): {(r1.max() - r0.min()) / 100:.2f} us; wave mean {(r1 - r0).mean() / 100:.2f} us;"
       f" start spread {(r0.max() - r0.min()) / 100:.2f} us")
