@@ -171,7 +171,8 @@ def source_hash() -> str | None:
     hdr = os.path.join(os.path.dirname(_HERE), "include", "raft_hip.h")
     if not (os.path.exists(mk) and os.path.exists(hdr)):
         return None
-    srcs = next(l.split(":=", 1)[1].split() for l in open(mk) if l.startswith("SRCS :="))
+    with open(mk) as fh:
+        srcs = next(l.split(":=", 1)[1].split() for l in fh if l.startswith("SRCS :="))
     files = [os.path.join(csrc, f) for f in srcs] + sorted(glob.glob(os.path.join(csrc, "*.hpp"))) + [hdr]
     h = hashlib.sha256()
     for f in files:

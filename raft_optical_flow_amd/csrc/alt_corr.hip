@@ -460,8 +460,39 @@ struct AltLevels {
   int n;
 };
 
+// the per-pixel path of a tile whose box does not fit, out of line (rare: keeps its registers out
+// of the MFMA tile kernel's main path)
+__device__ __noinline__ void alt_pixel_ni(const AltArgs& a, long gid, bool valid, int lane, float* ts) {
+  alt_pixel<1>(a, gid, valid, lane, ts);
+}
+
+#ifdef ALT_STAMPS  // dev-only phase timing (tools/alt_stamps.py with a -DALT_STAMPS variant)
+__device__ unsigned long long g_altstamp[16 * 8 * 4096];
+__device__ __forceinline__ unsigned long long alt_clock() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+// phase k gets the cycles since the previous stamp
+#define ALT_ST(k)                       \
+  do {                                  \
+    const unsigned long long n_ = alt_clock(); \
+    alt_t[k] += n_ - alt_prev;          \
+    alt_prev = n_;                      \
+  } while (0)
+#else
+#define ALT_ST(k)
+#endif
+
 template <int R>
 __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevels lvs) {
+#ifdef ALT_STAMPS
+  unsigned long long alt_t[12] = {}, alt_prev = alt_clock();
+  const unsigned long long alt_start = alt_prev;
+  int alt_bands = 0;
+#endif
   constexpr int WD = 2 * R + 2, NT = WD * WD, RD = 2 * R + 1;
   constexpr int TPT = (NT + 7) / 8;  // taps per thread (8 waves)
   constexpr int ABYTES = AT * AT * AM_KS * AM_ROW, BBYTES = AM_NB * AM_KS * AM_ROW;
@@ -514,21 +545,25 @@ __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevel
       if (s < ks) am_split_store(As, s * (AT * AT) + q, qd & 7, av[k]);
     }
   }
+  ALT_ST(0);  // F1 tile
   const int mi = g & 1, ni = g >> 1;  // S subtile of MFMA waves 0-5
   const int m = lane & 31, h = lane >> 5;
-  for (int l = 0; l < lvs.n; ++l) {
-    AltArgs a = a0;
-    a.f2 = lvs.f2[l];
-    a.H2 = lvs.H2[l];
-    a.W2 = lvs.W2[l];
-    a.coord_div = lvs.div[l];
-    a.out = lvs.out[l];
-    a.flow = l == 0 ? a0.flow : nullptr;
-    const float x = valid ? xr / a.coord_div : 0.f, y = valid ? yr / a.coord_div : 0.f;
-    const bool fin = isfinite(x) && isfinite(y) && fabsf(x) < 1e8f && fabsf(y) < 1e8f;
-    const int x0 = fin ? (int)floorf(x) - R : 0, y0 = fin ? (int)floorf(y) - R : 0;
-    int mnx = valid ? x0 : (1 << 30), mny = valid ? y0 : (1 << 30);
-    int mxx = valid ? x0 : -(1 << 30), mxy = valid ? y0 : -(1 << 30);
+  // ---- per-level window box (wave-uniform) and the band loads, set up one level ahead ------
+  struct Lvl {
+    float x, y;       // this lane's query at the level
+    int x0, y0;       // its window origin
+    int bx0, by0, bw, bh, br;  // the tile's box and box rows per band
+    bool fits;
+  };
+  auto setup = [&](int l, Lvl& v) {
+    const float div = lvs.div[l];
+    v.x = valid ? xr / div : 0.f;
+    v.y = valid ? yr / div : 0.f;
+    const bool fin = isfinite(v.x) && isfinite(v.y) && fabsf(v.x) < 1e8f && fabsf(v.y) < 1e8f;
+    v.x0 = fin ? (int)floorf(v.x) - R : 0;
+    v.y0 = fin ? (int)floorf(v.y) - R : 0;
+    int mnx = valid ? v.x0 : (1 << 30), mny = valid ? v.y0 : (1 << 30);
+    int mxx = valid ? v.x0 : -(1 << 30), mxy = valid ? v.y0 : -(1 << 30);
     int bad = valid && !fin;
 #pragma unroll
     for (int k = 1; k < 64; k <<= 1) {
@@ -538,59 +573,90 @@ __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevel
       mxy = max(mxy, __shfl_xor(mxy, k));
       bad |= __shfl_xor(bad, k);
     }
-    const int bx0 = __builtin_amdgcn_readfirstlane(mnx), by0 = __builtin_amdgcn_readfirstlane(mny);
-    const int bw = __builtin_amdgcn_readfirstlane(mxx) - bx0 + WD;
-    const int bh = __builtin_amdgcn_readfirstlane(mxy) - by0 + WD;
+    v.bx0 = __builtin_amdgcn_readfirstlane(mnx);
+    v.by0 = __builtin_amdgcn_readfirstlane(mny);
+    v.bw = __builtin_amdgcn_readfirstlane(mxx) - v.bx0 + WD;
+    v.bh = __builtin_amdgcn_readfirstlane(mxy) - v.by0 + WD;
     // any box up to AM_NB wide is consumed band by band (a tall box only costs more bands)
-    const bool fits = !__builtin_amdgcn_readfirstlane(bad) && bw <= AM_NB && bh <= AM_NB;
-    if (!fits) {
+    v.fits = !__builtin_amdgcn_readfirstlane(bad) && v.bw <= AM_NB && v.bh <= AM_NB;
+    v.br = v.fits ? AM_NB / v.bw : 1;  // box rows per band: as many whole rows as fit 96 pixels (>= 1)
+  };
+  // fmap2 band loads: thread = (band pixel j, quad) with j = g + 8k (wave-uniform), AM_PER per
+  // thread; zeros off the map / band / channels
+  f32x4 bv[AM_PER];
+  auto load_band = [&](int l, const Lvl& v, int r0) {
+    const int H2 = lvs.H2[l], W2 = lvs.W2[l];
+    const float* f2b = lvs.f2[l] + (long)b * H2 * W2 * a0.C;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(f2b), (short)0, (int)((long)H2 * W2 * a0.C * 4), 0x00020000);
+    const bool qin = 4 * lane < a0.C;
+    int rr = 0, xx = g;  // (box row, column) of band pixel j = g + 8k (bw >= WD > 8: one wrap per step)
+#pragma unroll
+    for (int k = 0; k < AM_PER; ++k) {
+      const int h2 = v.by0 + r0 + rr, w2 = v.bx0 + xx;
+      const bool in = rr < v.br && r0 + rr < v.bh && (unsigned)h2 < (unsigned)H2 && (unsigned)w2 < (unsigned)W2;
+      const unsigned off = (in && qin) ? (unsigned)((h2 * W2 + w2) * a0.C + 4 * lane) * 4u : 0x80000000u;
+      bv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      xx += 8;
+      if (xx >= v.bw) {
+        xx -= v.bw;
+        ++rr;
+      }
+    }
+  };
+  auto store_band = [&]() {
+#pragma unroll
+    for (int k = 0; k < AM_PER; ++k) {
+      const int j = g + 8 * k, s = lane >> 3;
+      if (s < ks) am_split_store(Bs, s * AM_NB + j, lane & 7, bv[k]);
+    }
+  };
+  Lvl cur;
+  setup(0, cur);
+  if (cur.fits) load_band(0, cur, 0);
+  ALT_ST(1);  // level setup + first band issue
+  for (int l = 0; l < lvs.n; ++l) {
+    float* const out = lvs.out[l];
+    const float cdiv = lvs.div[l];
+    Lvl nxt = cur;
+    if (!cur.fits) {
       // wave g finishes pixels 8g .. 8g + 7 of the tile one at a time (per-pixel path)
+      AltArgs a = a0;
+      a.f2 = lvs.f2[l];
+      a.H2 = lvs.H2[l];
+      a.W2 = lvs.W2[l];
+      a.coord_div = cdiv;
+      a.out = out;
+      a.flow = l == 0 ? a0.flow : nullptr;
       float* ts = reinterpret_cast<float*>(Bs) + g * 128;
       for (int i = 0; i < 8; ++i) {
         const int q = 8 * g + i;
         const int pq = __shfl(p, q), vq = __shfl((int)valid, q);
-        alt_pixel<1>(a, bn * P1 + pq, vq != 0, lane, ts);
+        alt_pixel_ni(a, bn * P1 + pq, vq != 0, lane, ts);
       }
       __syncthreads();  // the band region is free for the next level
+      if (l + 1 < lvs.n) {
+        setup(l + 1, nxt);
+        if (nxt.fits) load_band(l + 1, nxt, 0);
+      }
+      cur = nxt;
       continue;
     }
-    const int br = AM_NB / bw;  // box rows per band: as many whole rows as fit 96 pixels (>= 1)
-    // ---- fmap2 band loads: thread = (band pixel, quad), AM_PER per thread; zeros off the map / band
-    const float* f2b = a.f2 + (long)b * a.H2 * a.W2 * a.C;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(f2b), (short)0, (int)((long)a.H2 * a.W2 * a.C * 4), 0x00020000);
-    f32x4 bv[AM_PER];
-    auto load_band = [&](int r0) {
-#pragma unroll
-      for (int k = 0; k < AM_PER; ++k) {
-        const int i = tid + 512 * k;  // (pixel j, quad) with 64 quads per pixel (C = 256 max)
-        const int j = i >> 6, qd = i & 63;
-        const int rr = j / bw, xx = j - rr * bw;
-        const int h2 = by0 + r0 + rr, w2 = bx0 + xx;
-        const bool in = rr < br && r0 + rr < bh && 4 * qd < a.C && (unsigned)h2 < (unsigned)a.H2 &&
-                        (unsigned)w2 < (unsigned)a.W2;
-        const unsigned off = in ? (unsigned)((h2 * a.W2 + w2) * a.C + 4 * qd) * 4u : 0x80000000u;
-        bv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-      }
-    };
-    auto store_band = [&]() {
-#pragma unroll
-      for (int k = 0; k < AM_PER; ++k) {
-        const int i = tid + 512 * k;
-        const int j = i >> 6, qd = i & 63, s = qd >> 3;
-        if (s < ks) am_split_store(Bs, s * AM_NB + j, qd & 7, bv[k]);
-      }
-    };
     // box-relative window origin of this lane's query; taps t = g + 8j
-    const int ox0 = valid ? x0 - bx0 : 0, oy0 = valid ? y0 - by0 : 0;
+    const int ox0 = valid ? cur.x0 - cur.bx0 : 0, oy0 = valid ? cur.y0 - cur.by0 : 0;
     float tap[TPT];
 #pragma unroll
     for (int j = 0; j < TPT; ++j) tap[j] = 0.f;
-    load_band(0);
-    for (int r0 = 0; r0 < bh; r0 += br) {
+    for (int r0 = 0; r0 < cur.bh; r0 += cur.br) {
+#ifdef ALT_STAMPS
+      ++alt_bands;
+#endif
       store_band();
+      ALT_ST(2);  // band split + store (with the wait for its loads)
       __syncthreads();  // band r0 (and, first time round, the F1 tile) in LDS
-      if (r0 + br < bh) load_band(r0 + br);  // in flight under the MFMAs
+      ALT_ST(3);
+      if (r0 + cur.br < cur.bh) load_band(l, cur, r0 + cur.br);  // in flight under the MFMAs
+      ALT_ST(4);
       f32x16 acc = {}, acc2 = {}, acc3 = {};
       if (g < 6) {
         for (int s = 0; s < ks; ++s) {
@@ -610,14 +676,18 @@ __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevel
           }
         }
       }
+      ALT_ST(5);  // MFMAs
       __syncthreads();  // every MFMA wave has read the band: its region takes S
+      ALT_ST(6);
       if (g < 6) {
         // register r holds S[query 32mi + (r&3) + 8(r>>2) + 4h][band pixel 32ni + m]
 #pragma unroll
         for (int r = 0; r < 16; ++r)
           S[(32 * mi + (r & 3) + 8 * (r >> 2) + 4 * h) * AM_SLD + 32 * ni + m] = acc[r] + acc2[r] + acc3[r];
       }
+      ALT_ST(7);  // S stores
       __syncthreads();
+      ALT_ST(8);
       // every lane (query) picks the taps of its window in box rows r0 .. r0 + br - 1
 #pragma unroll
       for (int j = 0; j < TPT; ++j) {
@@ -625,12 +695,14 @@ __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevel
         if (t < NT) {
           const int iy = t / WD, ix = t - (t / WD) * WD;
           const int rr = oy0 + iy - r0;
-          if ((unsigned)rr < (unsigned)br) tap[j] = S[lane * AM_SLD + rr * bw + ox0 + ix];
+          if ((unsigned)rr < (unsigned)cur.br) tap[j] = S[lane * AM_SLD + rr * cur.bw + ox0 + ix];
         }
       }
+      ALT_ST(9);  // tap picks
       __syncthreads();  // S read: the region takes the next band (or the tap sums)
+      ALT_ST(10);
     }
-    // ---- tap sums -> LDS ts[q][t] (over the band region), then the tile kernel's binning
+    // ---- tap sums -> LDS ts[q][t] (over the band region), then the bilinear binning
     float* ts = reinterpret_cast<float*>(Bs);
 #pragma unroll
     for (int j = 0; j < TPT; ++j) {
@@ -638,23 +710,76 @@ __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevel
       if (t < NT) ts[lane * (NT + 1) + t] = tap[j];
     }
     __syncthreads();
-    if (a.out_layout == 1) {
-      for (int q = g; q < AT * AT; q += 8) {
-        const float xq = __shfl(x, q), yq = __shfl(y, q);
-        const int pq = __shfl(p, q), vq = __shfl((int)valid, q);
-        if (!vq) continue;
-        for (int o = lane; o < RD * RD; o += 64) alt_bin_store(a, bn, pq, xq, yq, ts + q * (NT + 1), o);
+    // the next level's box and first band go out before this level's binning
+    if (l + 1 < lvs.n) {
+      setup(l + 1, nxt);
+      if (nxt.fits) load_band(l + 1, nxt, 0);
+    }
+    // bin (core/corr.py + correlation_kernel.cu:95-116: the bilinear weights of frac(coords) over
+    // each bin's four integer taps, then / scale), the arithmetic of alt_bin_store
+    const float sdiv = a0.scale_div;
+    int big = 0;
+    if (a0.out_layout == 1) {
+      // wave g: queries q = g + 8i (uniform), lanes = output bins o, o + 64
+#pragma unroll 1
+      for (int i = 0; i < AT * AT / 8; ++i) {
+        const int q = g + 8 * i;
+        if (!__builtin_amdgcn_readlane((int)valid, q)) continue;
+        const float xq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cur.x), q));
+        const float yq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cur.y), q));
+        const int pq = __builtin_amdgcn_readlane(p, q);
+        const float dx = xq - floorf(xq), dy = yq - floorf(yq);
+        const float* tq = ts + q * (NT + 1);
+        float* orow = out + ((long)b * P1 + pq) * a0.out_ld;
+#pragma unroll
+        for (int o0 = 0; o0 < RD * RD; o0 += 64) {
+          const int o = o0 + lane;
+          if (o < RD * RD) {
+            const int ox = o / RD, oy = o - ox * RD;  // channel = oy + rd*ox
+            float val = tq[oy * WD + ox] * ((1.f - dy) * (1.f - dx));
+            val += tq[oy * WD + ox + 1] * ((1.f - dy) * dx);
+            val += tq[(oy + 1) * WD + ox] * (dy * (1.f - dx));
+            val += tq[(oy + 1) * WD + ox + 1] * (dy * dx);
+            val = val / sdiv;
+            big |= fabsf(val) > RAFT_RANGE_LIMIT;
+            orow[o] = val;
+          }
+        }
       }
     } else if (valid) {
-      for (int o = g; o < RD * RD; o += 8) alt_bin_store(a, bn, p, x, y, ts + lane * (NT + 1), o);
+      // lanes = queries, wave g: bins o = g + 8i ([B][N][RD^2][H1][W1])
+      const float dx = cur.x - floorf(cur.x), dy = cur.y - floorf(cur.y);
+      const float* tq = ts + lane * (NT + 1);
+      for (int o = g; o < RD * RD; o += 8) {
+        const int ox = o / RD, oy = o - ox * RD;
+        float val = tq[oy * WD + ox] * ((1.f - dy) * (1.f - dx));
+        val += tq[oy * WD + ox + 1] * ((1.f - dy) * dx);
+        val += tq[(oy + 1) * WD + ox] * (dy * (1.f - dx));
+        val += tq[(oy + 1) * WD + ox + 1] * (dy * dx);
+        val = val / sdiv;
+        big |= fabsf(val) > RAFT_RANGE_LIMIT;
+        out[(bn * (RD * RD) + o) * P1 + p] = val;
+      }
     }
-    if (valid && a.flow && g == 0) {
-      a.flow[((long)b * P1 + p) * a.flow_ld + 0] = x * a.coord_div - (float)(p % a.W1);
-      a.flow[((long)b * P1 + p) * a.flow_ld + 1] = y * a.coord_div - (float)(p / a.W1);
+    if (a0.range_flag && big) *a0.range_flag = 1;
+    if (valid && l == 0 && a0.flow && g == 0) {
+      a0.flow[((long)b * P1 + p) * a0.flow_ld + 0] = cur.x * cdiv - (float)(p % a0.W1);
+      a0.flow[((long)b * P1 + p) * a0.flow_ld + 1] = cur.y * cdiv - (float)(p / a0.W1);
     }
     __syncthreads();  // the tap sums are read: the band region takes the next level
+    ALT_ST(11);  // tap sums -> LDS, binning, output stores
+    cur = nxt;
   }
+#ifdef ALT_STAMPS
+  if (lane == 0 && blockIdx.x < 4096) {
+    unsigned long long* gs = g_altstamp + ((long)blockIdx.x * 8 + g) * 16;
+    for (int k = 0; k < 12; ++k) gs[k] = alt_t[k];
+    gs[12] = alt_clock() - alt_start;
+    gs[13] = (unsigned long long)alt_bands;
+  }
+#endif
 }
+
 
 // Any radius (the reference's CorrBlock / AlternateCorrBlock take any r; RAFT uses 3 and 4,
 // which the kernels above serve): one wave per query, the (2r+2)^2 tap sums in dynamic LDS
@@ -780,6 +905,12 @@ __global__ void avgpool2_nhwc_kernel(const float* in, float* out, int B, int H, 
 }
 
 }  // namespace
+
+#ifdef ALT_STAMPS
+extern "C" int raft_debug_altstamps(unsigned long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_altstamp), sizeof(unsigned long long) * (size_t)n);
+}
+#endif
 }  // namespace raft
 
 using namespace raft;

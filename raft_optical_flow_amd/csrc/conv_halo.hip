@@ -83,11 +83,12 @@ constexpr int patch_slots(int T, int U, int D) {
   }
   return 16;
 }
-constexpr int halo_lds_bytes(int T, int U, int D, int BNT, int PI) {
-  return U * (D + 1) * BNT * 128 + patch_slots(T, U, D) * PI * 1024;
+constexpr int halo_lds_bytes(int T, int U, int D, int BNT, int PI, int WR) {
+  return U * (D + 1) * BNT * WR + patch_slots(T, U, D) * PI * 1024;
 }
 
-template <int KH, int KW, int BNT>
+// WR: bytes per weight row in LDS (128: f16x3 hi | lo; 64: the one-product modes' hi half)
+template <int KH, int KW, int BNT, int WR = 128>
 struct HaloCfg {
   static constexpr int T = KH * KW;
   static constexpr int U = (BNT == 32 && T > 1) ? 4 : 2;  // K-steps per super-step
@@ -96,15 +97,15 @@ struct HaloCfg {
   static constexpr int PI = (NPIX + 7) / 8;  // 1-KiB DMA pieces per patch
   // load sets in flight ahead of the super-step: 3, or 2 where 3 does not fit
 #ifdef HALO_D  // dev builds: deeper load rings where they fit
-  static constexpr int D = halo_lds_bytes(T, U, HALO_D, BNT, PI) <= LB   ? HALO_D
-                           : halo_lds_bytes(T, U, 3, BNT, PI) <= LB ? 3
-                                                                          : 2;
+  static constexpr int D = halo_lds_bytes(T, U, HALO_D, BNT, PI, WR) <= LB   ? HALO_D
+                           : halo_lds_bytes(T, U, 3, BNT, PI, WR) <= LB ? 3
+                                                                              : 2;
 #else
-  static constexpr int D = halo_lds_bytes(T, U, 3, BNT, PI) <= LB ? 3 : 2;
+  static constexpr int D = halo_lds_bytes(T, U, 3, BNT, PI, WR) <= LB ? 3 : 2;
 #endif
   static constexpr int PA = patch_slots(T, U, D);
   static constexpr int SB = U * (D + 1);  // weight-block ring (K-steps)
-  static constexpr int LDS_B = SB * BNT * 128, LDS_A = PA * PI * 1024;
+  static constexpr int LDS_B = SB * BNT * WR, LDS_A = PA * PI * 1024;
 };
 
 #ifdef STAMPS  // dev-only phase timing (tools/conv_bench.py HSTAMPS=1 with a -DSTAMPS variant)
@@ -163,10 +164,10 @@ __device__ __forceinline__ void wait_vm_n(int n) {
 // compile exactly as without them
 template <int KH, int KW, int BNT, int PREC, bool ENC = false>
 __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
-  using C = HaloCfg<KH, KW, BNT>;
-  constexpr int T = C::T, U = C::U, D = C::D, PW = C::PW, NPIX = C::NPIX, PI = C::PI, PA = C::PA, SB = C::SB;
   constexpr bool X3 = PREC == RAFT_PREC_F16X3;
   constexpr bool BF = PREC == RAFT_PREC_BF16;
+  using C = HaloCfg<KH, KW, BNT, X3 ? 128 : 64>;
+  constexpr int T = C::T, U = C::U, D = C::D, PW = C::PW, NPIX = C::NPIX, PI = C::PI, PA = C::PA, SB = C::SB;
   // Weight rows in LDS: f16x3 the packed K-step row as it is (32 hi then 32 lo halves, 128 B);
   // the one-product modes (F16, BF16) read only hi, so only the 64-B hi half of each row
   // moves (half the weight bytes a CU ingests per K-step).  16-B quads XOR-swizzled by row
@@ -177,7 +178,15 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
   constexpr int RPP = 1024 / WROW;             // rows per 1-KiB DMA piece
   constexpr int NBI = BNT / RPP;    // 1-KiB DMA pieces per weight block (one K-step)
   constexpr int NWP = U * NBI / 4;  // weight pieces per loader wave per load set
-  constexpr int NSUB = BNT / 32;    // 32-column MFMA subtiles per compute wave
+  // Compute waves: BNT <= 64: 4 waves along M, each 32 pixels (tile rows 2w, 2w+1) x all BNT
+  // columns; BNT = 128 (the one-product modes' wide tiles): 2 x 2 waves, each 64 pixels (MF = 2
+  // MFMA row blocks) x 64 columns, half the LDS fragment bytes per MFMA
+  constexpr int MF = BNT == 128 ? 2 : 1;  // 32-pixel MFMA row blocks per compute wave
+  constexpr int WVM = 4 / MF;             // compute waves along M
+  constexpr int WCOL = BNT / MF;          // columns per compute wave
+  constexpr int NSUB = WCOL / 32;         // 32-column MFMA subtiles per compute wave
+  static_assert(!ENC || MF == 1, "the InstanceNorm partials are per 32-pixel wave");
+  static_assert(!(X3 && MF > 1), "f16x3 wide tiles exceed the register budget");
 
   // LSPLIT: the loaders stage each patch through registers and store it
   // pre-split (f16 hi | lo, the weight-row format), so the MFMA waves read
@@ -231,7 +240,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
     const bool in = j < nk;
     const int c = j / T, t = j - c * T;
     const unsigned soff = in ? (unsigned)(t * nch + c) * 128u : 0u;  // packed K-step (tap, chunk)
-    char* dst = smem + (U * (u % (D + 1)) + ew) * (BNT * 128) + wpc0 * 1024;
+    char* dst = smem + (U * (u % (D + 1)) + ew) * (BNT * WROW) + wpc0 * 1024;
 #pragma unroll
     for (int k = 0; k < NWP; ++k) dma16(rs_w, dst + k * 1024, in ? wvoff[k] : OFF_INVALID, soff);
   };
@@ -464,14 +473,19 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
 
   // ---- compute waves: fragments --------------------------------------------
   const int m = lane & 31, h = lane >> 5;
-  const int ppbase = (2 * w + (m >> 4)) * PW + (m & 15);
-  const int bsw = X3 ? (m >> 1) & 7 : (m >> 2) & 3;  // swizzle of weight row sb*32 + m
-  f32x16 acc[NSUB], accx[NSUB];
+  const int wm = w % WVM, cb = (w / WVM) * WCOL;  // the wave's pixel blocks and first column
+  int ppbase[MF];  // patch pixel of this lane's row in block f (tap 0, 0)
 #pragma unroll
-  for (int sb = 0; sb < NSUB; ++sb) {
-    acc[sb] = f32x16{};
-    accx[sb] = f32x16{};
-  }
+  for (int f = 0; f < MF; ++f) ppbase[f] = (2 * (wm * MF + f) + (m >> 4)) * PW + (m & 15);
+  const int bsw = X3 ? (m >> 1) & 7 : (m >> 2) & 3;  // swizzle of weight row cb + sb*32 + m
+  f32x16 acc[MF][NSUB], accx[MF][NSUB];
+#pragma unroll
+  for (int f = 0; f < MF; ++f)
+#pragma unroll
+    for (int sb = 0; sb < NSUB; ++sb) {
+      acc[f][sb] = f32x16{};
+      accx[f][sb] = f32x16{};
+    }
   // Fragment reads run ahead of the MFMAs: the B fragments of K-step j+1 and
   // the A (activation) values of K-step j+2 are read while K-step j's MFMAs
   // run, and A of j+1 (read one K-step earlier) is split to f16 behind them,
@@ -481,29 +495,24 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
   int b_bs = 0;
   int a_t = 0, a_ky = 0, a_kx = 0, a_ps = 0;
   struct Frag {
-    h8 ah[2], al[2];
+    h8 ah[MF][2], al[MF][2];
     h8 bh[NSUB][2], bl[NSUB][2];
   };
-  f32x4 av[4];  // raw A values of the K-step after the next
+  f32x4 av[MF][4];  // raw A values of the K-step after the next
   auto read_b = [&](Frag& F) {
-    const char* Bb = smem + b_bs * (BNT * 128);
+    const char* Bb = smem + b_bs * (BNT * WROW);
 #pragma unroll
     for (int sb = 0; sb < NSUB; ++sb) {
 #pragma unroll
       for (int qq = 0; qq < 2; ++qq) {
-        F.bh[sb][qq] = *reinterpret_cast<const h8*>(Bb + (sb * 32 + m) * WROW + (((2 * h + qq) ^ bsw) << 4));
+        F.bh[sb][qq] = *reinterpret_cast<const h8*>(Bb + (cb + sb * 32 + m) * WROW + (((2 * h + qq) ^ bsw) << 4));
         if constexpr (X3)
-          F.bl[sb][qq] = *reinterpret_cast<const h8*>(Bb + (sb * 32 + m) * WROW + (((4 + 2 * h + qq) ^ bsw) << 4));
+          F.bl[sb][qq] = *reinterpret_cast<const h8*>(Bb + (cb + sb * 32 + m) * WROW + (((4 + 2 * h + qq) ^ bsw) << 4));
       }
     }
     b_bs = b_bs + 1 == SB ? 0 : b_bs + 1;
   };
-  auto read_a = [&]() {
-    const char* Ab = smem + C::LDS_B + a_ps * (PI * 1024);
-    const int pp = ppbase + (a_ky * PW + a_kx);
-    const int sw = (((m & 15) + a_kx) >> 1) & 7;  // swizzle of patch column px
-#pragma unroll
-    for (int jq = 0; jq < 4; ++jq) av[jq] = *reinterpret_cast<const f32x4*>(Ab + pp * 128 + (((4 * h + jq) ^ sw) << 4));
+  auto advance_a = [&]() {
     ++a_kx;
     if (a_kx == KW) {
       a_kx = 0;
@@ -514,37 +523,46 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
       a_ky = 0;
       a_ps = a_ps + 1 == PA ? 0 : a_ps + 1;
     }
+  };
+  auto read_a = [&]() {
+    const char* Ab = smem + C::LDS_B + a_ps * (PI * 1024);
+    const int sw = (((m & 15) + a_kx) >> 1) & 7;  // swizzle of patch column px
+#pragma unroll
+    for (int f = 0; f < MF; ++f) {
+      const int pp = ppbase[f] + (a_ky * PW + a_kx);
+#pragma unroll
+      for (int jq = 0; jq < 4; ++jq)
+        av[f][jq] = *reinterpret_cast<const f32x4*>(Ab + pp * 128 + (((4 * h + jq) ^ sw) << 4));
+    }
+    advance_a();
   };
   auto read_a_split = [&](Frag& F) {  // LSPLIT: the patch holds f16 hi | lo quads
     const char* Ab = smem + C::LDS_B + a_ps * (PI * 1024);
-    const char* row = Ab + (ppbase + (a_ky * PW + a_kx)) * 128;
     const int sw = (((m & 15) + a_kx) >> 1) & 7;
 #pragma unroll
-    for (int qq = 0; qq < 2; ++qq) {
-      F.ah[qq] = *reinterpret_cast<const h8*>(row + (((2 * h + qq) ^ sw) << 4));
-      if constexpr (X3) F.al[qq] = *reinterpret_cast<const h8*>(row + (((4 + 2 * h + qq) ^ sw) << 4));
+    for (int f = 0; f < MF; ++f) {
+      const char* row = Ab + (ppbase[f] + (a_ky * PW + a_kx)) * 128;
+#pragma unroll
+      for (int qq = 0; qq < 2; ++qq) {
+        F.ah[f][qq] = *reinterpret_cast<const h8*>(row + (((2 * h + qq) ^ sw) << 4));
+        if constexpr (X3) F.al[f][qq] = *reinterpret_cast<const h8*>(row + (((4 + 2 * h + qq) ^ sw) << 4));
+      }
     }
-    ++a_kx;
-    if (a_kx == KW) {
-      a_kx = 0;
-      ++a_ky;
-    }
-    if (++a_t == T) {
-      a_t = 0;
-      a_ky = 0;
-      a_ps = a_ps + 1 == PA ? 0 : a_ps + 1;
-    }
+    advance_a();
   };
   auto split_a = [&](Frag& F) {
+#pragma unroll
+    for (int f = 0; f < MF; ++f) {
 #ifdef HALO_ABL_NOSPLIT  // timing ablation (dev builds only): bit casts instead of the split
-    F.ah[0] = __builtin_bit_cast(h8, av[0]);
-    F.al[0] = __builtin_bit_cast(h8, av[1]);
-    F.ah[1] = __builtin_bit_cast(h8, av[2]);
-    F.al[1] = __builtin_bit_cast(h8, av[3]);
+      F.ah[f][0] = __builtin_bit_cast(h8, av[f][0]);
+      F.al[f][0] = __builtin_bit_cast(h8, av[f][1]);
+      F.ah[f][1] = __builtin_bit_cast(h8, av[f][2]);
+      F.al[f][1] = __builtin_bit_cast(h8, av[f][3]);
 #else
-    split8<X3, BF>(av[0], av[1], F.ah[0], F.al[0]);
-    split8<X3, BF>(av[2], av[3], F.ah[1], F.al[1]);
+      split8<X3, BF>(av[f][0], av[f][1], F.ah[f][0], F.al[f][0]);
+      split8<X3, BF>(av[f][2], av[f][3], F.ah[f][1], F.al[f][1]);
 #endif
+    }
   };
   // the MFMAs of one accumulator never follow each other back to back
   auto mfma_step = [&](const Frag& F) {
@@ -552,21 +570,29 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
     for (int qq = 0; qq < 2; ++qq) {
       if constexpr (BF) {
 #pragma unroll
-        for (int sb = 0; sb < NSUB; ++sb)
-          acc[sb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8, F.ah[qq]),
-                                                            __builtin_bit_cast(bf8, F.bh[sb][qq]), acc[sb], 0, 0, 0);
+        for (int f = 0; f < MF; ++f)
+#pragma unroll
+          for (int sb = 0; sb < NSUB; ++sb)
+            acc[f][sb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                __builtin_bit_cast(bf8, F.ah[f][qq]), __builtin_bit_cast(bf8, F.bh[sb][qq]), acc[f][sb], 0, 0, 0);
       } else {
 #pragma unroll
-        for (int sb = 0; sb < NSUB; ++sb)
-          acc[sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.ah[qq], F.bh[sb][qq], acc[sb], 0, 0, 0);
+        for (int f = 0; f < MF; ++f)
+#pragma unroll
+          for (int sb = 0; sb < NSUB; ++sb)
+            acc[f][sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.ah[f][qq], F.bh[sb][qq], acc[f][sb], 0, 0, 0);
       }
       if constexpr (X3) {
 #pragma unroll
-        for (int sb = 0; sb < NSUB; ++sb)
-          accx[sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.ah[qq], F.bl[sb][qq], accx[sb], 0, 0, 0);
+        for (int f = 0; f < MF; ++f)
 #pragma unroll
-        for (int sb = 0; sb < NSUB; ++sb)
-          acc[sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.al[qq], F.bh[sb][qq], acc[sb], 0, 0, 0);
+          for (int sb = 0; sb < NSUB; ++sb)
+            accx[f][sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.ah[f][qq], F.bl[sb][qq], accx[f][sb], 0, 0, 0);
+#pragma unroll
+        for (int f = 0; f < MF; ++f)
+#pragma unroll
+          for (int sb = 0; sb < NSUB; ++sb)
+            acc[f][sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.al[f][qq], F.bh[sb][qq], acc[f][sb], 0, 0, 0);
       }
     }
   };
@@ -602,7 +628,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
     for (int e = 0; e < U; ++e) {
 #ifdef HALO_ABL_MFMAONLY  // timing ablation (dev builds only): MFMAs on fragments read once
       mfma_step(F[e & 1]);
-      asm volatile("" ::"v"(F[0].ah[0]), "v"(F[1].ah[0]));
+      asm volatile("" ::"v"(F[0].ah[0][0]), "v"(F[1].ah[0][0]));
 #else
       if constexpr (LSPLIT) {
         read_b(F[(e + 1) & 1]);
@@ -638,25 +664,30 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
 #endif
   if constexpr (X3) {
 #pragma unroll
-    for (int sb = 0; sb < NSUB; ++sb)
+    for (int f = 0; f < MF; ++f)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[sb][r] += accx[sb][r] * (1.0f / SPLIT_SCALE);
+      for (int sb = 0; sb < NSUB; ++sb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[f][sb][r] += accx[f][sb][r] * (1.0f / SPLIT_SCALE);
   }
 
-  // ---- epilogue: register r holds tile row m = (r&3) + 8(r>>2) + 4h of this wave's 32
-  int rows[16];
+  // ---- epilogue: register r of block f holds row m = (r&3) + 8(r>>2) + 4h of its 32 pixels
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int mm = (r & 3) + 8 * (r >> 2) + 4 * h;
-    const int y = y0 + 2 * w + (mm >> 4), x = x0 + (mm & 15);
-    rows[r] = (y < p.out_h && x < p.out_w) ? (b * p.out_h + y) * p.out_w + x : -1;
-  }
+  for (int f = 0; f < MF; ++f) {
+    int rows[16];
 #pragma unroll
-  for (int sb = 0; sb < NSUB; ++sb) tile_epilogue(p, rows, n0 + sb * 32 + m, acc[sb]);
-  if constexpr (ENC) {
-    if (p.stats_part) {  // InstanceNorm partials of the raw output (slot: spatial tile x 4 + wave)
+    for (int r = 0; r < 16; ++r) {
+      const int mm = (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int y = y0 + 2 * (wm * MF + f) + (mm >> 4), x = x0 + (mm & 15);
+      rows[r] = (y < p.out_h && x < p.out_w) ? (b * p.out_h + y) * p.out_w + x : -1;
+    }
 #pragma unroll
-      for (int sb = 0; sb < NSUB; ++sb) tile_stats(p, rows, n0 + sb * 32 + m, acc[sb], (long)st * 4 + w);
+    for (int sb = 0; sb < NSUB; ++sb) tile_epilogue(p, rows, n0 + cb + sb * 32 + m, acc[f][sb]);
+    if constexpr (ENC) {
+      if (p.stats_part) {  // InstanceNorm partials of the raw output (slot: spatial tile x 4 + wave)
+#pragma unroll
+        for (int sb = 0; sb < NSUB; ++sb) tile_stats(p, rows, n0 + sb * 32 + m, acc[f][sb], (long)st * 4 + w);
+      }
     }
   }
 #ifdef STAMPS
@@ -680,6 +711,12 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
 template <int KH, int KW, int PREC>
 void launch_halo_p(const HaloLaunch& l, int bn, dim3 grid, hipStream_t s) {
   const raft_conv2d_params& p = l.a[0].p;
+  if constexpr (PREC != RAFT_PREC_F16X3) {
+    if (bn == 128) {  // (conv_halo_launch picks it only without stats_part / in_norm)
+      hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 128, PREC>), grid, dim3(512), 0, s, l);
+      return;
+    }
+  }
   if constexpr ((KH == 1 && KW == 1) || (KH == 3 && KW == 3)) {
     if (p.stats_part || p.in_norm) {  // (one conv per launch: raft_conv2d_pair takes neither)
       if (bn == 64)
@@ -776,13 +813,26 @@ int conv_halo_stats_slots(const HaloOperands& o) {
 
 // Launches the halo kernel when the conv is one it covers; returns 1 without launching
 // otherwise.  Arguments are already validated by raft_conv2d.
+bool halo_wide_enabled() {
+  static const bool enabled = [] {
+    const char* e = getenv("RAFT_HALO_WIDE");
+    return !(e && e[0] == '0');
+  }();
+  return enabled;
+}
+
 int conv_halo_launch(const HaloOperands& o, hipStream_t s) {
   HaloLaunch l;
   if (!halo_enabled() || !halo_problem(o, l.a[0])) return 1;
   const long spatial = halo_spatial(l.a[0]);
+  const raft_conv2d_params& p = o.p;
   // one work-group per CU (LDS): 64 output channels per work-group unless
-  // 32 still fits the grid in one round of 256 CUs with half of them idle at 64
-  const int bn = spatial * (o.n_pad / 64) > 128 ? 64 : 32;
+  // 32 still fits the grid in one round of 256 CUs with half of them idle at 64;
+  // the one-product modes take 128-column tiles (2 x 2 waves of 64 x 64) where that still
+  // leaves two rounds of work-groups (configs 3 - 5; RAFT_HALO_WIDE=0: never)
+  const bool wide = p.precision != RAFT_PREC_F16X3 && !p.stats_part && !p.in_norm && o.n_pad % 128 == 0 &&
+                    spatial * (o.n_pad / 128) >= 512 && halo_wide_enabled();
+  const int bn = wide ? 128 : spatial * (o.n_pad / 64) > 128 ? 64 : 32;
   l.a[0].gn = o.n_pad / bn;
   const long tiles = spatial * l.a[0].gn;
   if (tiles >= (1L << 31)) return 1;

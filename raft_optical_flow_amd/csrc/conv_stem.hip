@@ -7,7 +7,8 @@
 // (2*8+5) x (2*16+5) pixels x 3 channels = 9.3 KB of fp32 in LDS, read as contiguous 111-float
 // rows.  The im2col operand is never built: each MFMA lane reads its 8 K values of a fragment
 // straight from the patch through a 160-entry offset table (k -> ky*111 + kx*3 + c, the GATHER
-// packing's k order), splits them to f16 hi | lo (or rounds to f16 / bf16) in registers, and
+// packing's k order; the 13 K-padding entries clamp to a zero sentinel past the patch, never
+// to LDS outside it), splits them to f16 hi | lo (or rounds to f16 / bf16) in registers, and
 // multiplies them with the pre-split weight staged in LDS once per work-group (40 KB, XOR-
 // swizzled rows).  Work-groups walk tiles (three per CU), so the weight staging is paid once
 // per ~2 tiles at config 2; the epilogue: bias, linear or relu, the range guard.
@@ -79,7 +80,10 @@ __global__ __launch_bounds__(256, 3) void conv_stem_kernel(StemArgs sa) {  // 3 
     __syncthreads();
     // wave w: output rows 2w, 2w+1 (32 pixels) x 64 outputs; lane m = pixel (row 2w + m/16, col m%16)
     const int py = 2 * w + (m >> 4), px = m & 15;
-    const float* pb = patch + py * ST_S * ST_ROW + px * ST_S * ST_C;
+    // the lane's window origin in the patch; a K-padding entry (koff = ST_PATCH) clamps to the
+    // zero sentinel (every real tap lies below it: base + koff <= ST_PATCH - 1)
+    const int pbase = py * ST_S * ST_ROW + px * ST_S * ST_C;
+    auto at = [&](int o) { return patch[min(pbase + o, ST_PATCH)]; };
     f32x16 acc[2] = {}, accx[2] = {};
 #pragma unroll
     for (int j = 0; j < ST_KS; ++j) {
@@ -88,8 +92,8 @@ __global__ __launch_bounds__(256, 3) void conv_stem_kernel(StemArgs sa) {  // 3 
       for (int qq = 0; qq < 2; ++qq) {
         const int4 o0 = *reinterpret_cast<const int4*>(&koff[32 * j + 8 * (2 * h + qq)]);
         const int4 o1 = *reinterpret_cast<const int4*>(&koff[32 * j + 8 * (2 * h + qq) + 4]);
-        const f32x4 x0 = {pb[o0.x], pb[o0.y], pb[o0.z], pb[o0.w]};
-        const f32x4 x1 = {pb[o1.x], pb[o1.y], pb[o1.z], pb[o1.w]};
+        const f32x4 x0 = {at(o0.x), at(o0.y), at(o0.z), at(o0.w)};
+        const f32x4 x1 = {at(o1.x), at(o1.y), at(o1.z), at(o1.w)};
         split8<X3, BF>(x0, x1, ah[qq], al[qq]);
       }
 #pragma unroll

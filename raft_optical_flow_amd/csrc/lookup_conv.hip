@@ -463,6 +463,10 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
   };
   store(acc, c1b, g.out, g.out_ld, 32 * wv + m, g.out_flag);
   if (wv < LC_F1N / 32) store(facc, f1b, g.f1out, g.f1out_ld, 32 * wv + m, g.f1flag);
+#ifdef LC_END_FENCE  // dev experiment: agent-scope release of the outputs before the waves exit
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __builtin_amdgcn_s_waitcnt(0);
+#endif
 #ifdef LC_STAMPS
   __builtin_amdgcn_s_waitcnt(0);
   LC_STAMP(6);

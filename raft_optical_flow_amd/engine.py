@@ -130,6 +130,16 @@ class PackedUpdate:
             bctx = torch.cat([cz.bias, cr.bias, cq.bias], 0)
             ctx = pack_conv(wctx, bctx, 1, cz.padding, device=device)
             self.gru.append((zr, q, ctx))
+        # the first half-step's z|r conv split by input columns (gru_hside): the h columns (h is
+        # known one iteration ahead, so this part can run beside the flow head and the motion
+        # encoder) and the motion | flow columns (after the motion encoder)
+        self.zr1_h = self.zr1_x = None
+        if not small:
+            cz, cr, _ = steps[0]
+            wzr = torch.cat([cz.weight, cr.weight], 0).detach()
+            self.zr1_h = pack_conv(wzr[:, hcols], None, 1, cz.padding, device=device)
+            self.zr1_x = pack_conv(wzr[:, mcols], None, 1, cz.padding, seg_real=[mc + 2], seg_decl=[mc + 2 + pad],
+                                   device=device)
         self.fh1 = pack_conv(fh.conv1.weight, fh.conv1.bias, 1, 1, device=device)
         self.fh2 = pack_conv(fh.conv2.weight, fh.conv2.bias, 1, 1, device=device)
         if not small:
@@ -353,6 +363,7 @@ class UpdateBuffers:
         self.rh = A.rows(P, hd)
         self.ctx = [A.rows(P, 3 * hd) for _ in pu.gru]   # z | r | q context terms per half-step
         self.coords = A.rows(P, 2)
+        self.pre_zr1 = A.rows(P, 2 * hd) if gru_hside(pu) else None  # h part + context of zr1
 
     # channel slots of HX
     def h(self, pu):
@@ -374,6 +385,20 @@ class UpdateBuffers:
     def x_dyn(self, pu):
         """motion | flow (| pad): the second segment of the q GEMM's input."""
         return Rows(self.hx, pu.hdim, pu.inp_off - pu.hdim)
+
+
+def gru_hside(pu: PackedUpdate) -> bool:
+    """Whether the first GRU half-step's z|r conv runs as an h-part on the side stream (issued
+    right after the previous iteration's h is final, beside the flow head, the next lookup and
+    the motion encoder) plus a motion|flow part on the main stream (RAFT_GRU_HSIDE=1)."""
+    return pu.zr1_h is not None and os.environ.get("RAFT_GRU_HSIDE", "0") == "1"
+
+
+def plan_zr1_hpart(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, side: bool):
+    """W_zr1[h columns] * h + the z|r context terms -> ub.pre_zr1 (the addend of zr1's x part)."""
+    hd = pu.hdim
+    _conv(L, pu.zr1_h, ub.h(pu), B, h, w, Rows(ub.pre_zr1), epilogue=_lib.EPI_LINEAR,
+          add0=Rows(ub.ctx[0]).sub(0, 2 * hd), range_flag=None, side=side)
 
 
 def plan_gru_context(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w):
@@ -435,7 +460,7 @@ def frag_weight(pc) -> torch.Tensor:
 
 
 def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool, convf1_done: bool = False,
-                convc1_done: bool = False):
+                convc1_done: bool = False, last: bool = True, hside_ok: bool = False):
     """One BasicUpdateBlock / SmallUpdateBlock step (core/update.py:297-325 / :250-263)
     followed by coords1 += delta_flow (core/raft.py:232).  Assumes ub.corr and the
     flow slot of HX were filled by the lookup and plan_gru_context ran for this pair
@@ -476,13 +501,23 @@ def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool
     _conv(L, pu.conv, cf, B, h, w, ub.motion(pu), epilogue=_lib.EPI_RELU)
     hd = pu.hdim
     hrows = ub.h(pu)
-    for (zr, q, _), ctx in zip(pu.gru, ub.ctx):
+    hside = hside_ok and gru_hside(pu)  # (RaftPlan only: it issues the h part before the loop)
+    for i, ((zr, q, _), ctx) in enumerate(zip(pu.gru, ub.ctx)):
         c = Rows(ctx)
         # (z, r*h and the new h are sigmoid / tanh blends of |h| <= 1: no range guard)
+        if i == 0 and hside:
+            L.append(K.JOIN)  # the h part (side stream) has landed in pre_zr1
+            _conv(L, pu.zr1_x, ub.x_dyn(pu), B, h, w, Rows(ub.z), epilogue=_lib.EPI_GRU_ZR, split=hd, aux0=hrows,
+                  out1=Rows(ub.rh), add0=Rows(ub.pre_zr1), range_flag=None)
+            continue
         _conv(L, zr, ub.gru_in(pu), B, h, w, Rows(ub.z), epilogue=_lib.EPI_GRU_ZR, split=hd, aux0=hrows,
               out1=Rows(ub.rh), add0=c.sub(0, 2 * hd), range_flag=None)
         _conv(L, q, Rows(ub.rh), B, h, w, hrows, src1=ub.x_dyn(pu), epilogue=_lib.EPI_GRU_Q, aux0=hrows,
               aux1=Rows(ub.z), add0=c.sub(2 * hd, hd), range_flag=None)
+    if hside and not last:
+        # the next iteration's zr1 h part: h is final here
+        L.append(K.FORK)
+        plan_zr1_hpart(L, pu, ub, B, h, w, side=True)
     coords = Rows(ub.coords)
     if pu.small:
         _conv(L, pu.fh1, hrows, B, h, w, Rows(ub.fh), epilogue=_lib.EPI_RELU, range_flag=None)  # feeds fp32 fh2
@@ -594,6 +629,9 @@ class RaftPlan:
             L.append(K.JOIN)
         L.append(Launch("raft_init_coords", ub.coords.data_ptr(),
                         self.flow_init.data_ptr() if self.flow_init is not None else None, B, h, w))
+        if gru_hside(pu):
+            L.append(K.FORK)
+            plan_zr1_hpart(L, pu, ub, B, h, w, side=True)
         self.loop_start = len(L)
         self.flow_up = [torch.empty(B, 2, H, W, device=device) for _ in range(1 if test_mode else iters)]
         flow_slot = ub.flow_off(pu)
@@ -641,7 +679,7 @@ class RaftPlan:
                                     ub.flo1.shape[1], gflag, keep=f1w))
             want_up = last or not test_mode
             plan_update(L, pu, ub, B, h, w, with_mask=want_up and not pu.small, convf1_done=fuse_f1,
-                        convc1_done=fuse_c1)
+                        convc1_done=fuse_c1, last=last, hside_ok=True)
             if want_up:
                 dst = self.flow_up[-1 if test_mode else it]
                 if pu.small:

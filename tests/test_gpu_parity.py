@@ -631,6 +631,37 @@ def test_conv2d_vs_torch_fp64(cin, cout, kh, kw, stride, pad, H, W, B, prec):
     assert err < CONV_TOL[prec] * max(1.0, float(ref.abs().max())), err
 
 
+@pytest.mark.parametrize("prec", ["bf16", "f16"])
+@pytest.mark.parametrize("cin,cout,kh,kw,H,W", [
+    (96, 256, 3, 3, 60, 70),    # ragged tiles in both axes, 640 128-column tiles
+    (128, 128, 1, 5, 60, 130),  # N = 128: one column tile per spatial tile, 576 tiles
+    (64, 256, 5, 1, 61, 64),
+    (64, 256, 1, 1, 60, 70),
+])
+def test_conv_halo_wide_tiles_multi_round(cin, cout, kh, kw, H, W, prec):
+    """The one-product modes' 128-column halo tiles (2 x 2 waves of 64 pixels x 64 columns, chosen
+    for convs with >= 2 rounds of work-groups: configs 3 - 5) vs torch fp64 on the first and last
+    image; the output row padding stays untouched."""
+    from raft_optical_flow_amd import kernels as K
+    from raft_optical_flow_amd import _lib
+    B = 8
+    g = torch.Generator().manual_seed(cin + cout + kh)
+    x = torch.randn(B, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, kh, kw, generator=g) / np.sqrt(cin * kh * kw)
+    b = torch.randn(cout, generator=g)
+    pad = ((kh - 1) // 2, (kw - 1) // 2)
+    pc = K.pack_conv(w, b, 1, pad, device=DEV)
+    pc.precision = _lib.PRECISIONS[prec]
+    src = K.Rows(K.nchw_to_rows(x.to(DEV)))
+    out = K.Rows(torch.full((B * H * W, cout + 4), -7.0, device=DEV), 0, cout)
+    K.conv2d_rows(pc, src, B, H, W, out, epilogue=_lib.EPI_RELU)
+    y = K.rows_to_nchw(out, B, H, W)
+    for i in (0, B - 1):
+        ref = torch.relu(F.conv2d(x[i:i + 1].double(), w.double(), b.double(), 1, pad))
+        assert maxabs(y[i:i + 1], ref) < CONV_TOL[prec] * max(1.0, float(ref.abs().max())), i
+    assert bool((out.t[:, cout:] == -7.0).all())
+
+
 @pytest.mark.parametrize("prec", ["f16x3", "bf16"])
 def test_conv_stem_full_size_relu(prec):
     """The encoders' 7x7 / stride-2 stem (conv_stem.hip) at config 2's size (440x1024 -> 220x512:
@@ -825,6 +856,24 @@ def test_raft_e2e_golden(name, small, alt, prec):
         low, up = m(t(g["image1"]), t(g["image2"]), iters=int(g["iters"]), test_mode=True)
     assert maxabs(low, g["flow_low"]) < 1e-3
     assert maxabs(up, g["flow_up"]) < 1e-3
+
+
+def test_raft_gru_hside_golden_and_graph(monkeypatch):
+    """RAFT_GRU_HSIDE=1 (zr1's h part on the side stream, one iteration ahead): the reference
+    golden within 1e-3, and eager == graph replay bit for bit."""
+    monkeypatch.setenv("RAFT_GRU_HSIDE", "1")
+    g = load_golden("raft_full_smooth_b2_128x192_i12.npz")
+    m, _ = make_model(False, int(g["seed"]), precision="f16x3")
+    i1, i2 = t(g["image1"]), t(g["image2"])
+    with torch.no_grad():
+        low0, up0 = m(i1, i2, iters=12, test_mode=True)
+        pl = m.plan(2, 128, 192, 12, True)
+        assert pl.kernel_names().count("raft_conv2d") > 0 and pl.pk.update.zr1_h is not None
+        low1, up1 = m(i1, i2, iters=12, test_mode=True)
+        assert pl.graph is not None
+    assert maxabs(low0, g["flow_low"]) < 1e-3
+    assert maxabs(up0, g["flow_up"]) < 1e-3
+    assert maxabs(low1, low0) == 0.0 and maxabs(up1, up0) == 0.0
 
 
 def test_raft_train_mode_output_list_and_graph_replay():
