@@ -139,7 +139,10 @@ def halo_bn(ns, batch, h, w):
 
 
 def launch_convs(l):
-    """The raft_conv2d_params of a conv launch: one, or the two of a raft_conv2d_pair."""
+    """The raft_conv2d_params of a conv launch: one, the two of a raft_conv2d_pair, or every conv
+    of a raft_conv2d_chain."""
+    if l.name == "raft_conv2d_chain":
+        return tuple(l.keep[1])
     return l.keep if isinstance(l.keep, tuple) else (l.keep,)
 
 
@@ -385,7 +388,7 @@ def main():
     iteration = {"launches": len(it_all), "iteration_us": round(t_it * 1e6, 1),
                  "timing": "HIP events around a hipGraph of 20 replays of one iteration's launches"}
     it_convs = [plan.launches[i] for i in range(lk_idx[per_it] + 1, lk_idx[2 * per_it])
-                if getattr(plan.launches[i], "name", "") in ("raft_conv2d", "raft_conv2d_pair")
+                if getattr(plan.launches[i], "name", "") in ("raft_conv2d", "raft_conv2d_pair", "raft_conv2d_chain")
                 and not plan.launches[i].side]
     t_upd = time_kernel_events(lambda: [l(K.stream_handle()) for l in it_convs], 20)
     fl = P * sum(2 * c.n * c.kh * c.kw * (c.in0_c + c.in1_c) for l in it_convs for c in launch_convs(l))
@@ -401,8 +404,20 @@ def main():
     dom = [l for l in it_convs
            if all(c.kh == 3 and c.kw == 3 and c.n > 4 and c.precision != 0 for c in launch_convs(l))
            and halo_bn([c.n for c in launch_convs(l)], args.batch, h8, w8) == 64]
+    chained = [l for l in it_convs if l.name == "raft_conv2d_chain"]
     dominant = None
-    if dom:
+    if chained:
+        # the chained launch (conv_chain_kernel): every update conv from convc2|convf2 to the flow
+        # head's conv1 in one persistent launch, flops 2*M*N*K per conv
+        cfl = sum(2 * P * c.n * c.kh * c.kw * (c.in0_c + c.in1_c) for l in chained for c in launch_convs(l))
+        dt = time_kernel_events(lambda: [l(K.stream_handle()) for l in chained], 50)
+        dominant = {"kernel": "conv_chain_kernel<f16x3> (raft_conv2d_chain: convc2|convf2, conv, z|r1, q1, z|r2, q2, "
+                              "flow-head conv1 of one iteration, one launch)",
+                    "bound": "mfma", "achieved": round(cfl / dt / 1e12, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+                    "frac": round(cfl / dt / 1e12 / peak, 4), "launches": len(chained),
+                    "launch_us": round(dt / len(chained) * 1e6, 2), "flops_per_launch": cfl // len(chained),
+                    "timing": "HIP events around a hipGraph of 50 replays of that launch"}
+    elif dom:
         dfl = sum(2 * P * c.n * 9 * (c.in0_c + c.in1_c) for l in dom for c in launch_convs(l))
         dt = time_kernel_events(lambda: [l(K.stream_handle()) for l in dom], 50)
         dominant = {"kernel": "conv_halo_kernel<3,3,64> (the convc2 | convf2 pair and the flow-head conv1 of one "

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define RAFT_HIP_ABI_VERSION 11
+#define RAFT_HIP_ABI_VERSION 12
 
 /* Negative return codes (argument errors, raised before any launch). */
 #define RAFT_E_INVALID (-1)   /* bad size / null pointer / unsupported shape */
@@ -337,6 +337,24 @@ int raft_conv2d(const raft_conv2d_params* p, raft_stream_t stream);
  * edge on ROCm).  Otherwise, or when one reads what the other writes, or both write a common
  * element (column ranges of their output rows meet), the two run in order. */
 int raft_conv2d_pair(const raft_conv2d_params* p0, const raft_conv2d_params* p1, raft_stream_t stream);
+/* Dependent convolutions in ONE launch (core/update.py:74-121,169-216,297-325: the update block's
+ * convc2|convf2 -> conv -> convz1|convr1 -> convq1 -> convz2|convr2 -> convq2 -> flow-head conv1
+ * sequence of one refinement iteration).  stages[2s] is stage s's conv and stages[2s+1] NULL or a
+ * second, independent conv of the stage (as raft_conv2d_pair); stage s+1 may read anything
+ * stages <= s wrote.  Results are identical to raft_conv2d / raft_conv2d_pair of the stages in
+ * order.  When every stage is a halo-kernel conv (stride 1, "same", 3x3 / 1x5 / 5x1,
+ * RAFT_PREC_F16X3, no stats_part / in_norm) of one output size, the stages run as one persistent
+ * launch whose tiles wait on completion counters of their 3x3 spatial neighbourhood in the
+ * previous stage (no kernel boundary between the stages); otherwise they run in order.
+ * sync: raft_conv2d_chain_sync_ints(n_stages, batch, out_h, out_w) ints in device memory, zeroed
+ * once before the first call (every launch leaves them zeroed), not shared by launches that may
+ * run concurrently (NULL: run in order).  err: optional device int set to 1 if a wait timed out
+ * (the results are then invalid), e.g. a range flag (RAFT_RANGE_LIMIT) that re-runs the work. */
+int raft_conv2d_chain_sync_ints(int n_stages, int batch, int out_h, int out_w);
+int raft_conv2d_chain(const raft_conv2d_params* const* stages, int n_stages, int* sync, int* err,
+                      raft_stream_t stream);
+/* 1 when raft_conv2d_chain (with a sync buffer) runs these stages as one chained launch, else 0. */
+int raft_conv2d_chain_covered(const raft_conv2d_params* const* stages, int n_stages);
 /* fp32 packed weight [n_pad][k_pad] -> split form for RAFT_PREC_F16X3 / F16:
  * per row and 32-wide K-step, 32 f16 hi then 32 f16 lo (lo scaled by 2048);
  * out holds n_pad*k_pad*4 bytes, like the input. */

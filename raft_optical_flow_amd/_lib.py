@@ -29,7 +29,7 @@ PREC_F16 = 2     # single f16 product (mixed precision)
 PREC_BF16 = 3    # single bf16 product on v_mfma_f32_32x32x16_bf16 (bf16 mixed precision)
 PRECISIONS = {"fp32": PREC_FP32, "f16x3": PREC_F16X3, "f16": PREC_F16, "bf16": PREC_BF16}
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 RANGE_LIMIT = 32768.0  # RAFT_RANGE_LIMIT: |x| above it raises the f16x3 range guard
 
 EPI_LINEAR = 0
@@ -103,6 +103,9 @@ _PROTOS = {
                                          ctypes.POINTER(c_int)]),
     "raft_conv2d": (c_int, [ctypes.POINTER(ConvParams), P]),
     "raft_conv2d_pair": (c_int, [ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), P]),
+    "raft_conv2d_chain_sync_ints": (c_int, [c_int, c_int, c_int, c_int]),
+    "raft_conv2d_chain": (c_int, [ctypes.POINTER(ctypes.POINTER(ConvParams)), c_int, P, P, P]),
+    "raft_conv2d_chain_covered": (c_int, [ctypes.POINTER(ctypes.POINTER(ConvParams)), c_int]),
     "raft_conv2d_stats_slots": (c_int, [ctypes.POINTER(ConvParams)]),
     "raft_conv2d_in_norm_ok": (c_int, [ctypes.POINTER(ConvParams)]),
     "raft_instnorm_merge": (c_int, [P, c_int, c_int, c_int, c_int, c_float, P, P]),

@@ -8,6 +8,7 @@ namespace raft {
 namespace {
 
 using h4 = __attribute__((ext_vector_type(4))) _Float16;
+using v4u = __attribute__((ext_vector_type(4))) unsigned;
 using h8 = __attribute__((ext_vector_type(8))) _Float16;
 using bf4 = __attribute__((ext_vector_type(4))) __bf16;
 using bf8 = __attribute__((ext_vector_type(8))) __bf16;
@@ -131,15 +132,48 @@ __device__ __forceinline__ long row_of(int mb, int r) { return mb + (r & 3) + 8 
 __device__ __forceinline__ unsigned eidx(int row, int ld, int col) {
   return (unsigned)(row < 0 ? 0 : row) * (unsigned)ld + (unsigned)col;
 }
+// WT: sc1 loads (served past the CU's L1: data another work-group of the launch wrote through)
+template <bool WT = false>
 __device__ __forceinline__ void load_rows(const float* base, int ld, const int (&rows)[16], int col, float (&t)[16]) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) t[r] = base[eidx(rows[r], ld, col)];
+  for (int r = 0; r < 16; ++r) {
+    if constexpr (WT)
+      t[r] = __hip_atomic_load(base + eidx(rows[r], ld, col), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      t[r] = base[eidx(rows[r], ld, col)];
+  }
 }
 
 // branch-free activations (no per-row control flow between the stores)
 __device__ __forceinline__ float sigmoid_bf(float x) { return __frcp_rn(1.0f + __expf(-x)); }
 __device__ __forceinline__ float tanh_bf(float x) { return 1.0f - 2.0f * __frcp_rn(__expf(2.0f * x) + 1.0f); }
 
+constexpr int CPOL_SC1 = 16;  // buffer cache-policy bit sc1 (gfx950): write-through to memory
+
+// 4x4 transpose across the four lanes of a quad: lane q's x[i] <- lane i's x[q] (two exchange
+// steps, with lane q^1 then lane q^2, by DPP quad permutes)
+__device__ __forceinline__ void quad_transpose(float (&x)[4]) {
+  const int q = threadIdx.x & 3;
+  float y[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float nb = __builtin_bit_cast(
+        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x[i ^ 1]), 0xB1, 0xF, 0xF, false));
+    y[i] = ((i ^ q) & 1) ? nb : x[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float nb = __builtin_bit_cast(
+        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, y[i ^ 2]), 0x4E, 0xF, 0xF, false));
+    x[i] = ((i ^ q) & 2) ? nb : y[i];
+  }
+}
+
+// WT: write-through stores (sc1: the bytes leave the XCD's L2 at once), for outputs another
+// work-group of the same launch reads after a completion counter (conv_chain_kernel); each lane
+// stores 16 B (4 columns of one row, after a quad transpose) where the destination allows it:
+// a 4-B sc1 store is a fabric write of its own
+template <bool WT = false>
 __device__ __forceinline__ void tile_epilogue(const raft_conv2d_params& p, const int (&rows)[16], int n,
                                               const f32x16& acc) {
   const bool ncol = n < p.n;
@@ -150,7 +184,7 @@ __device__ __forceinline__ void tile_epilogue(const raft_conv2d_params& p, const
   for (int r = 0; r < 16; ++r) v[r] = acc[r] + bias;
   if (p.add0) {
     float t[16];
-    load_rows(p.add0, p.add0_ld, rows, nc, t);
+    load_rows<WT>(p.add0, p.add0_ld, rows, nc, t);
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] += t[r];
   }
@@ -166,7 +200,7 @@ __device__ __forceinline__ void tile_epilogue(const raft_conv2d_params& p, const
     for (int r = 0; r < 16; ++r) v[r] = fmaxf(v[r], 0.f);
   } else if (epi == RAFT_EPI_RESID_RELU) {
     float t[16];
-    load_rows(p.aux0, p.aux0_ld, rows, nc, t);
+    load_rows<WT>(p.aux0, p.aux0_ld, rows, nc, t);
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = fmaxf(t[r] + fmaxf(v[r], 0.f), 0.f);
   } else if (epi == RAFT_EPI_GRU_ZR) {
@@ -176,7 +210,7 @@ __device__ __forceinline__ void tile_epilogue(const raft_conv2d_params& p, const
     } else {
       col = nc - p.split;
       float t[16];
-      load_rows(p.aux0, p.aux0_ld, rows, col, t);
+      load_rows<WT>(p.aux0, p.aux0_ld, rows, col, t);
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = sigmoid_bf(v[r]) * t[r];
       dst = p.out1;
@@ -184,8 +218,8 @@ __device__ __forceinline__ void tile_epilogue(const raft_conv2d_params& p, const
     }
   } else if (epi == RAFT_EPI_GRU_Q) {
     float h[16], z[16];
-    load_rows(p.aux0, p.aux0_ld, rows, nc, h);
-    load_rows(p.aux1, p.aux1_ld, rows, nc, z);
+    load_rows<WT>(p.aux0, p.aux0_ld, rows, nc, h);
+    load_rows<WT>(p.aux1, p.aux1_ld, rows, nc, z);
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = (1.0f - z[r]) * h[r] + z[r] * tanh_bf(v[r]);
   } else if (epi == RAFT_EPI_TANH_RELU) {
@@ -201,7 +235,7 @@ __device__ __forceinline__ void tile_epilogue(const raft_conv2d_params& p, const
     }
   } else if (epi == RAFT_EPI_ADD_TO_OUT) {
     float t[16];
-    load_rows(p.out, p.out_ld, rows, nc, t);
+    load_rows<WT>(p.out, p.out_ld, rows, nc, t);
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] += t[r];
   }
@@ -211,9 +245,40 @@ __device__ __forceinline__ void tile_epilogue(const raft_conv2d_params& p, const
     for (int r = 0; r < 16; ++r) big |= ncol && rows[r] >= 0 && fabsf(v[r]) > RAFT_RANGE_LIMIT;
     if (big) *p.range_flag = 1;
   }
+  if constexpr (WT) {
+    if ((((uintptr_t)dst) & 15) == 0 && (ld & 3) == 0) {
+      // lane q of a quad owns columns col - q .. col - q + 3 of rows[4j + q] after the transpose
+      const int q = threadIdx.x & 3;
+      const int c0 = col - q, nq = n - q;  // the quad's first column (destination / conv numbering)
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float x[4] = {v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]};
+        quad_transpose(x);
+        const int row = q == 0 ? rows[4 * j] : q == 1 ? rows[4 * j + 1] : q == 2 ? rows[4 * j + 2] : rows[4 * j + 3];
+        if (row < 0) continue;
+        const unsigned off = ((unsigned)row * (unsigned)ld + (unsigned)c0) * 4u;
+        if (nq + 3 < p.n) {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, f32x4{x[0], x[1], x[2], x[3]}), rs, off, 0,
+                                                 CPOL_SC1);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (nq + i < p.n) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x[i]), rs, off + 4u * i, 0,
+                                                                   CPOL_SC1);
+        }
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int r = 0; r < 16; ++r)
-    if (ncol && rows[r] >= 0) dst[eidx(rows[r], ld, col)] = v[r];
+    if (ncol && rows[r] >= 0) {
+      if constexpr (WT)
+        __hip_atomic_store(dst + eidx(rows[r], ld, col), v[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        dst[eidx(rows[r], ld, col)] = v[r];
+    }
 }
 
 // InstanceNorm partial statistics of one wave's 32x32 accumulator tile (raft_conv2d_stats_slots):
@@ -249,8 +314,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, unsig
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
 
+template <int CPOL = 0>
 __device__ __forceinline__ f32x4 buf_load4(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, CPOL));
 }
 
 }  // namespace
@@ -267,6 +333,11 @@ struct HaloOperands {
 int conv_halo_launch(const HaloOperands& o, hipStream_t s);
 // two independent convs of one shape class in one launch; 1 (nothing launched) if they do not qualify
 int conv_halo_launch_pair(const HaloOperands& o0, const HaloOperands& o1, hipStream_t s);
+// dependent stride-1 conv stages (nconv[s] = 1 or 2 convs each, ops in stage order) as one
+// persistent launch (conv_chain_kernel); 1 (nothing launched) if they do not qualify
+int conv_halo_launch_chain(const HaloOperands* ops, const int* nconv, int n_stages, int* sync, int* err,
+                           hipStream_t s);
+int conv_halo_chain_sync_ints(int n_stages, int batch, int out_h, int out_w);
 // conv_stem.hip: the encoders' 7x7 / stride-2 stem over 3 channels; 1 (nothing launched) otherwise
 int conv_stem_launch(const raft_conv2d_params& p, int k_pad, hipStream_t s);
 // tile-statistics slots per image of a conv on the halo / stem kernel (raft_conv2d_stats_slots), 0 if none

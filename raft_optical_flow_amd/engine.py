@@ -28,6 +28,7 @@ inp slot stay 16-byte aligned).
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import torch
@@ -130,16 +131,6 @@ class PackedUpdate:
             bctx = torch.cat([cz.bias, cr.bias, cq.bias], 0)
             ctx = pack_conv(wctx, bctx, 1, cz.padding, device=device)
             self.gru.append((zr, q, ctx))
-        # the first half-step's z|r conv split by input columns (gru_hside): the h columns (h is
-        # known one iteration ahead, so this part can run beside the flow head and the motion
-        # encoder) and the motion | flow columns (after the motion encoder)
-        self.zr1_h = self.zr1_x = None
-        if not small:
-            cz, cr, _ = steps[0]
-            wzr = torch.cat([cz.weight, cr.weight], 0).detach()
-            self.zr1_h = pack_conv(wzr[:, hcols], None, 1, cz.padding, device=device)
-            self.zr1_x = pack_conv(wzr[:, mcols], None, 1, cz.padding, seg_real=[mc + 2], seg_decl=[mc + 2 + pad],
-                                   device=device)
         self.fh1 = pack_conv(fh.conv1.weight, fh.conv1.bias, 1, 1, device=device)
         self.fh2 = pack_conv(fh.conv2.weight, fh.conv2.bias, 1, 1, device=device)
         if not small:
@@ -204,7 +195,7 @@ def _conv_in(L, A: Arena, pc: PackedConv, src: Rows, n_img, h, w, out: Rows, src
     applies in its loaders (the statistics; the caller checked _norm_in_loader).  (The raw conv
     outputs of an InstanceNorm encoder feed the fp32 statistics and normalisation only: no range
     guard, raft_hip.h.)"""
-    import ctypes
+
     p = conv_params(pc, src, n_img, h, w, out)
     if src_norm is not None:
         p.in_norm, p.in_norm_relu = src_norm.data_ptr(), 1
@@ -224,7 +215,7 @@ def _conv_in(L, A: Arena, pc: PackedConv, src: Rows, n_img, h, w, out: Rows, src
 def _norm_in_loader(pc: PackedConv, src: Rows, n_img, h, w) -> bool:
     """Whether the conv of pc over src can apply src's relu(InstanceNorm) in its loaders
     (raft_conv2d_in_norm_ok; RAFT_IN_NORM=0: never), which saves the normalised copy's pass."""
-    import ctypes
+
     if os.environ.get("RAFT_IN_NORM", "1") == "0":
         return False
     p = conv_params(pc, src, n_img, h, w, src)   # (only checked, never launched)
@@ -363,7 +354,10 @@ class UpdateBuffers:
         self.rh = A.rows(P, hd)
         self.ctx = [A.rows(P, 3 * hd) for _ in pu.gru]   # z | r | q context terms per half-step
         self.coords = A.rows(P, 2)
-        self.pre_zr1 = A.rows(P, 2 * hd) if gru_hside(pu) else None  # h part + context of zr1
+        # raft_conv2d_chain's completion counters (one launch at a time on the main stream) and
+        # its timeout flag where no range flag takes it
+        self.chain_sync = None  # (allocated by _Stages.launch: its size depends on the image)
+        self.chain_err = torch.zeros(1, dtype=torch.int32, device=A.device)
 
     # channel slots of HX
     def h(self, pu):
@@ -385,20 +379,6 @@ class UpdateBuffers:
     def x_dyn(self, pu):
         """motion | flow (| pad): the second segment of the q GEMM's input."""
         return Rows(self.hx, pu.hdim, pu.inp_off - pu.hdim)
-
-
-def gru_hside(pu: PackedUpdate) -> bool:
-    """Whether the first GRU half-step's z|r conv runs as an h-part on the side stream (issued
-    right after the previous iteration's h is final, beside the flow head, the next lookup and
-    the motion encoder) plus a motion|flow part on the main stream (RAFT_GRU_HSIDE=1)."""
-    return pu.zr1_h is not None and os.environ.get("RAFT_GRU_HSIDE", "0") == "1"
-
-
-def plan_zr1_hpart(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, side: bool):
-    """W_zr1[h columns] * h + the z|r context terms -> ub.pre_zr1 (the addend of zr1's x part)."""
-    hd = pu.hdim
-    _conv(L, pu.zr1_h, ub.h(pu), B, h, w, Rows(ub.pre_zr1), epilogue=_lib.EPI_LINEAR,
-          add0=Rows(ub.ctx[0]).sub(0, 2 * hd), range_flag=None, side=side)
 
 
 def plan_gru_context(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w):
@@ -459,8 +439,44 @@ def frag_weight(pc) -> torch.Tensor:
     return out
 
 
+CHAIN_MAX_STAGES = 8
+
+
+def chain_enabled(pu: PackedUpdate) -> bool:
+    """Whether RAFT-full's update convs from convc2|convf2 to the flow head's conv1 run as one
+    raft_conv2d_chain launch (RAFT_CHAIN=0: one launch per conv)."""
+    return not pu.small and os.environ.get("RAFT_CHAIN", "1") != "0" and os.environ.get("RAFT_CONV_PAIR", "1") != "0"
+
+
+class _Stages:
+    """Collects conv stages for one raft_conv2d_chain launch (plan_update)."""
+
+    def __init__(self):
+        self.stages = []
+
+    def add(self, p0, p1=None):
+        self.stages.append((p0, p1))
+
+    def launch(self, ub: UpdateBuffers) -> Launch:
+        n = len(self.stages)
+        assert 1 <= n <= CHAIN_MAX_STAGES
+        arr = (ctypes.POINTER(_lib.ConvParams) * (2 * n))()
+        for i, (p0, p1) in enumerate(self.stages):
+            arr[2 * i] = ctypes.pointer(p0)
+            if p1 is not None:
+                arr[2 * i + 1] = ctypes.pointer(p1)
+        flag = _GUARD["flag"]
+        err = flag.data_ptr() if flag is not None else ub.chain_err.data_ptr()
+        if ub.chain_sync is None:
+            p = self.stages[0][0]
+            nint = int(_lib.load().raft_conv2d_chain_sync_ints(CHAIN_MAX_STAGES, p.batch, p.out_h, p.out_w))
+            ub.chain_sync = torch.zeros(nint, dtype=torch.int32, device=ub.chain_err.device)
+        keep = (arr, [p for st in self.stages for p in st if p is not None])
+        return Launch("raft_conv2d_chain", arr, n, ub.chain_sync.data_ptr(), err, keep=keep)
+
+
 def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool, convf1_done: bool = False,
-                convc1_done: bool = False, last: bool = True, hside_ok: bool = False):
+                convc1_done: bool = False, last: bool = True):
     """One BasicUpdateBlock / SmallUpdateBlock step (core/update.py:297-325 / :250-263)
     followed by coords1 += delta_flow (core/raft.py:232).  Assumes ub.corr and the
     flow slot of HX were filled by the lookup and plan_gru_context ran for this pair
@@ -475,6 +491,15 @@ def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool
     # RAFT-small (different conv shapes per branch): side stream unless RAFT_FLOW_SIDE=0.
     pair = not pu.small and os.environ.get("RAFT_CONV_PAIR", "1") != "0"
     side = not pair and os.environ.get("RAFT_FLOW_SIDE", "1") != "0"
+    # RAFT-full: convc2|convf2 .. the flow head's conv1 as one chained launch (raft_conv2d_chain)
+    chain = _Stages() if chain_enabled(pu) else None
+
+    def conv(pc, src, out, **kw):
+        kw.setdefault("range_flag", _GUARD["flag"])
+        if chain is not None:
+            chain.add(conv_params(pc, src, B, h, w, out, **kw))
+        else:
+            L.append(conv_launch(conv_params(pc, src, B, h, w, out, **kw)))
     if side:
         L.append(K.FORK)
     if pu.small:
@@ -490,7 +515,10 @@ def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool
                          range_flag=_GUARD["flag"])
         f2 = conv_params(pu.convf2, Rows(ub.flo1), B, h, w, cf.sub(192, 64), epilogue=_lib.EPI_RELU,
                          range_flag=_GUARD["flag"])
-        L.append(K.conv_pair_launch(c2, f2))
+        if chain is not None:
+            chain.add(c2, f2)
+        else:
+            L.append(K.conv_pair_launch(c2, f2))
     else:
         _conv(L, pu.convf1, flow, B, h, w, Rows(ub.flo1), epilogue=_lib.EPI_RELU, side=side)
         _conv(L, pu.convf2, Rows(ub.flo1), B, h, w, cf.sub(192, 64), epilogue=_lib.EPI_RELU, side=side)
@@ -498,26 +526,16 @@ def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool
         _conv(L, pu.convc2, Rows(ub.cor1), B, h, w, cf.sub(0, 192), epilogue=_lib.EPI_RELU)
     if side:
         L.append(K.JOIN)
-    _conv(L, pu.conv, cf, B, h, w, ub.motion(pu), epilogue=_lib.EPI_RELU)
+    conv(pu.conv, cf, ub.motion(pu), epilogue=_lib.EPI_RELU)
     hd = pu.hdim
     hrows = ub.h(pu)
-    hside = hside_ok and gru_hside(pu)  # (RaftPlan only: it issues the h part before the loop)
     for i, ((zr, q, _), ctx) in enumerate(zip(pu.gru, ub.ctx)):
         c = Rows(ctx)
         # (z, r*h and the new h are sigmoid / tanh blends of |h| <= 1: no range guard)
-        if i == 0 and hside:
-            L.append(K.JOIN)  # the h part (side stream) has landed in pre_zr1
-            _conv(L, pu.zr1_x, ub.x_dyn(pu), B, h, w, Rows(ub.z), epilogue=_lib.EPI_GRU_ZR, split=hd, aux0=hrows,
-                  out1=Rows(ub.rh), add0=Rows(ub.pre_zr1), range_flag=None)
-            continue
-        _conv(L, zr, ub.gru_in(pu), B, h, w, Rows(ub.z), epilogue=_lib.EPI_GRU_ZR, split=hd, aux0=hrows,
-              out1=Rows(ub.rh), add0=c.sub(0, 2 * hd), range_flag=None)
-        _conv(L, q, Rows(ub.rh), B, h, w, hrows, src1=ub.x_dyn(pu), epilogue=_lib.EPI_GRU_Q, aux0=hrows,
-              aux1=Rows(ub.z), add0=c.sub(2 * hd, hd), range_flag=None)
-    if hside and not last:
-        # the next iteration's zr1 h part: h is final here
-        L.append(K.FORK)
-        plan_zr1_hpart(L, pu, ub, B, h, w, side=True)
+        conv(zr, ub.gru_in(pu), Rows(ub.z), epilogue=_lib.EPI_GRU_ZR, split=hd, aux0=hrows,
+             out1=Rows(ub.rh), add0=c.sub(0, 2 * hd), range_flag=None)
+        conv(q, Rows(ub.rh), hrows, src1=ub.x_dyn(pu), epilogue=_lib.EPI_GRU_Q, aux0=hrows,
+             aux1=Rows(ub.z), add0=c.sub(2 * hd, hd), range_flag=None)
     coords = Rows(ub.coords)
     if pu.small:
         _conv(L, pu.fh1, hrows, B, h, w, Rows(ub.fh), epilogue=_lib.EPI_RELU, range_flag=None)  # feeds fp32 fh2
@@ -525,9 +543,11 @@ def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool
     else:
         fh = Rows(ub.fh)
         if with_mask:
-            _conv(L, pu.fh1_mask, hrows, B, h, w, fh, epilogue=_lib.EPI_RELU)
+            conv(pu.fh1_mask, hrows, fh, epilogue=_lib.EPI_RELU)
         else:  # (feeds only the fp32 flow-head conv2: no range guard)
-            _conv(L, pu.fh1, hrows, B, h, w, fh.sub(0, 256), epilogue=_lib.EPI_RELU, range_flag=None)
+            conv(pu.fh1, hrows, fh.sub(0, 256), epilogue=_lib.EPI_RELU, range_flag=None)
+        if chain is not None:
+            L.append(chain.launch(ub))
         _conv(L, pu.fh2, fh.sub(0, 256), B, h, w, coords, epilogue=_lib.EPI_ADD_TO_OUT)
         if with_mask:
             # the mask feeds only the fp32 softmax of the upsampling: no range guard
@@ -629,9 +649,6 @@ class RaftPlan:
             L.append(K.JOIN)
         L.append(Launch("raft_init_coords", ub.coords.data_ptr(),
                         self.flow_init.data_ptr() if self.flow_init is not None else None, B, h, w))
-        if gru_hside(pu):
-            L.append(K.FORK)
-            plan_zr1_hpart(L, pu, ub, B, h, w, side=True)
         self.loop_start = len(L)
         self.flow_up = [torch.empty(B, 2, H, W, device=device) for _ in range(1 if test_mode else iters)]
         flow_slot = ub.flow_off(pu)
@@ -679,7 +696,7 @@ class RaftPlan:
                                     ub.flo1.shape[1], gflag, keep=f1w))
             want_up = last or not test_mode
             plan_update(L, pu, ub, B, h, w, with_mask=want_up and not pu.small, convf1_done=fuse_f1,
-                        convc1_done=fuse_c1, last=last, hside_ok=True)
+                        convc1_done=fuse_c1, last=last)
             if want_up:
                 dst = self.flow_up[-1 if test_mode else it]
                 if pu.small:

@@ -858,24 +858,6 @@ def test_raft_e2e_golden(name, small, alt, prec):
     assert maxabs(up, g["flow_up"]) < 1e-3
 
 
-def test_raft_gru_hside_golden_and_graph(monkeypatch):
-    """RAFT_GRU_HSIDE=1 (zr1's h part on the side stream, one iteration ahead): the reference
-    golden within 1e-3, and eager == graph replay bit for bit."""
-    monkeypatch.setenv("RAFT_GRU_HSIDE", "1")
-    g = load_golden("raft_full_smooth_b2_128x192_i12.npz")
-    m, _ = make_model(False, int(g["seed"]), precision="f16x3")
-    i1, i2 = t(g["image1"]), t(g["image2"])
-    with torch.no_grad():
-        low0, up0 = m(i1, i2, iters=12, test_mode=True)
-        pl = m.plan(2, 128, 192, 12, True)
-        assert pl.kernel_names().count("raft_conv2d") > 0 and pl.pk.update.zr1_h is not None
-        low1, up1 = m(i1, i2, iters=12, test_mode=True)
-        assert pl.graph is not None
-    assert maxabs(low0, g["flow_low"]) < 1e-3
-    assert maxabs(up0, g["flow_up"]) < 1e-3
-    assert maxabs(low1, low0) == 0.0 and maxabs(up1, up0) == 0.0
-
-
 def test_raft_train_mode_output_list_and_graph_replay():
     g = load_golden("raft_full_smooth_b2_128x192_i12.npz")
     m, _ = make_model(False, 0)
