@@ -919,6 +919,7 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
     RAFT_REQUIRE(p.stats_ld >= p.n && ((uintptr_t)p.stats_part & 15) == 0,
                  "raft_conv2d: stats_ld >= n and a 16-B aligned stats_part");
   }
+  if (p.mode == RAFT_CONV_VEC && conv_resident_launch(o, s) == 0) return check_launch("raft_conv2d(resident)");
   if (p.mode == RAFT_CONV_VEC && conv_halo_launch(o, s) == 0) return check_launch("raft_conv2d(halo)");
   if (p.mode == RAFT_CONV_GATHER && conv_stem_launch(p, o.k_pad, s) == 0) return check_launch("raft_conv2d(stem)");
   a.gn = n_pad / BN;

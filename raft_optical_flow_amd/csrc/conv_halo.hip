@@ -128,37 +128,6 @@ __device__ __forceinline__ unsigned long long hstamp_now() {
 }
 #endif
 
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, void* lds, unsigned voff, unsigned soff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
-}
-
-// s_waitcnt vmcnt(n) only (expcnt / lgkmcnt at their maxima)
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  __builtin_amdgcn_s_waitcnt((N & 15) | 0x70 | 0xF00 | ((N >> 4) << 14));
-}
-// n > 15 waits for 15 (stricter than needed, never looser)
-__device__ __forceinline__ void wait_vm_n(int n) {
-  switch (n) {
-    case 0: wait_vm<0>(); break;
-    case 1: wait_vm<1>(); break;
-    case 2: wait_vm<2>(); break;
-    case 3: wait_vm<3>(); break;
-    case 4: wait_vm<4>(); break;
-    case 5: wait_vm<5>(); break;
-    case 6: wait_vm<6>(); break;
-    case 7: wait_vm<7>(); break;
-    case 8: wait_vm<8>(); break;
-    case 9: wait_vm<9>(); break;
-    case 10: wait_vm<10>(); break;
-    case 11: wait_vm<11>(); break;
-    case 12: wait_vm<12>(); break;
-    case 13: wait_vm<13>(); break;
-    case 14: wait_vm<14>(); break;
-    default: wait_vm<15>(); break;
-  }
-}
-
 // Completion counters of a chained launch, one per 128-B line: a line takes only the adds of one
 // spatial tile's producers (atomics on one line serialise at ~90 per us) and its pollers
 constexpr int CHAIN_PAD = 32;
