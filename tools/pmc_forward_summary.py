@@ -59,7 +59,7 @@ lk_w = [c["WRITE_SIZE"] for k, c in fwd_w if k.startswith("corr_lookup")]
 hit = [c for k, c in passes["p4"][0] if k.startswith("corr_lookup")]
 P = B * 55 * 128
 alg_read, alg_write = P * (4 * 100 * 4 + 8), P * 4 * 81 * 4
-res = {
+res = {} if not lk_f else {
     "kernel": "corr_lookup_kernel<4, 4, false, SCAL> (B=1: the scalar-interval window form)", "source_sha": sha("corr_pyramid.hip"), "shape_bhw": [B, 440, 1024],
     "workload": f"bench.py config-2 forward, B={B}, 436x1024 padded to 440x1024, iters=32, f16x3; "
                 f"the {len(lk_f)} lookups of the last of two eager forwards (tools/pmc_forward.py)",
@@ -72,10 +72,13 @@ res = {
     "algorithmic_read_bytes": alg_read, "algorithmic_write_bytes": alg_write,
     "l2_hit_rate": round(sum(c["TCC_HIT_sum"] for c in hit) / sum(c["TCC_HIT_sum"] + c["TCC_MISS_sum"] for c in hit), 4),
 }
-res["hbm_bytes_per_launch"] = res["hbm_read_bytes_per_launch"] + res["hbm_write_bytes_per_launch"]
-res["traffic_over_algorithmic"] = round(res["hbm_bytes_per_launch"] / (alg_read + alg_write), 3)
+if lk_f:
+    res["hbm_bytes_per_launch"] = res["hbm_read_bytes_per_launch"] + res["hbm_write_bytes_per_launch"]
+    res["traffic_over_algorithmic"] = round(res["hbm_bytes_per_launch"] / (alg_read + alg_write), 3)
 sfx = "" if B == 1 else f"_b{B}"
-json.dump(res, open(os.path.join(ROOT, "profiles", f"r02_lookup_pmc{sfx}.json"), "w"), indent=1)
+# (the standalone lookup kernel only runs in the forward without the fused launch: RAFT_FUSE_CONVC1=0)
+if lk_f:
+    json.dump(res, open(os.path.join(ROOT, "profiles", f"r03_lookup_pmc{sfx}.json"), "w"), indent=1)
 print(json.dumps(res, indent=1))
 
 halo = {"source_sha": sha("conv_halo.hip"),
@@ -90,5 +93,24 @@ for k, v in per.items():
     halo[k] = {"dispatches": len(v), "mfma_busy": round(statistics.mean(x[0] for x in v), 4),
                "mfma_busy_cycles_avg": round(statistics.mean(x[1] for x in v)),
                "gui_active_cycles_avg": round(statistics.mean(x[2] for x in v))}
-json.dump(halo, open(os.path.join(ROOT, "profiles", f"r02_halo_pmc{sfx}.json"), "w"), indent=1)
+json.dump(halo, open(os.path.join(ROOT, "profiles", f"r03_halo_pmc{sfx}.json"), "w"), indent=1)
 print(json.dumps(halo, indent=1))
+
+# the forward's fused lookup launch (raft_corr_lookup_conv): window reads + coords + flow in,
+# convc1 (256) and convf1 (128) output rows out (bench.py fused_lookup_bytes_per_pixel)
+lc_f = [c["FETCH_SIZE"] for k, c in fwd_f if k.startswith("lookup_conv")]
+lc_w = [c["WRITE_SIZE"] for k, c in fwd_w if k.startswith("lookup_conv")]
+if lc_f:
+    lhit = [c for k, c in passes["p4"][0] if k.startswith("lookup_conv")]
+    a_r, a_w = P * (4 * 100 * 4 + 8), P * (4 * (256 + 128) + 8)
+    lc = {"kernel": "lookup_conv_kernel (raft_corr_lookup_conv: lookup + convc1 + convf1)", "source_sha": sha("lookup_conv.hip"),
+          "shape_bhw": [B, 440, 1024],
+          "workload": f"bench.py config-2 forward, B={B}, f16x3; the {len(lc_f)} fused lookups of the last forward",
+          "hbm_read_bytes_per_launch": round(statistics.mean(lc_f) * 1024 * read_scale),
+          "hbm_write_bytes_per_launch": round(statistics.mean(lc_w) * 1024 * write_scale),
+          "algorithmic_read_bytes": a_r, "algorithmic_write_bytes": a_w,
+          "l2_hit_rate": round(sum(c["TCC_HIT_sum"] for c in lhit) / max(1.0, sum(c["TCC_HIT_sum"] + c["TCC_MISS_sum"] for c in lhit)), 4)}
+    lc["hbm_bytes_per_launch"] = lc["hbm_read_bytes_per_launch"] + lc["hbm_write_bytes_per_launch"]
+    lc["traffic_over_algorithmic"] = round(lc["hbm_bytes_per_launch"] / (a_r + a_w), 3)
+    json.dump(lc, open(os.path.join(ROOT, "profiles", f"r03_lookup_conv_pmc{sfx}.json"), "w"), indent=1)
+    print(json.dumps(lc, indent=1))
