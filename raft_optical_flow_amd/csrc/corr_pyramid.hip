@@ -34,6 +34,7 @@ struct CorrBuildArgs {
   Level l0, l1;
   int has_l1;
   int nbx;  // 8x8 blocks along w2
+  int nt;   // corr_build2: non-temporal level-0 / level-1 stores (a volume far past the Infinity Cache)
 };
 
 // X3: fp32-accurate split-f16 MFMA (RAFT_PREC_F16X3): both fmaps are split at
@@ -307,8 +308,12 @@ __global__ __launch_bounds__(512, 2) void corr_build2_kernel(CorrBuildArgs a) {
     const int ty = 2 * by + ti, tx = 4 * bx + tj;
     if (p1 < a.P && ty < a.l0.th && tx < a.l0.tw) {
       const float* t = T + row * CB2_TLD + (ti * 4 + (e >> 2)) * 16 + tj * 4;
-      *reinterpret_cast<f32x4*>(a.pyr + a.l0.off + ((long)b * a.P + p1) * a.l0.mapsz + ((long)ty * a.l0.tw + tx) * 16 +
-                                e) = f32x4{t[0], t[1], t[2], t[3]};
+      f32x4* dst = reinterpret_cast<f32x4*>(a.pyr + a.l0.off + ((long)b * a.P + p1) * a.l0.mapsz +
+                                            ((long)ty * a.l0.tw + tx) * 16 + e);
+      if (a.nt)
+        __builtin_nontemporal_store(f32x4{t[0], t[1], t[2], t[3]}, dst);
+      else
+        *dst = f32x4{t[0], t[1], t[2], t[3]};
     }
   }
   if (a.has_l1 && by < a.l1.th) {
@@ -332,8 +337,12 @@ __global__ __launch_bounds__(512, 2) void corr_build2_kernel(CorrBuildArgs a) {
         }
         v4[c] = v;
       }
-      *reinterpret_cast<f32x4*>(a.pyr + a.l1.off + ((long)b * a.P + p1) * a.l1.mapsz + ((long)by * a.l1.tw + tx1) * 16 +
-                                e) = v4;
+      f32x4* dst = reinterpret_cast<f32x4*>(a.pyr + a.l1.off + ((long)b * a.P + p1) * a.l1.mapsz +
+                                            ((long)by * a.l1.tw + tx1) * 16 + e);
+      if (a.nt)
+        __builtin_nontemporal_store(v4, dst);
+      else
+        *dst = v4;
     }
   }
 }
@@ -920,6 +929,13 @@ extern "C" int raft_corr_build_prec(const float* fmap1, const float* fmap2, int 
   a.has_l1 = L > 1;
   a.l1 = lv[L > 1 ? 1 : 0];
   a.nbx = cdiv(W, 8);
+  {
+    // non-temporal pyramid stores when level 0 alone is far past the 256 MiB Infinity Cache (the
+    // lookups then read it from HBM either way); RAFT_CORR_NT=0 / 1 overrides
+    const char* e = getenv("RAFT_CORR_NT");
+    const double l0_bytes = 4.0 * B * (double)P * lv[0].mapsz;
+    a.nt = e && (e[0] == '0' || e[0] == '1') ? e[0] == '1' : l0_bytes > 512.0 * 1024 * 1024;
+  }
   hipStream_t s = as_stream(stream);
   static const bool big = [] {
     const char* e = getenv("RAFT_CORR_BUILD_BIG");
