@@ -182,7 +182,10 @@ __device__ __forceinline__ void chain_wait(const ChainCtl& c, int b, int ty, int
 // (conv_chain_kernel): the loaders wait for the producing stage's neighbourhood before the first
 // patch load, the epilogue stores write through to memory (sc1) and every compute wave bumps the
 // tile's completion counter once its stores have landed.
-template <int KH, int KW, int BNT, int PREC, bool ENC = false, bool CH = false>
+// KS = 2: two MFMA waves per SIMD share each 32-pixel block, taking alternate K-steps (a
+// 768-thread work-group); their partial sums meet in LDS before the epilogue, so one wave's
+// fragment reads and waits run under the other's MFMAs at the same LDS bytes per MFMA.
+template <int KH, int KW, int BNT, int PREC, bool ENC = false, bool CH = false, int KS = 1>
 __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q, char* smem, const ChainCtl& ctl) {
   constexpr bool X3 = PREC == RAFT_PREC_F16X3;
   constexpr bool BF = PREC == RAFT_PREC_BF16;
@@ -226,8 +229,10 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
 #endif
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool loader = w >= 4;  // waves 4-7 move the operands, waves 0-3 compute
+  const bool loader = w >= 4 * KS;  // the last 4 waves move the operands, the others compute
   const int lw = w & 3;
+  const int wc = w & 3, kp = w >> 2;  // compute waves: block index and K part (KS = 2)
+  static_assert(KS == 1 || (KS == 2 && LSPLIT && !ENC && !CH && MF == 1 && U % 2 == 0), "K-split pairs");
 
   // tile (N fastest: an output tile's N-tiles share its input patch in L2)
   const HaloArgs& a = args[prob];
@@ -460,6 +465,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
         __builtin_amdgcn_s_barrier();
       }
       wait_vm<0>();
+      if constexpr (KS == 2) __builtin_amdgcn_s_barrier();  // the K parts' partial sums are in LDS
       return;
     }
     // Super-step s: issue load set s+D, wait until load set s+2 has landed
@@ -496,7 +502,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
 
   // ---- compute waves: fragments --------------------------------------------
   const int m = lane & 31, h = lane >> 5;
-  const int wm = w % WVM, cb = (w / WVM) * WCOL;  // the wave's pixel blocks and first column
+  const int wm = wc % WVM, cb = (wc / WVM) * WCOL;  // the wave's pixel blocks and first column
   int ppbase[MF];  // patch pixel of this lane's row in block f (tap 0, 0)
 #pragma unroll
   for (int f = 0; f < MF; ++f) ppbase[f] = (2 * (wm * MF + f) + (m >> 4)) * PW + (m & 15);
@@ -625,8 +631,10 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
   // all in load sets s and s+1), then one barrier.  K-steps past nk (up to
   // U*ns) run on zero weights and zero patches: they add exact zeros, and the
   // loop body has no branches.
+  if (kp == 0) {
 #pragma unroll
-  for (int u = 0; u < D; ++u) issue_weights(u);
+    for (int u = 0; u < D; ++u) issue_weights(u);
+  }
   if constexpr (CH) __builtin_amdgcn_s_barrier();  // the loaders' wait for the producing stage
   wait_vm<NWP * (D - 2)>();      // the weights of sets 0 and 1 (sets 2 .. D-1: before the first loop barrier)
   __builtin_amdgcn_s_barrier();  // load sets 0 and 1 have landed
@@ -634,7 +642,9 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
   __builtin_amdgcn_s_setprio(HALO_PRIO);
 #endif
   Frag F[2];
-  if constexpr (LSPLIT) {
+  if constexpr (KS == 2) {
+    // (no look-ahead: the partner wave's MFMAs cover this wave's reads)
+  } else if constexpr (LSPLIT) {
     read_b(F[0]);
     read_a_split(F[0]);
   } else {
@@ -654,7 +664,16 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
       mfma_step(F[e & 1]);
       asm volatile("" ::"v"(F[0].ah[0][0]), "v"(F[1].ah[0][0]));
 #else
-      if constexpr (LSPLIT) {
+      if constexpr (KS == 2) {
+        if ((e & 1) == kp) {
+          read_b(F[0]);
+          read_a_split(F[0]);
+          mfma_step(F[0]);
+        } else {  // the partner's K-step: move the cursors past it
+          b_bs = b_bs + 1 == SB ? 0 : b_bs + 1;
+          advance_a();
+        }
+      } else if constexpr (LSPLIT) {
         read_b(F[(e + 1) & 1]);
         read_a_split(F[(e + 1) & 1]);
         mfma_step(F[e & 1]);
@@ -693,6 +712,24 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
       for (int sb = 0; sb < NSUB; ++sb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[f][sb][r] += accx[f][sb][r] * (1.0f / SPLIT_SCALE);
+  }
+  if constexpr (KS == 2) {
+    // K part 1 hands its partial sums to K part 0 through LDS (the rings are free: every read of
+    // the loop is done and no load is in flight after its last barrier), then leaves
+    float* red = reinterpret_cast<float*>(smem) + (wc * NSUB * 16) * 64 + lane;
+    if (kp == 1) {
+#pragma unroll
+      for (int sb = 0; sb < NSUB; ++sb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) red[(sb * 16 + r) * 64] = acc[0][sb][r];
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    if (kp == 1) return;
+#pragma unroll
+    for (int sb = 0; sb < NSUB; ++sb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[0][sb][r] += red[(sb * 16 + r) * 64];
   }
 
   // ---- epilogue: register r of block f holds row m = (r&3) + 8(r>>2) + 4h of its 32 pixels
@@ -752,12 +789,37 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
   halo_body<KH, KW, BNT, PREC, ENC, false>(hl.a, prob, q, smem, ChainCtl{});
 }
 
+// The K-split form (KS = 2, 768 threads): update-block convs (no encoder features), RAFT_HALO_KS=2
+template <int KH, int KW, int BNT, int PREC>
+__global__ __launch_bounds__(768) void conv_halo_ks2_kernel(HaloLaunch hl) {
+  using C = HaloCfg<KH, KW, BNT, PREC == RAFT_PREC_F16X3 ? 128 : 64>;
+  __shared__ __attribute__((aligned(1024))) char smem[C::LDS_B + C::LDS_A];
+  int q = xcd_tile(blockIdx.x, gridDim.x);
+  const int prob = q >= hl.tiles0 ? 1 : 0;
+  q -= prob * hl.tiles0;
+  halo_body<KH, KW, BNT, PREC, false, false, 2>(hl.a, prob, q, smem, ChainCtl{});
+}
+
+bool halo_ks2_enabled() {  // (read per call)
+  const char* e = getenv("RAFT_HALO_KS");
+  return e && e[0] == '2';
+}
+
 template <int KH, int KW, int PREC>
 void launch_halo_p(const HaloLaunch& l, int bn, dim3 grid, hipStream_t s) {
   const raft_conv2d_params& p = l.a[0].p;
   if constexpr (PREC != RAFT_PREC_F16X3) {
     if (bn == 128) {  // (conv_halo_launch picks it only without stats_part / in_norm)
       hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 128, PREC>), grid, dim3(512), 0, s, l);
+      return;
+    }
+  }
+  if constexpr (PREC == RAFT_PREC_F16X3 && !(KH == 1 && KW == 1)) {
+    if (!p.stats_part && !p.in_norm && halo_ks2_enabled() && (bn == 64 || bn == 32)) {
+      if (bn == 64)
+        hipLaunchKernelGGL((conv_halo_ks2_kernel<KH, KW, 64, PREC>), grid, dim3(768), 0, s, l);
+      else
+        hipLaunchKernelGGL((conv_halo_ks2_kernel<KH, KW, 32, PREC>), grid, dim3(768), 0, s, l);
       return;
     }
   }
