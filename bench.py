@@ -17,10 +17,10 @@ The line also carries
                 the 324-channel correlation rows never leave the CU), HBM-bound:
                 algorithmic bytes per pair-iteration = P * (L*(2r+2)^2*4 window reads +
                 8 coords + 4*(256 + 128) convc1 / convf1 outputs + 8 flow) over its
-                average duration IN the forward (HIP event pairs on the launch stream
-                around each of the 32 launches of an eagerly enqueued forward; the
-                rocprofv3 per-dispatch mean of the same kernel is committed under
-                profiles/); without the fused launch (fp32 mode) the lookup-only kernel
+                per-dispatch duration (the forward's own launch, back to back in one
+                hipGraph; the rocprofv3 per-dispatch mean of the same kernel in the
+                forward is committed under profiles/); without the fused launch (fp32
+                mode) the lookup-only kernel (HIP event pairs in an eager forward)
                 with SURVEY 8(d)'s P*2904 B; `traffic` = HBM bytes per launch from a
                 committed in-forward PMC summary taken on the current kernel source;
                 with --alternate-corr (config 3) the on-the-fly lookup against its peak;
@@ -392,6 +392,26 @@ def main():
     t_it = time_kernel_events(lambda: [l(K.stream_handle()) for l in it_all], 20)
     iteration = {"launches": len(it_all), "iteration_us": round(t_it * 1e6, 1),
                  "timing": "HIP events around a hipGraph of 20 replays of one iteration's launches"}
+    if roof is not None and roof["kernel"].startswith("lookup_conv"):
+        # the fused lookup's own duration in the iteration: the replayed iteration with and without
+        # it (graph-replayed kernels run back to back, as rocprofv3 times a dispatch; an event pair
+        # around one launch adds its own ~3-4 us)
+        rest = [l for l in it_all if getattr(l, "name", "") != "raft_corr_lookup_conv"]
+        lk = [l for l in it_all if getattr(l, "name", "") == "raft_corr_lookup_conv"][0]
+        t_rest = time_kernel_events(lambda: [l(K.stream_handle()) for l in rest], 20)
+        # the forward's own launch (its pyramid, final coords and outputs) 32 times back to back in
+        # one graph: per-dispatch time as rocprofv3 reports it (event pairs around single launches
+        # add their own ~3-4 us; so does a graph boundary)
+        us = time_kernel_events(lambda: [lk(K.stream_handle()) for _ in range(32)], 4) / 32 * 1e6
+        roof["event_pair_us"] = roof["launch_us"]
+        roof["iteration_delta_us"] = round((t_it - t_rest) * 1e6, 2)
+        roof["launch_us"] = round(us, 2)
+        roof["achieved"] = round(roof["algorithmic_bytes_per_launch"] / us / 1e3, 1)
+        roof["frac"] = round(roof["achieved"] / HBM_PEAK_GBS, 4)
+        roof["timing"] = ("HIP events around a hipGraph of 4 x 32 back-to-back replays of the forward's own fused lookup "
+                          "launch (its pyramid, the final coords); event_pair_us: HIP event pairs around each of the 32 "
+                          "launches of an eager forward; iteration_delta_us: one iteration's graph with minus without "
+                          "the launch")
     it_convs = [plan.launches[i] for i in range(lk_idx[per_it] + 1, lk_idx[2 * per_it])
                 if getattr(plan.launches[i], "name", "") in ("raft_conv2d", "raft_conv2d_pair", "raft_conv2d_chain")
                 and not plan.launches[i].side]
