@@ -350,9 +350,19 @@ __global__ __launch_bounds__(256) void instnorm_merge_kernel(const float* part, 
   __shared__ double red[3][256];
   const int c = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
   double n = 0.0, mean = 0.0, m2 = 0.0;
-  for (int k = t; k < slots; k += 256) {
-    const f32x4 v = *reinterpret_cast<const f32x4*>(part + (((long)b * slots + k) * ld + c) * 4);
-    chan_merge(n, mean, m2, (double)v[0], (double)v[1], (double)v[2]);
+  // 8 slots' loads in flight per thread, then their merges in slot order (the order, and so the
+  // result, of one load-merge per slot; one memory latency per 8 slots instead of per slot)
+  constexpr int PF = 8;
+  for (int k0 = t; k0 < slots; k0 += 256 * PF) {
+    f32x4 v[PF];
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int k = k0 + 256 * i;
+      v[i] = k < slots ? *reinterpret_cast<const f32x4*>(part + (((long)b * slots + k) * ld + c) * 4) : f32x4{};
+    }
+#pragma unroll
+    for (int i = 0; i < PF; ++i)
+      if (k0 + 256 * i < slots) chan_merge(n, mean, m2, (double)v[i][0], (double)v[i][1], (double)v[i][2]);
   }
   red[0][t] = n;
   red[1][t] = mean;
