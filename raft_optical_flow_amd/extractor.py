@@ -12,6 +12,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from . import _lib
 from . import kernels as K
 from .kernels import Rows
 
@@ -45,9 +46,17 @@ class _BlockBase(nn.Module):
         n, c, h, w = x.shape
         d = K.cached_pack(self, x.device, lambda: pack_block(self, self.norm_fn, self._small, x.device))
         pe = SimpleNamespace(norm=self.norm_fn, small=self._small)
-        L, A = [], Arena(x.device)
-        plan = _plan_bottleneck if self._small else _plan_residual
-        y, ho, wo = plan(L, A, pe, d, Rows(K.nchw_to_rows(x)), n, h, w)
+
+        def build():  # input rows, buffers and launches, cached per input shape (K.cached_plan)
+            L, A = [], Arena(x.device)
+            xr = Rows(A.rows(n * h * w, c))
+            plan = _plan_bottleneck if self._small else _plan_residual
+            y, ho, wo = plan(L, A, pe, d, xr, n, h, w)
+            return A, xr, L, y, ho, wo
+
+        _, xr, L, y, ho, wo = K.cached_plan(self, d, (n, c, h, w, str(x.device)), build)
+        xc = x.contiguous()
+        _lib.call("raft_nchw_to_nhwc", xc.data_ptr(), xr.ptr, xr.ld, n, c, h, w, K.stream_handle())
         K.run(L)
         return K.rows_to_nchw(y, n, ho, wo)
 

@@ -313,6 +313,18 @@ def cached_pack(mod, device, build):
     return hit[1]
 
 
+def cached_plan(mod, packed, key, build):
+    """A block-level forward's device buffers and pre-built launch list for one input shape, kept on
+    the module (the last shape only) and rebuilt when the packed weights object (cached_pack's,
+    compared by identity) or the key (shape, device) changes: repeated calls allocate nothing and
+    only copy their inputs in.  Calls on one module are stream-ordered (the buffers are shared)."""
+    hit = mod.__dict__.get("_hip_plan")
+    if hit is None or hit[0] is not packed or hit[1] != key:
+        hit = (packed, key, build())
+        mod.__dict__["_hip_plan"] = hit
+    return hit[2]
+
+
 def conv2d_rows(pc: PackedConv, src0: Rows, batch, in_h, in_w, out: Rows, **kw):
     conv_launch(conv_params(pc, src0, batch, in_h, in_w, out, **kw))(stream_handle())
 

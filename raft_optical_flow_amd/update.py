@@ -70,30 +70,36 @@ class _GRUHalf:
         self.q = K.pack_conv(cq.weight, cq.bias, 1, cq.padding, seg_real=[hd, xd], seg_decl=[hd, xp],
                              device=w.device)
 
-    def run(self, hx: torch.Tensor, hd, xp, z, rh, b, h, w):
+    def launches(self, hx: torch.Tensor, hd, xp, z, rh, b, h, w):
         hrows = Rows(hx, 0, hd)
-        K.conv2d_rows(self.zr, Rows(hx), b, h, w, Rows(z), epilogue=_lib.EPI_GRU_ZR, split=hd, aux0=hrows,
-                      out1=Rows(rh))
-        K.conv2d_rows(self.q, Rows(rh), b, h, w, hrows, src1=Rows(hx, hd, xp), epilogue=_lib.EPI_GRU_Q,
-                      aux0=hrows, aux1=Rows(z))
+        return [K.conv_launch(K.conv_params(self.zr, Rows(hx), b, h, w, Rows(z), epilogue=_lib.EPI_GRU_ZR, split=hd,
+                                            aux0=hrows, out1=Rows(rh))),
+                K.conv_launch(K.conv_params(self.q, Rows(rh), b, h, w, hrows, src1=Rows(hx, hd, xp),
+                                            epilogue=_lib.EPI_GRU_Q, aux0=hrows, aux1=Rows(z)))]
 
 
 def _gru_forward(mod, steps, h, x):
-    """Shared ConvGRU / SepConvGRU forward on NHWC rows [h | x | zero pad]."""
+    """Shared ConvGRU / SepConvGRU forward on NHWC rows [h | x | zero pad] (buffers and launches
+    cached per input shape: K.cached_plan)."""
     K.require_device(h, x)
     b, hd, hh, ww = h.shape
     xd = x.shape[1]
     xp = _pad4(xd)
     halves = K.cached_pack(mod, h.device, lambda: [_GRUHalf(*s, hd, xd) for s in steps])
-    hx = torch.zeros(b * hh * ww, hd + xp, device=h.device)
+
+    def build():
+        hx = torch.zeros(b * hh * ww, hd + xp, device=h.device)
+        z = torch.empty(b * hh * ww, hd, device=h.device)
+        rh = torch.empty_like(z)
+        # (z and rh stay referenced by the plan: the launches hold raw pointers only)
+        return hx, z, rh, [l for half in halves for l in half.launches(hx, hd, xp, z, rh, b, hh, ww)]
+
+    hx, _, _, L = K.cached_plan(mod, halves, (b, hd, xd, hh, ww, str(h.device)), build)
     s = K.stream_handle()
     for t, off in ((h, 0), (x, hd)):
         t = t.contiguous()
         _lib.call("raft_nchw_to_nhwc", t.data_ptr(), hx.data_ptr() + 4 * off, hx.shape[1], b, t.shape[1], hh, ww, s)
-    z = torch.empty(b * hh * ww, hd, device=h.device)
-    rh = torch.empty_like(z)
-    for half in halves:
-        half.run(hx, hd, xp, z, rh, b, hh, ww)
+    K.run(L)
     return K.rows_to_nchw(Rows(hx, 0, hd), b, hh, ww)
 
 
@@ -199,8 +205,15 @@ class _UpdateBase(nn.Module):
         pu = K.cached_pack(self, net.device, lambda: PackedUpdate(self, self._small, net.device))
         if corr.shape[1] != pu.cor_planes:
             raise ValueError(f"corr has {corr.shape[1]} channels, expected {pu.cor_planes}")
-        A = Arena(net.device)
-        ub = UpdateBuffers(A, pu, P, pu.cor_planes)
+        def build():  # buffers and launches, cached per input shape (K.cached_plan)
+            A = Arena(net.device)
+            ub = UpdateBuffers(A, pu, P, pu.cor_planes)
+            L = []
+            plan_gru_context(L, pu, ub, b, h, w)
+            plan_update(L, pu, ub, b, h, w, with_mask=not self._small)
+            return A, ub, L
+
+        _, ub, L = K.cached_plan(self, pu, (b, h, w, str(net.device)), build)
         s = K.stream_handle()
         lib = _lib.load()
         for t, rows in ((net, ub.h(pu)), (inp, ub.inp(pu)), (flow, K.Rows(ub.hx, ub.flow_off(pu), 2)),
@@ -208,9 +221,6 @@ class _UpdateBase(nn.Module):
             t = t.contiguous()
             _lib.check(lib.raft_nchw_to_nhwc(t.data_ptr(), rows.ptr, rows.ld, b, t.shape[1], h, w, s), "nchw_to_nhwc")
         ub.coords.zero_()  # coords1 += delta  ->  delta
-        L = []
-        plan_gru_context(L, pu, ub, b, h, w)
-        plan_update(L, pu, ub, b, h, w, with_mask=not self._small)
         K.run(L)
         net_out = K.rows_to_nchw(ub.h(pu), b, h, w)
         delta = K.rows_to_nchw(K.Rows(ub.coords), b, h, w)

@@ -156,3 +156,35 @@ def test_block_pack_cache_reused_until_weights_change():
         c = m(x)
     assert m.__dict__["_hip_pack"][1] is not pk
     np.testing.assert_allclose(c.cpu().numpy(), 2 * a.cpu().numpy(), rtol=1e-5, atol=1e-5)
+
+
+def test_block_plans_cached_per_shape():
+    """BasicUpdateBlock, SepConvGRU and ResidualBlock keep their buffers and launch lists per input
+    shape (kernels.cached_plan): a repeated call reuses them (same plan object, results of an
+    input identical whatever ran in between), a new shape or new weights rebuild them."""
+    from raft_optical_flow_amd.extractor import ResidualBlock
+    from raft_optical_flow_amd.update import BasicUpdateBlock, SepConvGRU
+    args = argparse.Namespace(corr_levels=4, corr_radius=4)
+    torch.manual_seed(5)
+    ub = BasicUpdateBlock(args, 128).to(DEV).eval()
+    gru = SepConvGRU(128, 256).to(DEV).eval()
+    blk = ResidualBlock(64, 64, "instance", 1).to(DEV).eval()
+    cases = [
+        (ub, lambda s: (rnd(1, 128, 6, 10, seed=s), rnd(1, 128, 6, 10, seed=s + 1), rnd(1, 324, 6, 10, seed=s + 2),
+                        rnd(1, 2, 6, 10, seed=s + 3))),
+        (gru, lambda s: (rnd(2, 128, 5, 7, seed=s), rnd(2, 256, 5, 7, seed=s + 1))),
+        (blk, lambda s: (rnd(2, 64, 9, 12, seed=s),)),
+    ]
+    with torch.no_grad():
+        for m, mk in cases:
+            a = m(*mk(1))
+            plan = m.__dict__["_hip_plan"][2]
+            m(*mk(7))
+            a2 = m(*mk(1))
+            assert m.__dict__["_hip_plan"][2] is plan
+            for x, y in zip(a if isinstance(a, tuple) else (a,), a2 if isinstance(a2, tuple) else (a2,)):
+                assert (x is None and y is None) or torch.equal(x, y)
+            # a new shape rebuilds the plan
+            big = tuple(t.repeat(1, 1, 2, 1) if t.dim() == 4 else t for t in mk(3))
+            m(*big)
+            assert m.__dict__["_hip_plan"][2] is not plan
