@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define RAFT_HIP_ABI_VERSION 12
+#define RAFT_HIP_ABI_VERSION 13
 
 /* Negative return codes (argument errors, raised before any launch). */
 #define RAFT_E_INVALID (-1)   /* bad size / null pointer / unsupported shape */
@@ -374,6 +374,18 @@ int raft_instnorm_stats(const float* x, int ld, int B, int HW, int C, float eps,
 /* out = act( norm(x) + resid ) where resid = 0 (resid NULL), raw resid rows, or
  * norm(resid) with its own stats (resid_stats != NULL); relu_mode: 0 none, 1 relu(norm(x)),
  * 2 relu(resid + relu(norm(x)))  (ResidualBlock tail). */
+/* nn.GroupNorm (core/extractor.py:23-25: ResidualBlock / BottleneckBlock with norm_fn='group', the
+ * blocks' default): per (image, group of C/G consecutive channels) mean and 1/sqrt(var + eps) over the
+ * group's channels x HW pixels (double, deterministic), written per (image, channel) as
+ * stats[b][c] = {mean, rstd} of c's group — the layout raft_instnorm_apply reads.  C % G == 0. */
+int raft_groupnorm_stats(const float* x, int ld, int B, int HW, int C, int G, float eps, float* stats,
+                         raft_stream_t stream);
+/* raft_instnorm_apply with a per-channel affine: v = (x - mean) * rstd * gamma[c] + beta[c]
+ * (gamma / beta NULL = 1 / 0); the residual likewise with resid_gamma / resid_beta. */
+int raft_norm_apply_affine(const float* x, int ld, const float* stats, const float* gamma, const float* beta,
+                           const float* resid, int resid_ld, const float* resid_stats, const float* resid_gamma,
+                           const float* resid_beta, int relu_mode, float* out, int out_ld, int B, int HW, int C,
+                           raft_stream_t stream);
 int raft_instnorm_apply(const float* x, int ld, const float* stats, const float* resid, int resid_ld,
                         const float* resid_stats, int relu_mode, float* out, int out_ld,
                         int B, int HW, int C, raft_stream_t stream);

@@ -29,7 +29,7 @@ PREC_F16 = 2     # single f16 product (mixed precision)
 PREC_BF16 = 3    # single bf16 product on v_mfma_f32_32x32x16_bf16 (bf16 mixed precision)
 PRECISIONS = {"fp32": PREC_FP32, "f16x3": PREC_F16X3, "f16": PREC_F16, "bf16": PREC_BF16}
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 RANGE_LIMIT = 32768.0  # RAFT_RANGE_LIMIT: |x| above it raises the f16x3 range guard
 
 EPI_LINEAR = 0
@@ -113,6 +113,8 @@ _PROTOS = {
     "raft_conv2d_split_weight_prec": (c_int, [P, P, c_int, c_int, c_int, P]),
     "raft_instnorm_workspace_floats": (c_size_t, [c_int, c_int, c_int]),
     "raft_instnorm_stats": (c_int, [P, c_int, c_int, c_int, c_int, c_float, P, P, P]),
+    "raft_groupnorm_stats": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_float, P, P]),
+    "raft_norm_apply_affine": (c_int, [P, c_int, P, P, P, P, c_int, P, P, P, c_int, P, c_int, c_int, c_int, c_int, P]),
     "raft_instnorm_apply": (c_int, [P, c_int, P, P, c_int, P, c_int, P, c_int, c_int, c_int, c_int, P]),
     "raft_prep_images": (c_int, [P, P, P, c_int, c_int, c_int, P]),
     "raft_init_coords": (c_int, [P, P, c_int, c_int, c_int, P]),

@@ -385,6 +385,80 @@ __global__ __launch_bounds__(256) void instnorm_merge_kernel(const float* part, 
   stats[2 * (b * C + c) + 1] = (float)(1.0 / sqrt(var + (double)eps));
 }
 
+// nn.GroupNorm statistics (core/extractor.py:23-25, the blocks' norm_fn='group'): one block per
+// (group, image); mean, then the variance around it, over the group's C/G channels x HW pixels in
+// double with a fixed-order tree (deterministic); written per (image, channel) as the {mean, rstd}
+// of the channel's group.
+__device__ double block_sum256(double v, double* red) {
+  const int t = threadIdx.x;
+  red[t] = v;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) red[t] += red[t + w];
+    __syncthreads();
+  }
+  const double r = red[0];
+  __syncthreads();
+  return r;
+}
+__global__ __launch_bounds__(256) void groupnorm_stats_kernel(const float* x, int ld, int HW, int C, int G, float eps,
+                                                              float* stats) {
+  __shared__ double red[256];
+  const int g = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  const int cg = C / G, c0 = g * cg;
+  const long n = (long)HW * cg;
+  const float* xb = x + (long)b * HW * ld + c0;
+  double s = 0.0;
+  for (long i = t; i < n; i += 256) {
+    const long pix = i / cg;
+    s += (double)xb[pix * ld + (i - pix * cg)];
+  }
+  const double mean = block_sum256(s, red) / (double)n;
+  double q = 0.0;
+  for (long i = t; i < n; i += 256) {
+    const long pix = i / cg;
+    const double d = (double)xb[pix * ld + (i - pix * cg)] - mean;
+    q += d * d;
+  }
+  const double var = block_sum256(q, red) / (double)n;
+  for (int c = t; c < cg; c += 256) {
+    stats[2 * ((long)b * C + c0 + c)] = (float)mean;
+    stats[2 * ((long)b * C + c0 + c) + 1] = (float)(1.0 / sqrt(var + (double)eps));
+  }
+}
+
+// The normalisation with a per-channel affine (GroupNorm's weight / bias): v = (x - mean) * rstd *
+// gamma[c] + beta[c], relu (mode >= 1), + the residual (itself normalised and scaled when rstats /
+// rgamma / rbeta are given), relu (mode 2): raft_instnorm_apply plus the affine.
+__global__ void norm_apply_affine_kernel(const float* x, int ld, const float* stats, const float* gamma,
+                                         const float* beta, const float* resid, int rld, const float* rstats,
+                                         const float* rgamma, const float* rbeta, int mode, float* out, int old, int B,
+                                         int HW, int C) {
+  const long total = (long)B * HW * C;
+  GRID_STRIDE(i, total) {
+    const int c = i % C;
+    const long pix = i / C;
+    const int b = (int)(pix / HW);
+    const float* st = stats + 2 * ((long)b * C + c);
+    float v = (x[pix * ld + c] - st[0]) * st[1];
+    if (gamma) v = v * gamma[c];
+    if (beta) v = v + beta[c];
+    if (mode >= 1) v = fmaxf(v, 0.f);
+    if (resid) {
+      float r = resid[pix * rld + c];
+      if (rstats) {
+        const float* rs = rstats + 2 * ((long)b * C + c);
+        r = (r - rs[0]) * rs[1];
+        if (rgamma) r = r * rgamma[c];
+        if (rbeta) r = r + rbeta[c];
+      }
+      v = r + v;
+      if (mode == 2) v = fmaxf(v, 0.f);
+    }
+    out[pix * old + c] = v;
+  }
+}
+
 bool aligned16(const void* q) { return ((uintptr_t)q & 15) == 0; }
 
 }  // namespace
@@ -511,4 +585,26 @@ extern "C" int raft_instnorm_apply(const float* x, int ld, const float* stats, c
     hipLaunchKernelGGL(instnorm_apply_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, ld, stats, resid,
                        resid_ld, resid_stats, relu_mode, out, out_ld, B, HW, C);
   return check_launch("raft_instnorm_apply");
+}
+
+extern "C" int raft_groupnorm_stats(const float* x, int ld, int B, int HW, int C, int G, float eps, float* stats,
+                                    raft_stream_t stream) {
+  RAFT_REQUIRE(x && stats && B > 0 && HW > 0 && C > 0 && G > 0 && C % G == 0 && ld >= C && B < 65536 && G < 65536,
+               "raft_groupnorm_stats: bad arguments (C %% G == 0 required)");
+  hipLaunchKernelGGL(groupnorm_stats_kernel, dim3(G, B), dim3(256), 0, as_stream(stream), x, ld, HW, C, G, eps, stats);
+  return check_launch("raft_groupnorm_stats");
+}
+
+extern "C" int raft_norm_apply_affine(const float* x, int ld, const float* stats, const float* gamma, const float* beta,
+                                      const float* resid, int resid_ld, const float* resid_stats,
+                                      const float* resid_gamma, const float* resid_beta, int relu_mode, float* out,
+                                      int out_ld, int B, int HW, int C, raft_stream_t stream) {
+  RAFT_REQUIRE(x && stats && out && B > 0 && HW > 0 && C > 0 && ld >= C && out_ld >= C,
+               "raft_norm_apply_affine: bad arguments");
+  RAFT_REQUIRE(relu_mode >= 0 && relu_mode <= 2, "raft_norm_apply_affine: bad relu_mode");
+  RAFT_REQUIRE(!resid || resid_ld >= C, "raft_norm_apply_affine: bad resid_ld");
+  const long n = (long)B * HW * C;
+  hipLaunchKernelGGL(norm_apply_affine_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, ld, stats, gamma,
+                     beta, resid, resid_ld, resid_stats, resid_gamma, resid_beta, relu_mode, out, out_ld, B, HW, C);
+  return check_launch("raft_norm_apply_affine");
 }

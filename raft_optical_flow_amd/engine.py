@@ -49,9 +49,18 @@ def _conv_bn(conv, bn, device, **kw):
     return pack_conv(w, b, conv.stride, conv.padding, device=device, **kw)
 
 
-def check_norm(norm):
-    if norm not in ("instance", "batch", "none"):
+def check_norm(norm, block=False):
+    """The norms the HIP path plans: the encoders' instance / batch / none; block-level calls
+    (ResidualBlock / BottleneckBlock, core/extractor.py:6-116) also take their default, group."""
+    if norm not in ("instance", "batch", "none") and not (block and norm == "group"):
         raise NotImplementedError(f"norm_fn={norm!r} is not on the RAFT inference path")
+
+
+def _gn(mod):
+    """(num_groups, gamma, beta, eps) of an nn.GroupNorm, fp32 on its device."""
+    g = mod.weight.detach().float().contiguous() if mod.weight is not None else None
+    b = mod.bias.detach().float().contiguous() if mod.bias is not None else None
+    return (mod.num_groups, g, b, float(mod.eps))
 
 
 def pack_block(blk, norm, small, device) -> dict:
@@ -67,6 +76,11 @@ def pack_block(blk, norm, small, device) -> dict:
         dsn = getattr(blk, "norm3", None)
     d["ds"] = None if blk.downsample is None else _conv_bn(blk.downsample[0], bn(dsn), device)
     d["planes"] = d["conv3" if small else "conv2"].n
+    if norm == "group":
+        d["n1"], d["n2"] = _gn(blk.norm1), _gn(blk.norm2)
+        if small:
+            d["n3"] = _gn(blk.norm3)
+        d["nds"] = None if blk.downsample is None else _gn(dsn)
     return d
 
 
@@ -263,8 +277,74 @@ def plan_encoder_trunk(L, A: Arena, pe: PackedEncoder, x: Rows, n_img, h, w):
     return x, h, w
 
 
+def _gn_stats(L, A: Arena, x: Rows, n_img, hw, gn):
+    st = A.flat(2 * n_img * x.c)
+    L.append(Launch("raft_groupnorm_stats", x.ptr, x.ld, n_img, hw, x.c, gn[0], gn[3], st.data_ptr()))
+    return st
+
+
+def _gn_apply(L, A: Arena, x: Rows, st, gn, n_img, hw, mode, resid: Rows | None = None, rst=None, rgn=None) -> Rows:
+    """relu / residual tail of a GroupNorm (raft_norm_apply_affine: the normalisation, its affine, the
+    residual's own normalisation + affine where given)."""
+    out = Rows(A.rows(n_img * hw, x.c))
+    p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    L.append(Launch("raft_norm_apply_affine", x.ptr, x.ld, st.data_ptr(), p(gn[1]), p(gn[2]),
+                    resid.ptr if resid else None, resid.ld if resid else 0, p(rst),
+                    p(rgn[1]) if rgn else None, p(rgn[2]) if rgn else None, mode, out.ptr, out.ld, n_img, hw, x.c,
+                    keep=(gn, rgn)))
+    return out
+
+
+def _plan_residual_group(L, A, d, x: Rows, n, h, w):
+    """ResidualBlock with norm_fn='group' (core/extractor.py:6-56, the block's default norm):
+    relu(gn1(conv1 x)) -> relu(gn2(conv2 .)) -> relu(x or gn3(downsample x) + .)."""
+    c1, c2, ds = d["conv1"], d["conv2"], d["ds"]
+    ho, wo = K.conv_out_hw(c1, h, w)
+    npx, hw = n * ho * wo, ho * wo
+    t1 = Rows(A.rows(npx, c1.n))
+    _conv(L, c1, x, n, h, w, t1)
+    y1 = _gn_apply(L, A, t1, _gn_stats(L, A, t1, n, hw, d["n1"]), d["n1"], n, hw, 1)
+    t2 = Rows(A.rows(npx, c2.n))
+    _conv(L, c2, y1, n, ho, wo, t2)
+    st2 = _gn_stats(L, A, t2, n, hw, d["n2"])
+    if ds is not None:
+        t3 = Rows(A.rows(npx, ds.n))
+        _conv(L, ds, x, n, h, w, t3)
+        out = _gn_apply(L, A, t2, st2, d["n2"], n, hw, 2, resid=t3, rst=_gn_stats(L, A, t3, n, hw, d["nds"]),
+                        rgn=d["nds"])
+    else:
+        out = _gn_apply(L, A, t2, st2, d["n2"], n, hw, 2, resid=x)
+    return out, ho, wo
+
+
+def _plan_bottleneck_group(L, A, d, x: Rows, n, h, w):
+    """BottleneckBlock with norm_fn='group' (core/extractor.py:60-116)."""
+    c1, c2, c3, ds = d["conv1"], d["conv2"], d["conv3"], d["ds"]
+    ho, wo = K.conv_out_hw(c2, h, w)
+    t1 = Rows(A.rows(n * h * w, c1.n))
+    _conv(L, c1, x, n, h, w, t1)
+    y1 = _gn_apply(L, A, t1, _gn_stats(L, A, t1, n, h * w, d["n1"]), d["n1"], n, h * w, 1)
+    hw = ho * wo
+    t2 = Rows(A.rows(n * hw, c2.n))
+    _conv(L, c2, y1, n, h, w, t2)
+    y2 = _gn_apply(L, A, t2, _gn_stats(L, A, t2, n, hw, d["n2"]), d["n2"], n, hw, 1)
+    t3 = Rows(A.rows(n * hw, c3.n))
+    _conv(L, c3, y2, n, ho, wo, t3)
+    st3 = _gn_stats(L, A, t3, n, hw, d["n3"])
+    if ds is not None:
+        t4 = Rows(A.rows(n * hw, ds.n))
+        _conv(L, ds, x, n, h, w, t4)
+        out = _gn_apply(L, A, t3, st3, d["n3"], n, hw, 2, resid=t4, rst=_gn_stats(L, A, t4, n, hw, d["nds"]),
+                        rgn=d["nds"])
+    else:
+        out = _gn_apply(L, A, t3, st3, d["n3"], n, hw, 2, resid=x)
+    return out, ho, wo
+
+
 def _plan_residual(L, A, pe, d, x: Rows, n, h, w):
     """ResidualBlock (core/extractor.py:6-56)."""
+    if pe.norm == "group":
+        return _plan_residual_group(L, A, d, x, n, h, w)
     c1, c2, ds = d["conv1"], d["conv2"], d["ds"]
     ho, wo = K.conv_out_hw(c1, h, w)
     npx = n * ho * wo
@@ -297,6 +377,8 @@ def _plan_residual(L, A, pe, d, x: Rows, n, h, w):
 
 def _plan_bottleneck(L, A, pe, d, x: Rows, n, h, w):
     """BottleneckBlock (core/extractor.py:60-116)."""
+    if pe.norm == "group":
+        return _plan_bottleneck_group(L, A, d, x, n, h, w)
     c1, c2, c3, ds = d["conv1"], d["conv2"], d["conv3"], d["ds"]
     ho, wo = K.conv_out_hw(c2, h, w)
     if pe.norm == "instance":

@@ -41,7 +41,7 @@ class _BlockBase(nn.Module):
         from .engine import Arena, _plan_bottleneck, _plan_residual, check_norm, pack_block
         if self.training and isinstance(self.norm1, nn.BatchNorm2d):
             raise NotImplementedError("raft_optical_flow_amd blocks are inference-only: call .eval()")
-        check_norm(self.norm_fn)
+        check_norm(self.norm_fn, block=True)
         K.require_device(x)
         n, c, h, w = x.shape
         d = K.cached_pack(self, x.device, lambda: pack_block(self, self.norm_fn, self._small, x.device))

@@ -98,6 +98,8 @@ def _norm64(x, norm, mod):
                             mod.bias.double(), False, 0.0, mod.eps)
     if isinstance(mod, torch.nn.InstanceNorm2d):
         return F.instance_norm(x, eps=mod.eps)
+    if isinstance(mod, torch.nn.GroupNorm):
+        return F.group_norm(x, mod.num_groups, mod.weight.double(), mod.bias.double(), mod.eps)
     return x
 
 
@@ -110,9 +112,13 @@ def _randomise_bn(m, seed):
             mod.running_var.copy_(torch.rand(n, generator=g) * 0.4 + 0.8)
             mod.weight.data.copy_(torch.rand(n, generator=g) * 0.4 + 0.8)
             mod.bias.data.copy_(torch.randn(n, generator=g) * 0.1)
+        if isinstance(mod, torch.nn.GroupNorm):  # a non-trivial affine (its init is 1 / 0)
+            n = mod.num_channels
+            mod.weight.data.copy_(torch.rand(n, generator=g) * 0.8 + 0.6)
+            mod.bias.data.copy_(torch.randn(n, generator=g) * 0.2)
 
 
-@pytest.mark.parametrize("norm", ["instance", "batch", "none"])
+@pytest.mark.parametrize("norm", ["instance", "batch", "none", "group"])
 @pytest.mark.parametrize("stride", [1, 2])
 @pytest.mark.parametrize("bottleneck", [False, True])
 def test_encoder_blocks(norm, stride, bottleneck):
