@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define RAFT_HIP_ABI_VERSION 13
+#define RAFT_HIP_ABI_VERSION 14
 
 /* Negative return codes (argument errors, raised before any launch). */
 #define RAFT_E_INVALID (-1)   /* bad size / null pointer / unsupported shape */
@@ -82,6 +82,15 @@ int raft_corr_build(const float* fmap1, const float* fmap2, int ld, int B, int H
  * 5x the MFMA rate).  The RAFT forward uses F16X3 unless conv_precision="fp32". */
 int raft_corr_build_prec(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C,
                          int num_levels, float sqrt_c, int precision, float* pyramid, raft_stream_t stream);
+/* raft_corr_build_prec with a caller-owned workspace (the RAFT forward's call): in F16X3 the two
+ * feature maps are split into f16 hi / lo once (ws: raft_corr_build_ws_bytes, 16-byte aligned) and
+ * the GEMM streams the split rows into LDS by DMA; the pyramid is bit-identical to
+ * raft_corr_build_prec's.  ws = NULL (or FP32, or a split past 2 GiB) runs raft_corr_build_prec's
+ * kernels; a non-NULL ws smaller than needed is an error. */
+size_t raft_corr_build_ws_bytes(int B, int H, int W, int C);
+int raft_corr_build_ws(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C,
+                       int num_levels, float sqrt_c, int precision, void* ws, size_t ws_bytes,
+                       float* pyramid, raft_stream_t stream);
 /* Row-major copy of one level, out [B*H*W][H_l][W_l] (the reference's corr_pyramid[l]). */
 int raft_corr_pyramid_level(const float* pyramid, int B, int H, int W, int num_levels, int level,
                             float* out, raft_stream_t stream);

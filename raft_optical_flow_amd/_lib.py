@@ -29,7 +29,7 @@ PREC_F16 = 2     # single f16 product (mixed precision)
 PREC_BF16 = 3    # single bf16 product on v_mfma_f32_32x32x16_bf16 (bf16 mixed precision)
 PRECISIONS = {"fp32": PREC_FP32, "f16x3": PREC_F16X3, "f16": PREC_F16, "bf16": PREC_BF16}
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 RANGE_LIMIT = 32768.0  # RAFT_RANGE_LIMIT: |x| above it raises the f16x3 range guard
 
 EPI_LINEAR = 0
@@ -75,6 +75,8 @@ _PROTOS = {
     "raft_corr_pyramid_floats": (c_size_t, [c_int, c_int, c_int, c_int]),
     "raft_corr_build": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, P, P]),
     "raft_corr_build_prec": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, P, P]),
+    "raft_corr_build_ws_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "raft_corr_build_ws": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, P, c_size_t, P, P]),
     "raft_corr_pyramid_level": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "raft_corr_lookup": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, c_int, c_int, P, c_int, P, P]),
     "raft_corr_lookup_convf1": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, c_int, c_int, P, c_int, P,

@@ -702,8 +702,13 @@ class RaftPlan:
             # the correlation GEMM follows the conv arithmetic: exact f32 MFMA in "fp32"
             # mode, the fp32-accurate f16 split otherwise (raft_hip.h)
             cprec = _lib.PREC_FP32 if pk.precision == _lib.PREC_FP32 else _lib.PREC_F16X3
-            L.append(Launch("raft_corr_build_prec", fmap1.data_ptr(), fmap2.data_ptr(), C, B, h, w, C, lv, div,
-                            cprec, self.pyramid.data_ptr()))
+            # RAFT_CORR_BUILD3=1: the f16 split of both maps made once per build and the LDS-DMA
+            # GEMM (raft_corr_build_ws; bit-identical, not faster in the forward)
+            v3 = cprec == _lib.PREC_F16X3 and os.environ.get("RAFT_CORR_BUILD3", "0") == "1"
+            wsb = int(_lib.load().raft_corr_build_ws_bytes(B, h, w, C)) if v3 else 0
+            ws = A.flat((wsb + 3) // 4) if wsb else None
+            L.append(Launch("raft_corr_build_ws", fmap1.data_ptr(), fmap2.data_ptr(), C, B, h, w, C, lv, div,
+                            cprec, ws.data_ptr() if ws is not None else None, wsb, self.pyramid.data_ptr()))
         else:
             # AlternateCorrBlock pools num_levels times (core/corr.py:157-161); the
             # last level is never used, but its existence is the reference's size check.

@@ -161,7 +161,7 @@ class RAFT(nn.Module):
                  os.environ.get("RAFT_CONV_PAIR", "1"), os.environ.get("RAFT_FUSE_CONVF1", "1"),
                  os.environ.get("RAFT_FUSE_CONVC1", "1"), os.environ.get("RAFT_EPI_STATS", "1"),
                  os.environ.get("RAFT_IN_NORM", "1"), os.environ.get("RAFT_CHAIN", "0"), os.environ.get("RAFT_RESIDENT", "0"),
-                 os.environ.get("RAFT_HALO_KS", "1"))
+                 os.environ.get("RAFT_HALO_KS", "1"), os.environ.get("RAFT_CORR_BUILD3", "0"))
         guard = self.range_guard != "off"  # "off": no device-side checks either
         key = (batch, height, width, iters, bool(test_mode), bool(self.args.alternate_corr), bool(flow_init), prec,
                knobs, guard)
