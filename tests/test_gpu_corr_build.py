@@ -76,3 +76,23 @@ def test_corr_build_ws_too_small_is_an_error():
                                         B, H, W, C, 2, K.sqrt_c(C), _lib.PREC_F16X3, ctypes.c_void_p(ws.data_ptr()),
                                         need - 16, ctypes.c_void_p(pyr.data_ptr()), ctypes.c_void_p(K.stream_handle()))
     assert rc != 0
+
+
+def test_forward_corr_build3_bit_exact(monkeypatch):
+    """RAFT-full at config 2's size: the forward with the pre-split LDS-DMA correlation build
+    (RAFT_CORR_BUILD3=1) gives the flow of the default build bit for bit."""
+    import argparse
+    from raft_optical_flow_amd import RAFT
+    from raft_optical_flow_amd.init import seeded_images, seeded_state_dict
+    m = RAFT(argparse.Namespace(small=False, mixed_precision=False, alternate_corr=False))
+    m.conv_precision = "f16x3"
+    m.load_state_dict(seeded_state_dict(m, 0))
+    m = m.to(DEV).eval()
+    i1, i2 = seeded_images(1, 440, 1024, seed=4)
+    i1, i2 = i1.to(DEV), i2.to(DEV)
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("RAFT_CORR_BUILD3", v)
+        with torch.no_grad():
+            outs.append(m(i1, i2, iters=4, test_mode=True))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
