@@ -207,7 +207,7 @@ __global__ __launch_bounds__(256) void corr_build_kernel(CorrBuildArgs a) {
 // products (the 64 x 64 kernel moved 2 x the L2 bytes per output).  The N tile is an 8 x 16
 // (h2, w2) block: per query pixel the epilogue writes two 256-B runs of level-0 tiles and one
 // 128-B run of two level-1 tiles.
-constexpr int CB2_BM = 128, CB2_BN = 128, CB2_TLD = CB2_BN + 1;
+constexpr int CB2_BM = 128, CB2_BN = 128, CB2_TLD = CB2_BN + 4;  // 16-B aligned epilogue rows
 
 // the (batch, M tile, N tile) of this work-group in the order CorrBuildArgs names
 __device__ __forceinline__ void cb_tile(const CorrBuildArgs& a, int& b, int& mi, int& ni) {
@@ -234,6 +234,7 @@ __device__ __forceinline__ void cb_tile(const CorrBuildArgs& a, int& b, int& mi,
 __global__ __launch_bounds__(512, 2) void corr_build2_kernel(CorrBuildArgs a) {
   constexpr int STAGE = (CB2_BM + CB2_BN) * CB_LDSK;  // floats per stage (144-B rows)
   static_assert(2 * STAGE >= CB2_BM * CB2_TLD, "the epilogue tile fits the staging area");
+  static_assert(CB2_TLD % 4 == 0, "16-B aligned epilogue rows");
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 3, wn = wave >> 2;  // 32 query rows x 64 block pixels per wave
@@ -242,7 +243,10 @@ __global__ __launch_bounds__(512, 2) void corr_build2_kernel(CorrBuildArgs a) {
   const int m0 = mi * CB2_BM;
   const int nbx = (a.W + 15) / 16;
   const int by = ni / nbx, bx = ni - (ni / nbx) * nbx;
-  const int lr = tid >> 3, lq = tid & 7;  // staged rows lr, lr + 64; channel quad lq of the K-step
+  // staged rows lr, lr + 64; channel quad lq of the K-step.  The 16 lanes of a ds_write_b64 group
+  // take rows R and R + 4 (row stride 36 dwords: 4 rows apart is 16 banks apart), conflict-free
+  const int g16 = tid >> 4;
+  const int lr = 8 * (g16 >> 2) + (g16 & 3) + 4 * ((tid >> 3) & 1), lq = tid & 7;
   const float* arow[2];
   const float* brow[2];
   bool av_[2], bv_[2];
@@ -356,13 +360,14 @@ __global__ __launch_bounds__(512, 2) void corr_build2_kernel(CorrBuildArgs a) {
 #else
     if (p1 < a.P && ty < a.l0.th && tx < a.l0.tw) {
 #endif
-      const float* t = T + row * CB2_TLD + (ti * 4 + (e >> 2)) * 16 + tj * 4;
+      // one conflict-free ds_read_b128 (row stride 132 floats)
+      const f32x4 v = *reinterpret_cast<const f32x4*>(T + row * CB2_TLD + (ti * 4 + (e >> 2)) * 16 + tj * 4);
       f32x4* dst = reinterpret_cast<f32x4*>(a.pyr + a.l0.off + ((long)b * a.P + p1) * a.l0.mapsz +
                                             ((long)ty * a.l0.tw + tx) * 16 + e);
       if (a.nt)
-        __builtin_nontemporal_store(f32x4{t[0], t[1], t[2], t[3]}, dst);
+        __builtin_nontemporal_store(v, dst);
       else
-        *dst = f32x4{t[0], t[1], t[2], t[3]};
+        *dst = v;
     }
   }
   if (a.has_l1 && by < a.l1.th) {
@@ -385,7 +390,8 @@ __global__ __launch_bounds__(512, 2) void corr_build2_kernel(CorrBuildArgs a) {
         float v = 0.f;
         if (by * 4 + yy < a.l1.h && bx * 8 + xx < a.l1.w) {
           const float* t = T + row * CB2_TLD + (2 * yy) * 16 + 2 * xx;
-          v = (((t[0] + t[1]) + t[16]) + t[17]) / 4.0f;  // avg_pool2d window order
+          const float2 u0 = *reinterpret_cast<const float2*>(t), u1 = *reinterpret_cast<const float2*>(t + 16);
+          v = (((u0.x + u0.y) + u1.x) + u1.y) / 4.0f;  // avg_pool2d window order
         }
         v4[c] = v;
       }
