@@ -96,3 +96,18 @@ def test_forward_corr_build3_bit_exact(monkeypatch):
         with torch.no_grad():
             outs.append(m(i1, i2, iters=4, test_mode=True))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("order", ["8,0,1", "1,1,0", "4,1,1", "3,0,0"])
+def test_corr_build_tile_order_bit_identical(monkeypatch, order):
+    """RAFT_CB_ORDER only permutes which work-group builds which tile: every order gives the same
+    pyramid bit for bit (ragged tiles, B = 2, so the XCD runs straddle images)."""
+    B, H, W, C, L = 2, 29, 70, 256, 4
+    g = torch.Generator(device=DEV).manual_seed(7)
+    f = torch.randn(2 * B * H * W, C, device=DEV, generator=g)
+    f1, f2 = f[: B * H * W], f[B * H * W:]
+    monkeypatch.delenv("RAFT_CB_ORDER", raising=False)
+    ref = _build(f1, f2, C, B, H, W, C, L, None)
+    monkeypatch.setenv("RAFT_CB_ORDER", order)
+    got = _build(f1, f2, C, B, H, W, C, L, None)
+    assert torch.equal(got, ref)
