@@ -1,6 +1,6 @@
 """Benchmark: RAFT inference image-pairs/s on MI355X (BASELINE.json config 2).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W]     (N > 1: spawns one rank per GPU itself)
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
 A step = one RAFT-full forward (random-init weights, seeded) over one batch of
@@ -232,6 +232,44 @@ def cpu_baseline(args, budget_s=12.0):
                       f"container), torch.set_num_threads({threads}), {dt:.1f} s"}
 
 
+def spawn_ranks(n):
+    """`bench.py --gpus N` (N > 1) without a launcher: start N rank processes of this script, rank r on
+    cuda:r (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, as torch.distributed.run
+    sets them), and exit with the worst of their exit codes.  This process never touches the GPU
+    (torch.cuda.device_count() does not initialise it on this image): the ranks are children, not an
+    exec.  Rank 0 prints the JSON line on the inherited stdout.  A failed rank stops the others."""
+    import socket
+    import subprocess
+    rehearse = os.environ.get("RAFT_BENCH_REHEARSE_1GPU") == "1"
+    visible = torch.cuda.device_count()
+    if not rehearse and n > visible:
+        raise SystemExit(f"bench.py: --gpus {n} but only {visible} GPU(s) are visible")
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:  # the exact child PIDs this process started
+                    q.terminate()
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+    return rc if rc >= 0 else 1
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -248,13 +286,21 @@ def main():
     ap.add_argument("--precision", choices=["fp32", "f16x3", "f16", "bf16"], default=None,
                     help="conv arithmetic (default: the RAFT default, f16x3)")
     args = ap.parse_args()
-
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per GPU "
+                         f"(--nproc-per-node {args.gpus}) or drop --gpus")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal of the N > 1 path on a one-GPU box (tests / development only): every rank on
     # cuda:0 over gloo (RCCL, like NCCL, refuses two ranks on one device)
     rehearse = os.environ.get("RAFT_BENCH_REHEARSE_1GPU") == "1"
+    if not rehearse and local_rank >= torch.cuda.device_count():
+        raise SystemExit(f"bench.py: rank {rank} needs cuda:{local_rank}, only {torch.cuda.device_count()} visible")
     dev_index = 0 if rehearse else local_rank
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
@@ -319,6 +365,9 @@ def main():
         elapsed = float(t.item())
     pairs = world * args.batch * args.steps
     value = pairs / elapsed
+    if rank != 0:  # the per-kernel figures and the JSON line are rank 0's
+        dist.destroy_process_group()
+        return
 
     # ---- per-kernel live timing (HIP events on the launch stream, hipGraph replays) ----------
     from raft_optical_flow_amd import kernels as K

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define RAFT_HIP_ABI_VERSION 14
+#define RAFT_HIP_ABI_VERSION 15
 
 /* Negative return codes (argument errors, raised before any launch). */
 #define RAFT_E_INVALID (-1)   /* bad size / null pointer / unsupported shape */
@@ -55,9 +55,15 @@ int raft_hip_abi_version(void);
 const char* raft_hip_arch(void);        /* offload arch the library was built for ("gfx950") */
 const char* raft_hip_last_error(void);  /* message of the last failure on this thread ("" if none) */
 /* first 16 hex digits of the sha256 of the sources the library was built from (csrc/Makefile
- * SRC_HASH: the .hip files in SRCS order, csrc/*.hpp, include/raft_hip.h); the Python loader
+ * SRC_HASH: the .hip files in SRCS order, the csrc .hpp headers and include/raft_hip.h); the loader
  * refuses a library whose hash differs from the sources beside it (a stale prebuilt .so) */
 const char* raft_hip_source_hash(void);
+/* Debug (tests only): fill the LDS of every CU with all-ones words (NaN as fp32, f16 and bf16) by
+ * kernels that take a CU's whole 160 KiB each; no global memory is touched.  A kernel launched next
+ * on the stream that reads LDS it did not write then sees NaN: the parity tests run every launch of
+ * a forward behind it and require the bit-identical, finite result (round 3's conv_stem K-padding
+ * read was such a bug). */
+int raft_debug_fill_lds_nan(raft_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * All-pairs correlation pyramid (CorrBlock)
@@ -82,15 +88,6 @@ int raft_corr_build(const float* fmap1, const float* fmap2, int ld, int B, int H
  * 5x the MFMA rate).  The RAFT forward uses F16X3 unless conv_precision="fp32". */
 int raft_corr_build_prec(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C,
                          int num_levels, float sqrt_c, int precision, float* pyramid, raft_stream_t stream);
-/* raft_corr_build_prec with a caller-owned workspace (the RAFT forward's call): in F16X3 the two
- * feature maps are split into f16 hi / lo once (ws: raft_corr_build_ws_bytes, 16-byte aligned) and
- * the GEMM streams the split rows into LDS by DMA; the pyramid is bit-identical to
- * raft_corr_build_prec's.  ws = NULL (or FP32, or a split past 2 GiB) runs raft_corr_build_prec's
- * kernels; a non-NULL ws smaller than needed is an error. */
-size_t raft_corr_build_ws_bytes(int B, int H, int W, int C);
-int raft_corr_build_ws(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C,
-                       int num_levels, float sqrt_c, int precision, void* ws, size_t ws_bytes,
-                       float* pyramid, raft_stream_t stream);
 /* Row-major copy of one level, out [B*H*W][H_l][W_l] (the reference's corr_pyramid[l]). */
 int raft_corr_pyramid_level(const float* pyramid, int B, int H, int W, int num_levels, int level,
                             float* out, raft_stream_t stream);
@@ -346,24 +343,6 @@ int raft_conv2d(const raft_conv2d_params* p, raft_stream_t stream);
  * edge on ROCm).  Otherwise, or when one reads what the other writes, or both write a common
  * element (column ranges of their output rows meet), the two run in order. */
 int raft_conv2d_pair(const raft_conv2d_params* p0, const raft_conv2d_params* p1, raft_stream_t stream);
-/* Dependent convolutions in ONE launch (core/update.py:74-121,169-216,297-325: the update block's
- * convc2|convf2 -> conv -> convz1|convr1 -> convq1 -> convz2|convr2 -> convq2 -> flow-head conv1
- * sequence of one refinement iteration).  stages[2s] is stage s's conv and stages[2s+1] NULL or a
- * second, independent conv of the stage (as raft_conv2d_pair); stage s+1 may read anything
- * stages <= s wrote.  Results are identical to raft_conv2d / raft_conv2d_pair of the stages in
- * order.  When every stage is a halo-kernel conv (stride 1, "same", 3x3 / 1x5 / 5x1,
- * RAFT_PREC_F16X3, no stats_part / in_norm) of one output size, the stages run as one persistent
- * launch whose tiles wait on completion counters of their 3x3 spatial neighbourhood in the
- * previous stage (no kernel boundary between the stages); otherwise they run in order.
- * sync: raft_conv2d_chain_sync_ints(n_stages, batch, out_h, out_w) ints in device memory, zeroed
- * once before the first call (every launch leaves them zeroed), not shared by launches that may
- * run concurrently (NULL: run in order).  err: optional device int set to 1 if a wait timed out
- * (the results are then invalid), e.g. a range flag (RAFT_RANGE_LIMIT) that re-runs the work. */
-int raft_conv2d_chain_sync_ints(int n_stages, int batch, int out_h, int out_w);
-int raft_conv2d_chain(const raft_conv2d_params* const* stages, int n_stages, int* sync, int* err,
-                      raft_stream_t stream);
-/* 1 when raft_conv2d_chain (with a sync buffer) runs these stages as one chained launch, else 0. */
-int raft_conv2d_chain_covered(const raft_conv2d_params* const* stages, int n_stages);
 /* fp32 packed weight [n_pad][k_pad] -> split form for RAFT_PREC_F16X3 / F16:
  * per row and 32-wide K-step, 32 f16 hi then 32 f16 lo (lo scaled by 2048);
  * out holds n_pad*k_pad*4 bytes, like the input. */

@@ -29,7 +29,7 @@ PREC_F16 = 2     # single f16 product (mixed precision)
 PREC_BF16 = 3    # single bf16 product on v_mfma_f32_32x32x16_bf16 (bf16 mixed precision)
 PRECISIONS = {"fp32": PREC_FP32, "f16x3": PREC_F16X3, "f16": PREC_F16, "bf16": PREC_BF16}
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 RANGE_LIMIT = 32768.0  # RAFT_RANGE_LIMIT: |x| above it raises the f16x3 range guard
 
 EPI_LINEAR = 0
@@ -72,11 +72,10 @@ _PROTOS = {
     "raft_hip_arch": (c_char_p, []),
     "raft_hip_last_error": (c_char_p, []),
     "raft_hip_source_hash": (c_char_p, []),
+    "raft_debug_fill_lds_nan": (c_int, [P]),
     "raft_corr_pyramid_floats": (c_size_t, [c_int, c_int, c_int, c_int]),
     "raft_corr_build": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, P, P]),
     "raft_corr_build_prec": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, P, P]),
-    "raft_corr_build_ws_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
-    "raft_corr_build_ws": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, P, c_size_t, P, P]),
     "raft_corr_pyramid_level": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "raft_corr_lookup": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, c_int, c_int, P, c_int, P, P]),
     "raft_corr_lookup_convf1": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, c_int, c_int, P, c_int, P,
@@ -105,9 +104,6 @@ _PROTOS = {
                                          ctypes.POINTER(c_int)]),
     "raft_conv2d": (c_int, [ctypes.POINTER(ConvParams), P]),
     "raft_conv2d_pair": (c_int, [ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), P]),
-    "raft_conv2d_chain_sync_ints": (c_int, [c_int, c_int, c_int, c_int]),
-    "raft_conv2d_chain": (c_int, [ctypes.POINTER(ctypes.POINTER(ConvParams)), c_int, P, P, P]),
-    "raft_conv2d_chain_covered": (c_int, [ctypes.POINTER(ctypes.POINTER(ConvParams)), c_int]),
     "raft_conv2d_stats_slots": (c_int, [ctypes.POINTER(ConvParams)]),
     "raft_conv2d_in_norm_ok": (c_int, [ctypes.POINTER(ConvParams)]),
     "raft_instnorm_merge": (c_int, [P, c_int, c_int, c_int, c_int, c_float, P, P]),
@@ -163,7 +159,8 @@ def load():
         got = lib.raft_hip_source_hash().decode()
         if want is not None and got != want and os.environ.get("RAFT_SKIP_SRC_CHECK", "0") != "1":
             raise RaftHipError(f"{LIB_PATH} was built from other sources (hash {got}, the sources here hash "
-                               f"{want}): rebuild it with `python __graft_entry__.py build`")
+                               f"{want}; the hash covers csrc/*.hip, csrc/*.hpp and include/raft_hip.h): rebuild it "
+                               f"with `python __graft_entry__.py build`, or set RAFT_SKIP_SRC_CHECK=1 to load it anyway")
         _lib = lib
         return lib
 
@@ -179,7 +176,10 @@ def source_hash() -> str | None:
     if not (os.path.exists(mk) and os.path.exists(hdr)):
         return None
     with open(mk) as fh:
-        srcs = next(l.split(":=", 1)[1].split() for l in fh if l.startswith("SRCS :="))
+        srcs = next((ln.split(":=", 1)[1].split() for ln in fh if ln.startswith("SRCS :=")), None)
+    if not srcs:
+        raise RaftHipError(f"{mk} has no one-line 'SRCS := ...' list: cannot hash the HIP sources to check "
+                           f"{LIB_PATH} against them (RAFT_SKIP_SRC_CHECK=1 skips the check)")
     files = [os.path.join(csrc, f) for f in srcs] + sorted(glob.glob(os.path.join(csrc, "*.hpp"))) + [hdr]
     h = hashlib.sha256()
     for f in files:

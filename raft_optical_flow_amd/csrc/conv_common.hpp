@@ -202,8 +202,7 @@ __device__ __forceinline__ void store_tile16(float* dst, int ld, long nrows, con
   }
 }
 
-// WT: write-through stores (sc1: the bytes leave the XCD's L2 at once), for outputs another
-// work-group of the same launch reads after a completion counter (conv_chain_kernel)
+// WT: write-through stores (sc1: the bytes leave the XCD's L2 at once)
 template <bool WT = false>
 __device__ __forceinline__ void tile_epilogue(const raft_conv2d_params& p, const int (&rows)[16], int n,
                                               const f32x16& acc) {
@@ -378,14 +377,6 @@ struct HaloOperands {
 int conv_halo_launch(const HaloOperands& o, hipStream_t s);
 // two independent convs of one shape class in one launch; 1 (nothing launched) if they do not qualify
 int conv_halo_launch_pair(const HaloOperands& o0, const HaloOperands& o1, hipStream_t s);
-// dependent stride-1 conv stages (nconv[s] = 1 or 2 convs each, ops in stage order) as one
-// persistent launch (conv_chain_kernel); 1 (nothing launched) if they do not qualify
-int conv_halo_launch_chain(const HaloOperands* ops, const int* nconv, int n_stages, int* sync, int* err,
-                           hipStream_t s);
-int conv_halo_chain_sync_ints(int n_stages, int batch, int out_h, int out_w);
-// conv_resident.hip: the weight-resident persistent 3x3 conv (<= 96 input channels, many tiles);
-// 1 (nothing launched) when the conv is not one it covers
-int conv_resident_launch(const HaloOperands& o, hipStream_t s);
 // conv_stem.hip: the encoders' 7x7 / stride-2 stem over 3 channels; 1 (nothing launched) otherwise
 int conv_stem_launch(const raft_conv2d_params& p, int k_pad, hipStream_t s);
 // tile-statistics slots per image of a conv on the halo / stem kernel (raft_conv2d_stats_slots), 0 if none

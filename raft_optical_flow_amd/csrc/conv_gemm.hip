@@ -919,7 +919,6 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
     RAFT_REQUIRE(p.stats_ld >= p.n && ((uintptr_t)p.stats_part & 15) == 0,
                  "raft_conv2d: stats_ld >= n and a 16-B aligned stats_part");
   }
-  if (p.mode == RAFT_CONV_VEC && conv_resident_launch(o, s) == 0) return check_launch("raft_conv2d(resident)");
   if (p.mode == RAFT_CONV_VEC && conv_halo_launch(o, s) == 0) return check_launch("raft_conv2d(halo)");
   if (p.mode == RAFT_CONV_GATHER && conv_stem_launch(p, o.k_pad, s) == 0) return check_launch("raft_conv2d(stem)");
   a.gn = n_pad / BN;
@@ -966,69 +965,4 @@ extern "C" int raft_conv2d_pair(const raft_conv2d_params* p0, const raft_conv2d_
   rc = raft_conv2d(p0, stream);
   if (rc) return rc;
   return raft_conv2d(p1, stream);
-}
-
-constexpr int CHAIN_MAXC = 16;
-
-extern "C" int raft_conv2d_chain_sync_ints(int n_stages, int batch, int out_h, int out_w) {
-  if (n_stages < 1 || batch < 1 || out_h < 1 || out_w < 1) return 0;
-  return conv_halo_chain_sync_ints(n_stages, batch, out_h, out_w);
-}
-
-namespace {
-// raft_conv2d_chain's checks; sets chainable when the stages may run as one chained launch
-int chain_prepare(const raft_conv2d_params* const* stages, int n_stages, HaloOperands* ops, int* nconv,
-                  bool& chainable) {
-  RAFT_REQUIRE(stages && n_stages >= 1, "raft_conv2d_chain: no stages");
-  RAFT_REQUIRE(n_stages <= CHAIN_MAXC / 2, "raft_conv2d_chain: at most %d stages", CHAIN_MAXC / 2);
-  int nc = 0;
-  for (int s = 0; s < n_stages; ++s) {
-    const raft_conv2d_params* p0 = stages[2 * s];
-    const raft_conv2d_params* p1 = stages[2 * s + 1];
-    RAFT_REQUIRE(p0 != nullptr, "raft_conv2d_chain: stage %d has no conv", s);
-    ConvArgs a;
-    int rc = conv_prepare(p0, a, ops[nc]);
-    if (rc) return rc;
-    nconv[s] = 1;
-    if (p1) {
-      rc = conv_prepare(p1, a, ops[nc + 1]);
-      if (rc) return rc;
-      nconv[s] = 2;
-      // a pair stage runs as one only when it could run as one raft_conv2d_pair launch
-      chainable = chainable && !reads_output_of(*p1, *p0) && !reads_output_of(*p0, *p1) && !writes_overlap(*p0, *p1);
-    }
-    for (int j = 0; j < nconv[s]; ++j) {
-      const raft_conv2d_params& p = ops[nc + j].p;
-      chainable = chainable && p.mode == RAFT_CONV_VEC && !small_n(p) && !p.stats_part && !p.in_norm;
-    }
-    nc += nconv[s];
-  }
-  return 0;
-}
-}  // namespace
-
-extern "C" int raft_conv2d_chain_covered(const raft_conv2d_params* const* stages, int n_stages) {
-  HaloOperands ops[CHAIN_MAXC];
-  int nconv[CHAIN_MAXC / 2];
-  bool chainable = true;
-  if (chain_prepare(stages, n_stages, ops, nconv, chainable)) return 0;
-  return chainable && conv_halo_launch_chain(ops, nconv, n_stages, nullptr, nullptr, nullptr) == 0 ? 1 : 0;
-}
-
-extern "C" int raft_conv2d_chain(const raft_conv2d_params* const* stages, int n_stages, int* sync, int* err,
-                                 raft_stream_t stream) {
-  HaloOperands ops[CHAIN_MAXC];
-  int nconv[CHAIN_MAXC / 2];
-  bool chainable = sync != nullptr;
-  const int rc0 = chain_prepare(stages, n_stages, ops, nconv, chainable);
-  if (rc0) return rc0;
-  if (chainable && conv_halo_launch_chain(ops, nconv, n_stages, sync, err, as_stream(stream)) == 0)
-    return check_launch("raft_conv2d_chain");
-  // not chainable: the stages in order
-  for (int s = 0; s < n_stages; ++s) {
-    const int rc = stages[2 * s + 1] ? raft_conv2d_pair(stages[2 * s], stages[2 * s + 1], stream)
-                                     : raft_conv2d(stages[2 * s], stream);
-    if (rc) return rc;
-  }
-  return 0;
 }

@@ -128,65 +128,12 @@ __device__ __forceinline__ unsigned long long hstamp_now() {
 }
 #endif
 
-// Completion counters of a chained launch, one per 128-B line: a line takes only the adds of one
-// spatial tile's producers (atomics on one line serialise at ~90 per us) and its pollers
-constexpr int CHAIN_PAD = 32;
-
-// A chained launch's view of one tile (conv_chain_kernel): the completion counters of the stage
-// the tile waits for (its 3x3 spatial neighbourhood, dep_target each) and of its own stage.
-struct ChainCtl {
-  const int* dep;   // per spatial tile of the producing stage, or nullptr (no wait)
-  int dep_target;   // a spatial tile of the producing stage is complete at this count
-  int* pub;         // per spatial tile of this tile's stage: +1 per compute wave when its stores landed
-  int* abort;       // set when a wait timed out: later waits give up at once
-  int* err;         // sticky error flag (the plan's range flag: the forward re-runs in fp32)
-};
-
-// Tile wait of a chained launch (one loader wave): polls the producing stage's counters of the
-// tile's 3x3 neighbourhood with relaxed agent-scope (sc1) loads.  The hand-off is the counter form
-// of MI355X_MICROARCH.md's inter-workgroup table: producers store every handed-off byte sc1 (whole
-// 128-B lines per store instruction), drain them (vmcnt 0) and add to the counter per wave; the
-// consumer polls with sc1 loads, a work-group barrier follows the poll, and every load of handed-off
-// bytes (the patch loads, the epilogue's operand loads) is an sc1 load: no acquire fence.
-// Bounded: after ~50 ms it sets abort + err and goes on (a wrong, flagged result instead of a
-// hung GPU).
-__device__ __forceinline__ void chain_wait(const ChainCtl& c, int b, int ty, int tx, int ty_n, int tx_n, int lane) {
-  const int dy = lane / 3 - 1, dx = lane % 3 - 1;
-  const int y = ty + dy, x = tx + dx;
-  const bool need = lane < 9 && (unsigned)y < (unsigned)ty_n && (unsigned)x < (unsigned)tx_n;
-  const int* cnt = c.dep + (((long)b * ty_n + (need ? y : 0)) * tx_n + (need ? x : 0)) * CHAIN_PAD;
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  while (true) {
-    const int v = need ? __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : c.dep_target;
-    if (__all(v >= c.dep_target)) break;
-    if (__hip_atomic_load(c.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {  // 50 ms at 100 MHz
-      if (lane == 0) {
-        __hip_atomic_store(c.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (c.err) __hip_atomic_store(c.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      break;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-#ifdef CHAIN_ACQ  // dev builds: the acquire form (buffer_inv sc1) on top
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 // The tile body (one 8x16-pixel x BNT-column tile of the conv `a`, tile index q within it; smem =
 // the work-group's LDS).  ENC: the encoder features (InstanceNorm partial statistics in the
 // epilogue, the input's InstanceNorm applied by the 3x3 loaders); separate instantiations, so the
-// update block's convs compile exactly as without them.  CH: a tile of a chained launch
-// (conv_chain_kernel): the loaders wait for the producing stage's neighbourhood before the first
-// patch load, the epilogue stores write through to memory (sc1) and every compute wave bumps the
-// tile's completion counter once its stores have landed.
-// KS = 2: two MFMA waves per SIMD share each 32-pixel block, taking alternate K-steps (a
-// 768-thread work-group); their partial sums meet in LDS before the epilogue, so one wave's
-// fragment reads and waits run under the other's MFMAs at the same LDS bytes per MFMA.
-template <int KH, int KW, int BNT, int PREC, bool ENC = false, bool CH = false, int KS = 1>
-__device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q, char* smem, const ChainCtl& ctl) {
+// update block's convs compile exactly as without them.
+template <int KH, int KW, int BNT, int PREC, bool ENC = false>
+__device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q, char* smem) {
   constexpr bool X3 = PREC == RAFT_PREC_F16X3;
   constexpr bool BF = PREC == RAFT_PREC_BF16;
   using C = HaloCfg<KH, KW, BNT, X3 ? 128 : 64>;
@@ -222,17 +169,15 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
   // (+ the input InstanceNorm table of the 3x3 convs: {mean, 1/std} of <= 256 channels)
   constexpr int NORM_BYTES = (ENC && KH == 3 && KW == 3 && D == 3) ? 256 * 8 : 0;
   static_assert(C::LDS_B + C::LDS_A + NORM_BYTES <= C::LB, "LDS budget with the norm table");
-  static_assert(!CH || (LSPLIT && !ENC), "chained tiles: the pre-split patch path, no encoder features");
 
 #ifdef STAMPS
   const unsigned long long r_entry = hstamp_real(), c_entry = hstamp_now();
 #endif
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool loader = w >= 4 * KS;  // the last 4 waves move the operands, the others compute
+  const bool loader = w >= 4;  // the last 4 waves move the operands, the others compute
   const int lw = w & 3;
-  const int wc = w & 3, kp = w >> 2;  // compute waves: block index and K part (KS = 2)
-  static_assert(KS == 1 || (KS == 2 && LSPLIT && !ENC && !CH && MF == 1 && U % 2 == 0), "K-split pairs");
+  const int wc = w & 3;  // compute waves: block index
 
   // tile (N fastest: an output tile's N-tiles share its input patch in L2)
   const HaloArgs& a = args[prob];
@@ -373,7 +318,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
           for (int q = 0; q < 2; ++q) {
             const unsigned ch = cb + tg8[i] + 4u * q;
             const unsigned voff = (tpix[i] != OFF_INVALID && ch < lim) ? (tpix[i] * ld + ch) * 4u : OFF_INVALID;
-            dst[i][q] = buf_load4<CH ? CPOL_SC1 : 0>(s0 ? rs0 : rs1, voff, 0);
+            dst[i][q] = buf_load4<0>(s0 ? rs0 : rs1, voff, 0);
           }
       };
       const bool nrm = NORM_BYTES > 0 && p.in_norm != nullptr;
@@ -410,12 +355,6 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
         const int c = (U * u + T - 1) / T;
         return c * T < U * u + U ? c : -1;
       };
-      if constexpr (CH) {
-#ifndef CHAIN_ABL_NOWAIT  // timing ablation (dev builds only): no waits (wrong results)
-        if (lw == 0 && ctl.dep) chain_wait(ctl, b, sr / a.tx_n, sr % a.tx_n, a.ty_n, a.tx_n, lane);
-#endif
-        __builtin_amdgcn_s_barrier();  // no wave loads the tile's operands before the acquire
-      }
       constexpr int PMAX = (U * D + T - 1) / T + 1;  // chunk starts in the prologue's sets
       Staged pv[PMAX];
       int pcs[PMAX];
@@ -465,7 +404,6 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
         __builtin_amdgcn_s_barrier();
       }
       wait_vm<0>();
-      if constexpr (KS == 2) __builtin_amdgcn_s_barrier();  // the K parts' partial sums are in LDS
       return;
     }
     // Super-step s: issue load set s+D, wait until load set s+2 has landed
@@ -631,20 +569,15 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
   // all in load sets s and s+1), then one barrier.  K-steps past nk (up to
   // U*ns) run on zero weights and zero patches: they add exact zeros, and the
   // loop body has no branches.
-  if (kp == 0) {
 #pragma unroll
-    for (int u = 0; u < D; ++u) issue_weights(u);
-  }
-  if constexpr (CH) __builtin_amdgcn_s_barrier();  // the loaders' wait for the producing stage
+  for (int u = 0; u < D; ++u) issue_weights(u);
   wait_vm<NWP * (D - 2)>();      // the weights of sets 0 and 1 (sets 2 .. D-1: before the first loop barrier)
   __builtin_amdgcn_s_barrier();  // load sets 0 and 1 have landed
 #ifdef HALO_PRIO
   __builtin_amdgcn_s_setprio(HALO_PRIO);
 #endif
   Frag F[2];
-  if constexpr (KS == 2) {
-    // (no look-ahead: the partner wave's MFMAs cover this wave's reads)
-  } else if constexpr (LSPLIT) {
+  if constexpr (LSPLIT) {
     read_b(F[0]);
     read_a_split(F[0]);
   } else {
@@ -664,16 +597,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
       mfma_step(F[e & 1]);
       asm volatile("" ::"v"(F[0].ah[0][0]), "v"(F[1].ah[0][0]));
 #else
-      if constexpr (KS == 2) {
-        if ((e & 1) == kp) {
-          read_b(F[0]);
-          read_a_split(F[0]);
-          mfma_step(F[0]);
-        } else {  // the partner's K-step: move the cursors past it
-          b_bs = b_bs + 1 == SB ? 0 : b_bs + 1;
-          advance_a();
-        }
-      } else if constexpr (LSPLIT) {
+      if constexpr (LSPLIT) {
         read_b(F[(e + 1) & 1]);
         read_a_split(F[(e + 1) & 1]);
         mfma_step(F[e & 1]);
@@ -713,25 +637,6 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[f][sb][r] += accx[f][sb][r] * (1.0f / SPLIT_SCALE);
   }
-  if constexpr (KS == 2) {
-    // K part 1 hands its partial sums to K part 0 through LDS (the rings are free: every read of
-    // the loop is done and no load is in flight after its last barrier), then leaves
-    float* red = reinterpret_cast<float*>(smem) + (wc * NSUB * 16) * 64 + lane;
-    if (kp == 1) {
-#pragma unroll
-      for (int sb = 0; sb < NSUB; ++sb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) red[(sb * 16 + r) * 64] = acc[0][sb][r];
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
-    if (kp == 1) return;
-#pragma unroll
-    for (int sb = 0; sb < NSUB; ++sb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[0][sb][r] += red[(sb * 16 + r) * 64];
-  }
-
   // ---- epilogue: register r of block f holds row m = (r&3) + 8(r>>2) + 4h of its 32 pixels
 #pragma unroll
   for (int f = 0; f < MF; ++f) {
@@ -743,21 +648,13 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
       rows[r] = (y < p.out_h && x < p.out_w) ? (b * p.out_h + y) * p.out_w + x : -1;
     }
 #pragma unroll
-#ifdef CHAIN_ABL_NOWT  // timing ablation (dev builds only): plain stores
     for (int sb = 0; sb < NSUB; ++sb) tile_epilogue<false>(p, rows, n0 + cb + sb * 32 + m, acc[f][sb]);
-#else
-    for (int sb = 0; sb < NSUB; ++sb) tile_epilogue<CH>(p, rows, n0 + cb + sb * 32 + m, acc[f][sb]);
-#endif
     if constexpr (ENC) {
       if (p.stats_part) {  // InstanceNorm partials of the raw output (slot: spatial tile x 4 + wave)
 #pragma unroll
         for (int sb = 0; sb < NSUB; ++sb) tile_stats(p, rows, n0 + sb * 32 + m, acc[f][sb], (long)st * 4 + w);
       }
     }
-  }
-  if constexpr (CH) {  // this wave's stores have landed (write-through): count it in the tile's counter
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_fetch_add(ctl.pub + (long)st * CHAIN_PAD, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 #ifdef STAMPS
   {
@@ -786,23 +683,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
   int q = xcd_tile(blockIdx.x, gridDim.x);
   const int prob = q >= hl.tiles0 ? 1 : 0;
   q -= prob * hl.tiles0;
-  halo_body<KH, KW, BNT, PREC, ENC, false>(hl.a, prob, q, smem, ChainCtl{});
-}
-
-// The K-split form (KS = 2, 768 threads): update-block convs (no encoder features), RAFT_HALO_KS=2
-template <int KH, int KW, int BNT, int PREC>
-__global__ __launch_bounds__(768) void conv_halo_ks2_kernel(HaloLaunch hl) {
-  using C = HaloCfg<KH, KW, BNT, PREC == RAFT_PREC_F16X3 ? 128 : 64>;
-  __shared__ __attribute__((aligned(1024))) char smem[C::LDS_B + C::LDS_A];
-  int q = xcd_tile(blockIdx.x, gridDim.x);
-  const int prob = q >= hl.tiles0 ? 1 : 0;
-  q -= prob * hl.tiles0;
-  halo_body<KH, KW, BNT, PREC, false, false, 2>(hl.a, prob, q, smem, ChainCtl{});
-}
-
-bool halo_ks2_enabled() {  // (read per call)
-  const char* e = getenv("RAFT_HALO_KS");
-  return e && e[0] == '2';
+  halo_body<KH, KW, BNT, PREC, ENC>(hl.a, prob, q, smem);
 }
 
 template <int KH, int KW, int PREC>
@@ -811,15 +692,6 @@ void launch_halo_p(const HaloLaunch& l, int bn, dim3 grid, hipStream_t s) {
   if constexpr (PREC != RAFT_PREC_F16X3) {
     if (bn == 128) {  // (conv_halo_launch picks it only without stats_part / in_norm)
       hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 128, PREC>), grid, dim3(512), 0, s, l);
-      return;
-    }
-  }
-  if constexpr (PREC == RAFT_PREC_F16X3 && !(KH == 1 && KW == 1)) {
-    if (!p.stats_part && !p.in_norm && halo_ks2_enabled() && (bn == 64 || bn == 32)) {
-      if (bn == 64)
-        hipLaunchKernelGGL((conv_halo_ks2_kernel<KH, KW, 64, PREC>), grid, dim3(768), 0, s, l);
-      else
-        hipLaunchKernelGGL((conv_halo_ks2_kernel<KH, KW, 32, PREC>), grid, dim3(768), 0, s, l);
       return;
     }
   }
@@ -895,93 +767,6 @@ void launch_halo(const HaloLaunch& l, int bn, long tiles, hipStream_t s) {
 }
 
 
-// ---- chained launch: dependent stride-1 convs of one spatial size in ONE persistent launch ----
-//
-// conv_chain_kernel runs stage 0's tiles, then stage 1's, ... (a stage = one conv or an
-// independent pair) with grid-stride static schedules: work-group g (XCD-ordered) takes tiles
-// g, g + G, ... of every stage in stage order.  A tile of stage s > 0 waits (chain_wait) until
-// the 3x3 neighbourhood of its spatial tile is complete in stage s - 1 (every halo of these convs
-// is <= 2 pixels < a tile; the write-after-read hazards on buffers a stage rewrites - h, z, r*h -
-// are covered because a stage-(s-1) tile itself waited for its neighbourhood in stage s - 2,
-// and so on), and publishes its own completion per compute wave.  No tile waits for a tile of a
-// later position in any work-group's schedule, so the launch cannot deadlock while its G
-// work-groups are resident (G <= CUs, one work-group per CU); the bounded wait turns anything
-// else into a flagged error instead of a hang.  What the launch saves over one launch per conv:
-// the dependent-launch boundary, the per-launch fill / drain of the grid, and the next tile's
-// weight prologue (issued before its wait).
-constexpr int CHAIN_MAX_CONVS = 8, CHAIN_MAX_STAGES = 8;
-constexpr int CHAIN_HDR = 32;  // sync ints before the counters: [0] abort, [1] exit count
-
-struct ChainArgs {
-  HaloArgs conv[CHAIN_MAX_CONVS];
-  int first[CHAIN_MAX_STAGES];   // the stage's first conv
-  int tiles0[CHAIN_MAX_STAGES];  // tiles of that conv (the rest: the pair's second conv)
-  int items[CHAIN_MAX_STAGES];   // tiles of the stage
-  int shape[CHAIN_MAX_STAGES];   // tile body (chain_shape)
-  int target[CHAIN_MAX_STAGES];  // counter value of a complete spatial tile: 4 x the stage's N-tiles
-  int ns, spatial;
-  int* sync;
-  int* err;
-};
-static_assert(sizeof(ChainArgs) <= 4096, "chain kernel arguments");
-
-// tile bodies of a chain: (kh, kw) x N-tile
-constexpr int chain_shape(int kh, int kw, int bn) {
-  return (kh == 3 && kw == 3 ? 0 : kh == 1 && kw == 5 ? 2 : kh == 5 && kw == 1 ? 4 : -8) + (bn == 32 ? 1 : 0);
-}
-
-template <int PREC>
-__global__ __launch_bounds__(512) void conv_chain_kernel(const ChainArgs c) {
-  __shared__ __attribute__((aligned(1024))) char smem[HALO_LDS];
-  const int G = gridDim.x;
-  const int g = xcd_tile(blockIdx.x, G);
-  int* cnt = c.sync + CHAIN_HDR;
-  for (int s = 0; s < c.ns; ++s) {
-    const ChainCtl ctl{s > 0 ? cnt + (long)(s - 1) * c.spatial * CHAIN_PAD : nullptr, s > 0 ? c.target[s - 1] : 0,
-                       cnt + (long)s * c.spatial * CHAIN_PAD, c.sync, c.err};
-    const HaloArgs* as = c.conv + c.first[s];
-    for (int i = g; i < c.items[s]; i += G) {
-      const int prob = i >= c.tiles0[s] ? 1 : 0;
-      const int q = i - prob * c.tiles0[s];
-      switch (c.shape[s]) {
-        case chain_shape(3, 3, 64): halo_body<3, 3, 64, PREC, false, true>(as, prob, q, smem, ctl); break;
-        case chain_shape(3, 3, 32): halo_body<3, 3, 32, PREC, false, true>(as, prob, q, smem, ctl); break;
-        case chain_shape(1, 5, 64): halo_body<1, 5, 64, PREC, false, true>(as, prob, q, smem, ctl); break;
-        case chain_shape(1, 5, 32): halo_body<1, 5, 32, PREC, false, true>(as, prob, q, smem, ctl); break;
-        case chain_shape(5, 1, 64): halo_body<5, 1, 64, PREC, false, true>(as, prob, q, smem, ctl); break;
-        default: halo_body<5, 1, 32, PREC, false, true>(as, prob, q, smem, ctl); break;
-      }
-    }
-  }
-  // the last work-group out clears the counters for the next launch (every other work-group has
-  // finished all of its tiles: no wait reads them any more; every wave's counter adds have landed)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    int last = 0;
-    if (threadIdx.x == 0) last = __hip_atomic_fetch_add(c.sync + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
-    last = __builtin_amdgcn_readfirstlane(last);
-    if (last) {
-      for (int k = threadIdx.x; k < c.ns * c.spatial; k += 64)
-        __hip_atomic_store(cnt + (long)k * CHAIN_PAD, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (threadIdx.x < 2) __hip_atomic_store(c.sync + threadIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-int chain_grid_limit() {
-  static const int limit = [] {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 0;
-    int per = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, conv_chain_kernel<RAFT_PREC_F16X3>, 512, 0) != hipSuccess)
-      return 0;
-    return cus * (per < 1 ? 0 : 1);
-  }();
-  return limit;
-}
-
 }  // namespace
 
 #ifdef STAMPS
@@ -1002,6 +787,8 @@ bool conv_halo_norm_ok(const HaloOperands& o) {
 int conv_halo_stats_slots(const HaloOperands& o) {
   HaloArgs a;
   if (!halo_enabled() || !halo_problem(o, a)) return 0;
+  // only the ENC instantiations (1x1 and 3x3, launch_halo_p) write InstanceNorm partials
+  if (!((o.p.kh == 1 && o.p.kw == 1) || (o.p.kh == 3 && o.p.kw == 3))) return 0;
   return a.tx_n * a.ty_n * 4;
 }
 
@@ -1056,73 +843,5 @@ int conv_halo_launch_pair(const HaloOperands& o0, const HaloOperands& o1, hipStr
   return 0;
 }
 
-
-bool chain_enabled() {
-  static const bool enabled = [] {
-    const char* e = getenv("RAFT_CHAIN");
-    return !(e && e[0] == '0');
-  }();
-  return enabled;
-}
-
-int conv_halo_chain_sync_ints(int n_stages, int batch, int out_h, int out_w) {
-  return CHAIN_HDR + n_stages * batch * cdiv(out_h, HTH) * cdiv(out_w, HTW) * CHAIN_PAD;
-}
-
-// Dependent stages (one conv, or an independent pair, each) as one conv_chain_kernel launch;
-// returns 1 without launching when the stages do not qualify (the caller runs them in order).
-int conv_halo_launch_chain(const HaloOperands* ops, const int* nconv, int n_stages, int* sync, int* err,
-                           hipStream_t s) {
-  if (!halo_enabled() || !chain_enabled() || n_stages < 1 || n_stages > CHAIN_MAX_STAGES) return 1;
-  ChainArgs c;
-  memset(&c, 0, sizeof(c));
-  int ci = 0, maxitems = 0;
-  const raft_conv2d_params& p00 = ops[0].p;
-  for (int st = 0; st < n_stages; ++st) {
-    const int k = nconv[st];
-    if (k < 1 || k > 2 || ci + k > CHAIN_MAX_CONVS) return 1;
-    long spatial = 0, nb = 0;
-    for (int j = 0; j < k; ++j) {
-      const HaloOperands& o = ops[ci + j];
-      HaloArgs& a = c.conv[ci + j];
-      if (!halo_problem(o, a)) return 1;
-      const raft_conv2d_params& p = o.p;
-      if (p.precision != RAFT_PREC_F16X3 || p.stats_part || p.in_norm) return 1;
-      if (p.kh == 1 && p.kw == 1) return 1;  // (1x1: the fp32-patch path, not chained)
-      if (p.batch != p00.batch || p.out_h != p00.out_h || p.out_w != p00.out_w) return 1;
-      if (j == 1 && (p.kh != ops[ci].p.kh || p.kw != ops[ci].p.kw)) return 1;
-      spatial = halo_spatial(a);
-      nb += o.n_pad / 64;
-    }
-    // the N tile of conv_halo_launch / _pair
-    const int bn = spatial * nb > 128 ? 64 : 32;
-    int items = 0, ncol = 0;
-    for (int j = 0; j < k; ++j) {
-      const HaloOperands& o = ops[ci + j];
-      if (o.n_pad % bn) return 1;
-      c.conv[ci + j].gn = o.n_pad / bn;
-      ncol += c.conv[ci + j].gn;
-      if (j == 0) c.tiles0[st] = (int)(spatial * c.conv[ci].gn);
-      items += (int)(spatial * c.conv[ci + j].gn);
-    }
-    c.first[st] = ci;
-    c.items[st] = items;
-    c.shape[st] = chain_shape(ops[ci].p.kh, ops[ci].p.kw, bn);
-    if (c.shape[st] < 0) return 1;
-    c.target[st] = 4 * ncol;
-    c.spatial = (int)spatial;
-    if (items > maxitems) maxitems = items;
-    ci += k;
-  }
-  const int lim = chain_grid_limit();
-  if (lim <= 0) return 1;
-  if (!sync) return 0;  // (raft_conv2d_chain_covered: the stages qualify)
-  c.ns = n_stages;
-  c.sync = sync;
-  c.err = err;
-  const int G = maxitems < lim ? maxitems : lim;
-  hipLaunchKernelGGL((conv_chain_kernel<RAFT_PREC_F16X3>), dim3((unsigned)G), dim3(512), 0, s, c);
-  return 0;
-}
 
 }  // namespace raft

@@ -405,181 +405,6 @@ __global__ __launch_bounds__(512, 2) void corr_build2_kernel(CorrBuildArgs a) {
   }
 }
 
-// The f16 split of both feature maps, once per build (the input of corr_build3_kernel): row p of
-// the split holds, per 32-channel K-step, the 32 hi halves then the 32 lo halves (128 B; zeros past
-// C), hi = f16(x), lo = f16(x - hi): the values corr_build2_kernel's staging computes per tile.
-__global__ void corr_split_kernel(const float* __restrict__ f, int ld, int C, long n_rows, int nk,
-                                  h8* __restrict__ out) {
-  const long total = n_rows * nk * 4;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const long row = i / (nk * 4);
-    const int rem = (int)(i - row * nk * 4), kc = rem >> 2, g = rem & 3;
-    const int ch = kc * CB_BK + g * 8;
-    const float* src = f + row * ld + ch;
-    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-    const f32x4 v0 = ch < C ? *reinterpret_cast<const f32x4*>(src) : z;
-    const f32x4 v1 = ch + 4 < C ? *reinterpret_cast<const f32x4*>(src + 4) : z;
-    h8 hi, lo;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float v = e < 4 ? v0[e] : v1[e - 4];
-      const _Float16 hh = (_Float16)v;
-      hi[e] = hh;
-      lo[e] = (_Float16)(v - (float)hh);
-    }
-    h8* dst = out + row * nk * 8 + kc * 8;
-    dst[g] = hi;
-    dst[4 + g] = lo;
-  }
-}
-
-// K2 from the pre-split maps (the forward's corr build when the caller passes a workspace): the
-// tiles, products, summation order and epilogue of corr_build2_kernel (bit-identical pyramid), but
-// the K-steps' 128-B split rows move global -> LDS by LDS-DMA through a ring of CB3_NS stages
-// (3 K-steps in flight per work-group, no staging registers, no split / ds_write pass): in
-// corr_build2 each K-step's loads had one K-step of MFMA work to land and the staging itself
-// (convert + LDS writes) held the MFMA waves (profiles/r03_corr_build_ablation.txt).  A stage's
-// rows are 128 B with the 16-B chunk c of row r at slot c ^ ((r >> 1) & 7), which keeps the MFMA
-// waves' ds_read_b128 conflict-free without padding (the DMA writes 1 KiB runs).  One work-group
-// per CU (128 KiB of LDS); the epilogue tile (stride 132: conflict-free 16-B reads) reuses the ring.
-// NS = 2 (the one launched): two work-groups per CU (64 KiB each), one K-step in flight, the
-// epilogue tile with stride 128 and its 4-column groups XOR-swizzled by row.  NS = 4 (one
-// work-group per CU, three K-steps in flight) measured 10 % slower than corr_build2: nothing then
-// overlaps a tile's epilogue stores.
-constexpr int CB3_STAGE = 2 * CB2_BM * 128;
-
-template <int NS>
-__global__ __launch_bounds__(512, NS == 2 ? 2 : 1) void corr_build3_kernel(CorrBuildArgs a, const void* split,
-                                                                          unsigned split_bytes, int nk) {
-  constexpr int CB3_NS = NS, CB3_TLD = NS == 2 ? 128 : 132;
-  static_assert(CB3_NS * CB3_STAGE >= CB2_BM * CB3_TLD * 4, "the epilogue tile fits the ring");
-  auto tcol = [](int row, int n) { return NS == 2 ? n ^ ((row & 3) << 2) : n; };
-  __shared__ __attribute__((aligned(16))) char smem[CB3_NS * CB3_STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave & 3, wn = wave >> 2;  // 32 query rows x 64 block pixels per wave
-  int b, mi, ni;
-  cb_tile(a, b, mi, ni);
-  const int m0 = mi * CB2_BM;
-  const int nbx = (a.W + 15) / 16;
-  const int by = ni / nbx, bx = ni - (ni / nbx) * nbx;
-  const unsigned rowb = (unsigned)nk * 128u;
-  const __amdgpu_buffer_rsrc_t rs = make_rsrc(split, split_bytes);
-  // DMA rows: wave w moves rows 32w .. 32w + 31 of the stage (waves 0-3: fmap1 rows of the M tile,
-  // 4-7: fmap2 pixels of the 8 x 16 block), 8 rows x 128 B per instruction
-  unsigned voff[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int rr = ((wave * 4 + j) * 8 + (lane >> 3)) & 127;
-    const unsigned c = (unsigned)((lane & 7) ^ ((rr >> 1) & 7));
-    bool ok;
-    long pix;
-    if (wave < 4) {
-      ok = m0 + rr < a.P;
-      pix = (long)b * a.P + m0 + rr;
-    } else {
-      const int h2 = by * 8 + (rr >> 4), w2 = bx * 16 + (rr & 15);
-      ok = h2 < a.H && w2 < a.W;
-      pix = (long)(a.B + b) * a.P + h2 * a.W + w2;
-    }
-    voff[j] = ok ? (unsigned)pix * rowb + c * 16u : OFF_INVALID;
-  }
-  auto issue = [&](int kc) {
-    char* st = smem + (kc & (CB3_NS - 1)) * CB3_STAGE + wave * 4096;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) dma16(rs, st + j * 1024, voff[j], (unsigned)kc * 128u);
-  };
-  const int pre = min(nk, CB3_NS - 1);
-  for (int k = 0; k < pre; ++k) issue(k);
-  const int ra = wm * 32 + (lane & 31), ka = (ra >> 1) & 7;  // A row of this lane and its swizzle key
-  f32x16 acc[2] = {}, accl[2] = {};  // hi*hi | lo*hi + hi*lo
-  for (int kc = 0; kc < nk; ++kc) {
-    // this wave's DMAs of stage kc have landed once at most the later stages' are outstanding
-    const int later = NS == 2 ? 0 : min(nk - 1 - kc, CB3_NS - 2);
-    if (later >= 2)
-      wait_vm<8>();
-    else if (later == 1)
-      wait_vm<4>();
-    else
-      wait_vm<0>();
-    __syncthreads();  // every wave's rows of stage kc landed; stage kc - 1 fully read
-    if (kc + CB3_NS - 1 < nk) issue(kc + CB3_NS - 1);  // into stage kc - 1's buffer
-    const char* S = smem + (kc & (CB3_NS - 1)) * CB3_STAGE;
-#pragma unroll
-    for (int qq = 0; qq < 2; ++qq) {
-      const int c = qq * 2 + (lane >> 5);
-      const char* Ar = S + ra * 128;
-      const h8 xh = *reinterpret_cast<const h8*>(Ar + ((c ^ ka) << 4));
-      const h8 xl = *reinterpret_cast<const h8*>(Ar + (((c + 4) ^ ka) << 4));
-#pragma unroll
-      for (int sb = 0; sb < 2; ++sb) {
-        const int rb = wn * 64 + sb * 32 + (lane & 31), kb = (rb >> 1) & 7;
-        const char* Br = S + CB2_BM * 128 + rb * 128;
-        const h8 yh = *reinterpret_cast<const h8*>(Br + ((c ^ kb) << 4));
-        const h8 yl = *reinterpret_cast<const h8*>(Br + (((c + 4) ^ kb) << 4));
-        acc[sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, yh, acc[sb], 0, 0, 0);
-        accl[sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, yh, accl[sb], 0, 0, 0);
-        accl[sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, yl, accl[sb], 0, 0, 0);
-      }
-    }
-  }
-  __syncthreads();  // the ring is free (the last stage read, no DMA outstanding)
-  float* T = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb) {
-    const int n = wn * 64 + sb * 32 + (lane & 31);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      T[row * CB3_TLD + tcol(row, n)] = (acc[sb][r] + accl[sb][r]) / a.sqrt_c;
-    }
-  }
-  __syncthreads();
-  for (int idx = tid; idx < CB2_BM * 32; idx += 512) {
-    const int row = idx >> 5, o = (idx & 31) * 4;
-    const int p1 = m0 + row;
-    const int ti = o >> 6, tj = (o >> 4) & 3, e = o & 15;
-    const int ty = 2 * by + ti, tx = 4 * bx + tj;
-    if (p1 < a.P && ty < a.l0.th && tx < a.l0.tw) {
-      const f32x4 v =
-          *reinterpret_cast<const f32x4*>(T + row * CB3_TLD + tcol(row, (ti * 4 + (e >> 2)) * 16 + tj * 4));
-      f32x4* dst = reinterpret_cast<f32x4*>(a.pyr + a.l0.off + ((long)b * a.P + p1) * a.l0.mapsz +
-                                            ((long)ty * a.l0.tw + tx) * 16 + e);
-      if (a.nt)
-        __builtin_nontemporal_store(v, dst);
-      else
-        *dst = v;
-    }
-  }
-  if (a.has_l1 && by < a.l1.th) {
-    for (int idx = tid; idx < CB2_BM * 8; idx += 512) {
-      const int row = idx >> 3, o = (idx & 7) * 4;
-      const int p1 = m0 + row;
-      const int tj = o >> 4, e = o & 15;
-      const int tx1 = 2 * bx + tj;
-      if (p1 >= a.P || tx1 >= a.l1.tw) continue;
-      const int yy = e >> 2;
-      f32x4 v4;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int xx = tj * 4 + c;
-        float v = 0.f;
-        if (by * 4 + yy < a.l1.h && bx * 8 + xx < a.l1.w) {
-          const float* t = T + row * CB3_TLD + tcol(row, (2 * yy) * 16 + 2 * xx);  // the swizzle keeps n, n + 1
-          const float2 u0 = *reinterpret_cast<const float2*>(t), u1 = *reinterpret_cast<const float2*>(t + 16);
-          v = (((u0.x + u0.y) + u1.x) + u1.y) / 4.0f;  // avg_pool2d window order
-        }
-        v4[c] = v;
-      }
-      f32x4* dst = reinterpret_cast<f32x4*>(a.pyr + a.l1.off + ((long)b * a.P + p1) * a.l1.mapsz +
-                                            ((long)by * a.l1.tw + tx1) * 16 + e);
-      if (a.nt)
-        __builtin_nontemporal_store(v4, dst);
-      else
-        *dst = v4;
-    }
-  }
-}
-
 // Level l -> l+1 2x2 average pool (floor), tiled -> tiled, zeros in the padding.
 __global__ void pool2_tiled_kernel(const float* pyr, float* out_base, long n_maps, Level src,
                                    Level dst) {
@@ -1135,33 +960,9 @@ extern "C" int raft_corr_build(const float* fmap1, const float* fmap2, int ld, i
   return raft_corr_build_prec(fmap1, fmap2, ld, B, H, W, C, L, sqrt_c, RAFT_PREC_FP32, pyramid, stream);
 }
 
-extern "C" size_t raft_corr_build_ws_bytes(int B, int H, int W, int C) {
-  if (B <= 0 || H <= 0 || W <= 0 || C <= 0) return 0;
-  return (size_t)2 * B * H * W * (size_t)cdiv(C, CB_BK) * 128;
-}
-
-namespace raft {
-namespace {
-int corr_build_impl(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C, int L, float sqrt_c,
-                    int precision, void* ws, size_t ws_bytes, float* pyramid, raft_stream_t stream);
-}
-}  // namespace raft
-
 extern "C" int raft_corr_build_prec(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C, int L,
                                     float sqrt_c, int precision, float* pyramid, raft_stream_t stream) {
-  return corr_build_impl(fmap1, fmap2, ld, B, H, W, C, L, sqrt_c, precision, nullptr, 0, pyramid, stream);
-}
-
-extern "C" int raft_corr_build_ws(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C, int L,
-                                  float sqrt_c, int precision, void* ws, size_t ws_bytes, float* pyramid,
-                                  raft_stream_t stream) {
-  return corr_build_impl(fmap1, fmap2, ld, B, H, W, C, L, sqrt_c, precision, ws, ws_bytes, pyramid, stream);
-}
-
-namespace raft {
-namespace {
-int corr_build_impl(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C, int L, float sqrt_c,
-                    int precision, void* ws, size_t ws_bytes, float* pyramid, raft_stream_t stream) {
+  using namespace raft;
   RAFT_REQUIRE(precision == RAFT_PREC_FP32 || precision == RAFT_PREC_F16X3,
                "raft_corr_build_prec: precision must be RAFT_PREC_FP32 or RAFT_PREC_F16X3 (got %d)", precision);
   RAFT_REQUIRE(fmap1 && fmap2 && pyramid, "raft_corr_build: null pointer");
@@ -1217,30 +1018,8 @@ int corr_build_impl(const float* fmap1, const float* fmap2, int ld, int B, int H
         a.xcd = xc != 0;
       }
     }
-    const size_t need = raft_corr_build_ws_bytes(B, H, W, C);
-    RAFT_REQUIRE(!ws || ws_bytes >= need, "raft_corr_build_ws: workspace of %zu bytes, %zu needed", ws_bytes, need);
-    RAFT_REQUIRE(!ws || ((uintptr_t)ws & 15) == 0, "raft_corr_build_ws: workspace must be 16-byte aligned");
-    // opt-in (RAFT_CORR_BUILD3=1): alone 5 % faster at config 5's map, but in the forward the build
-    // runs beside the context network and the forward did not move
-    const char* e3 = getenv("RAFT_CORR_BUILD3");
-    const bool v3 = e3 && e3[0] == '1';
     const dim3 grid((unsigned)((long)B * a.mt * a.ntl));
-    if (ws && v3 && need < 0x80000000ull) {  // 32-bit buffer offsets below OFF_INVALID
-      const int nk = cdiv(C, CB_BK);
-      // fmap1 then fmap2 rows: the split of both maps in one pass when they are one array
-      if (fmap2 == fmap1 + (long)B * P * ld) {
-        hipLaunchKernelGGL(corr_split_kernel, dim3(grid_for(2L * B * P * nk * 4)), dim3(256), 0, s, fmap1, ld, C,
-                           2L * B * P, nk, reinterpret_cast<h8*>(ws));
-      } else {
-        hipLaunchKernelGGL(corr_split_kernel, dim3(grid_for((long)B * P * nk * 4)), dim3(256), 0, s, fmap1, ld, C,
-                           (long)B * P, nk, reinterpret_cast<h8*>(ws));
-        hipLaunchKernelGGL(corr_split_kernel, dim3(grid_for((long)B * P * nk * 4)), dim3(256), 0, s, fmap2, ld, C,
-                           (long)B * P, nk, reinterpret_cast<h8*>(ws) + (long)B * P * nk * 8);
-      }
-      hipLaunchKernelGGL(corr_build3_kernel<2>, grid, dim3(512), 0, s, a, (const void*)ws, (unsigned)need, nk);
-    } else {
-      hipLaunchKernelGGL(corr_build2_kernel, grid, dim3(512), 0, s, a);
-    }
+    hipLaunchKernelGGL(corr_build2_kernel, grid, dim3(512), 0, s, a);
   } else {
     dim3 grid(cdiv((int)P, CB_BM), cdiv(H, 8) * a.nbx, B);
     hipLaunchKernelGGL(corr_build_kernel<true>, grid, dim3(256), 0, s, a);
@@ -1256,8 +1035,6 @@ int corr_build_impl(const float* fmap1, const float* fmap2, int ld, int B, int H
   }
   return 0;
 }
-}  // namespace
-}  // namespace raft
 
 extern "C" int raft_corr_pyramid_level(const float* pyramid, int B, int H, int W, int L, int level, float* out,
                                        raft_stream_t stream) {

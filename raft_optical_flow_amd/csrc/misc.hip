@@ -461,6 +461,18 @@ __global__ void norm_apply_affine_kernel(const float* x, int ld, const float* st
 
 bool aligned16(const void* q) { return ((uintptr_t)q & 15) == 0; }
 
+// Debug: every work-group takes a CU's whole LDS (160 KiB) and fills it with all-ones words (a NaN
+// as one fp32 or two f16 / bf16 values), so the next kernel on that CU starts with NaN wherever it
+// reads LDS it did not write.  Only the value of LDS changes: no global memory is touched.
+constexpr int LDS_FILL_BYTES = 160 * 1024;
+__global__ __launch_bounds__(1024) void fill_lds_nan_kernel() {
+  extern __shared__ __attribute__((aligned(16))) unsigned lds_fill[];
+  const unsigned ones = 0xffffffffu;
+  for (int i = threadIdx.x; i < LDS_FILL_BYTES / 16; i += blockDim.x)
+    reinterpret_cast<uint4*>(lds_fill)[i] = make_uint4(ones, ones, ones, ones);
+  __syncthreads();
+}
+
 }  // namespace
 }  // namespace raft
 
@@ -607,4 +619,19 @@ extern "C" int raft_norm_apply_affine(const float* x, int ld, const float* stats
   hipLaunchKernelGGL(norm_apply_affine_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, ld, stats, gamma,
                      beta, resid, resid_ld, resid_stats, resid_gamma, resid_beta, relu_mode, out, out_ld, B, HW, C);
   return check_launch("raft_norm_apply_affine");
+}
+
+extern "C" int raft_debug_fill_lds_nan(raft_stream_t stream) {
+  int dev = 0, cus = 0;
+  RAFT_REQUIRE(hipGetDevice(&dev) == hipSuccess &&
+               hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0,
+               "raft_debug_fill_lds_nan: no device");
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(fill_lds_nan_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_FILL_BYTES) == hipSuccess;
+  }();
+  RAFT_REQUIRE(attr, "raft_debug_fill_lds_nan: cannot request %d B of LDS", LDS_FILL_BYTES);
+  // several work-groups per CU, one resident at a time (the LDS), so every CU runs at least one
+  hipLaunchKernelGGL(fill_lds_nan_kernel, dim3((unsigned)(4 * cus)), dim3(1024), LDS_FILL_BYTES, as_stream(stream));
+  return check_launch("raft_debug_fill_lds_nan");
 }

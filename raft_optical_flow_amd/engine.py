@@ -436,10 +436,6 @@ class UpdateBuffers:
         self.rh = A.rows(P, hd)
         self.ctx = [A.rows(P, 3 * hd) for _ in pu.gru]   # z | r | q context terms per half-step
         self.coords = A.rows(P, 2)
-        # raft_conv2d_chain's completion counters (one launch at a time on the main stream) and
-        # its timeout flag where no range flag takes it
-        self.chain_sync = None  # (allocated by _Stages.launch: its size depends on the image)
-        self.chain_err = torch.zeros(1, dtype=torch.int32, device=A.device)
 
     # channel slots of HX
     def h(self, pu):
@@ -521,43 +517,6 @@ def frag_weight(pc) -> torch.Tensor:
     return out
 
 
-CHAIN_MAX_STAGES = 8
-
-
-def chain_enabled(pu: PackedUpdate) -> bool:
-    """Whether RAFT-full's update convs from convc2|convf2 to the flow head's conv1 run as one
-    raft_conv2d_chain launch (RAFT_CHAIN=1; off by default: measured neutral to slightly slower than one
-    launch per conv at B=1 and B=8)."""
-    return not pu.small and os.environ.get("RAFT_CHAIN", "0") == "1" and os.environ.get("RAFT_CONV_PAIR", "1") != "0"
-
-
-class _Stages:
-    """Collects conv stages for one raft_conv2d_chain launch (plan_update)."""
-
-    def __init__(self):
-        self.stages = []
-
-    def add(self, p0, p1=None):
-        self.stages.append((p0, p1))
-
-    def launch(self, ub: UpdateBuffers) -> Launch:
-        n = len(self.stages)
-        assert 1 <= n <= CHAIN_MAX_STAGES
-        arr = (ctypes.POINTER(_lib.ConvParams) * (2 * n))()
-        for i, (p0, p1) in enumerate(self.stages):
-            arr[2 * i] = ctypes.pointer(p0)
-            if p1 is not None:
-                arr[2 * i + 1] = ctypes.pointer(p1)
-        flag = _GUARD["flag"]
-        err = flag.data_ptr() if flag is not None else ub.chain_err.data_ptr()
-        if ub.chain_sync is None:
-            p = self.stages[0][0]
-            nint = int(_lib.load().raft_conv2d_chain_sync_ints(CHAIN_MAX_STAGES, p.batch, p.out_h, p.out_w))
-            ub.chain_sync = torch.zeros(nint, dtype=torch.int32, device=ub.chain_err.device)
-        keep = (arr, [p for st in self.stages for p in st if p is not None])
-        return Launch("raft_conv2d_chain", arr, n, ub.chain_sync.data_ptr(), err, keep=keep)
-
-
 def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool, convf1_done: bool = False,
                 convc1_done: bool = False, last: bool = True):
     """One BasicUpdateBlock / SmallUpdateBlock step (core/update.py:297-325 / :250-263)
@@ -574,15 +533,10 @@ def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool
     # RAFT-small (different conv shapes per branch): side stream unless RAFT_FLOW_SIDE=0.
     pair = not pu.small and os.environ.get("RAFT_CONV_PAIR", "1") != "0"
     side = not pair and os.environ.get("RAFT_FLOW_SIDE", "1") != "0"
-    # RAFT-full: convc2|convf2 .. the flow head's conv1 as one chained launch (raft_conv2d_chain)
-    chain = _Stages() if chain_enabled(pu) else None
 
     def conv(pc, src, out, **kw):
         kw.setdefault("range_flag", _GUARD["flag"])
-        if chain is not None:
-            chain.add(conv_params(pc, src, B, h, w, out, **kw))
-        else:
-            L.append(conv_launch(conv_params(pc, src, B, h, w, out, **kw)))
+        L.append(conv_launch(conv_params(pc, src, B, h, w, out, **kw)))
     if side:
         L.append(K.FORK)
     if pu.small:
@@ -598,10 +552,7 @@ def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool
                          range_flag=_GUARD["flag"])
         f2 = conv_params(pu.convf2, Rows(ub.flo1), B, h, w, cf.sub(192, 64), epilogue=_lib.EPI_RELU,
                          range_flag=_GUARD["flag"])
-        if chain is not None:
-            chain.add(c2, f2)
-        else:
-            L.append(K.conv_pair_launch(c2, f2))
+        L.append(K.conv_pair_launch(c2, f2))
     else:
         _conv(L, pu.convf1, flow, B, h, w, Rows(ub.flo1), epilogue=_lib.EPI_RELU, side=side)
         _conv(L, pu.convf2, Rows(ub.flo1), B, h, w, cf.sub(192, 64), epilogue=_lib.EPI_RELU, side=side)
@@ -629,8 +580,6 @@ def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool
             conv(pu.fh1_mask, hrows, fh, epilogue=_lib.EPI_RELU)
         else:  # (feeds only the fp32 flow-head conv2: no range guard)
             conv(pu.fh1, hrows, fh.sub(0, 256), epilogue=_lib.EPI_RELU, range_flag=None)
-        if chain is not None:
-            L.append(chain.launch(ub))
         _conv(L, pu.fh2, fh.sub(0, 256), B, h, w, coords, epilogue=_lib.EPI_ADD_TO_OUT)
         if with_mask:
             # the mask feeds only the fp32 softmax of the upsampling: no range guard
@@ -702,13 +651,8 @@ class RaftPlan:
             # the correlation GEMM follows the conv arithmetic: exact f32 MFMA in "fp32"
             # mode, the fp32-accurate f16 split otherwise (raft_hip.h)
             cprec = _lib.PREC_FP32 if pk.precision == _lib.PREC_FP32 else _lib.PREC_F16X3
-            # RAFT_CORR_BUILD3=1: the f16 split of both maps made once per build and the LDS-DMA
-            # GEMM (raft_corr_build_ws; bit-identical, not faster in the forward)
-            v3 = cprec == _lib.PREC_F16X3 and os.environ.get("RAFT_CORR_BUILD3", "0") == "1"
-            wsb = int(_lib.load().raft_corr_build_ws_bytes(B, h, w, C)) if v3 else 0
-            ws = A.flat((wsb + 3) // 4) if wsb else None
-            L.append(Launch("raft_corr_build_ws", fmap1.data_ptr(), fmap2.data_ptr(), C, B, h, w, C, lv, div,
-                            cprec, ws.data_ptr() if ws is not None else None, wsb, self.pyramid.data_ptr()))
+            L.append(Launch("raft_corr_build_prec", fmap1.data_ptr(), fmap2.data_ptr(), C, B, h, w, C, lv, div,
+                            cprec, self.pyramid.data_ptr()))
         else:
             # AlternateCorrBlock pools num_levels times (core/corr.py:157-161); the
             # last level is never used, but its existence is the reference's size check.

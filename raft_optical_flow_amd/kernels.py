@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+from collections import OrderedDict
 from dataclasses import dataclass
 
 import torch
@@ -313,15 +314,22 @@ def cached_pack(mod, device, build):
     return hit[1]
 
 
-def cached_plan(mod, packed, key, build):
+def cached_plan(mod, packed, key, build, max_streams=4):
     """A block-level forward's device buffers and pre-built launch list for one input shape, kept on
-    the module (the last shape only) and rebuilt when the packed weights object (cached_pack's,
+    the module (the last shape per stream) and rebuilt when the packed weights object (cached_pack's,
     compared by identity) or the key (shape, device) changes: repeated calls allocate nothing and
-    only copy their inputs in.  Calls on one module are stream-ordered (the buffers are shared)."""
-    hit = mod.__dict__.get("_hip_plan")
+    only copy their inputs in.  The cache is per current stream: calls on one stream are ordered, so
+    they may share buffers; a call on another stream (or inside another stream's graph capture) gets
+    buffers of its own, so calls from two streams never race on one set of buffers."""
+    sid = torch.cuda.current_stream().cuda_stream if torch.cuda.is_available() else 0
+    plans = mod.__dict__.setdefault("_hip_plan", OrderedDict())
+    hit = plans.get(sid)
     if hit is None or hit[0] is not packed or hit[1] != key:
         hit = (packed, key, build())
-        mod.__dict__["_hip_plan"] = hit
+        plans[sid] = hit
+        while len(plans) > max_streams:
+            plans.popitem(last=False)
+    plans.move_to_end(sid)
     return hit[2]
 
 

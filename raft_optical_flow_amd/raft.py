@@ -24,25 +24,29 @@ f16x3 range guard: the default fp32-accurate split arithmetic holds only while e
 conv input stays below 65504 in magnitude (include/raft_hip.h).  The convs and lookups
 whose outputs feed split convs raise a device flag above 2^15.  `model.range_guard`
 (env RAFT_RANGE_GUARD) chooses what happens then:
-  "fallback" (default)  the check is deferred so forwards queue back to back with no host
-                        sync: the flag is copied to pinned host memory behind the forward
-                        and read once that copy has completed (at a later forward() call, or
-                        at model.check_range_guard(), which waits).  A raised flag warns and
-                        re-runs that forward on exact f32 MFMA INTO the tensors it returned,
-                        so they hold the exact result once check_range_guard() returns
-                        (a reader before that point may have seen the inexact values; the
-                        re-run needs the input tensors unmodified in place, else it warns
-                        that it cannot correct them);
-  "sync"                forward() waits for its flag and returns the f32 re-run's result
-                        (the round-2 behaviour: one host sync per forward);
-  "raise"               as "sync", but raises FloatingPointError;
+  "fallback" (default)  forward() waits for its flag (one host sync per forward) and, when it
+                        is raised, warns and returns the result of a re-run on exact f32 MFMA:
+                        what forward() returns is always the exact-range result ("sync" is
+                        the same mode);
+  "deferred"            opt-in, for callers that queue forwards back to back: the flag is
+                        copied to pinned host memory behind the forward and read once that
+                        copy has completed (at a later forward() call, at
+                        model.check_range_guard(), which waits, or at interpreter exit).  A
+                        raised flag warns and re-runs that forward on exact f32 MFMA INTO the
+                        tensors it returned; values read from them before that point were
+                        the inexact ones (the warning says so);
+  "raise"               as "fallback", but raises FloatingPointError;
   "off"                 no device checks at all.
 """
 from __future__ import annotations
 
+import atexit
 import os
 import warnings
+import weakref
 from collections import OrderedDict, deque
+
+import threading
 
 import torch
 import torch.nn as nn
@@ -60,6 +64,8 @@ autocast = torch.amp.autocast
 # default conv arithmetic of an fp32 model (include/raft_hip.h, RAFT_PREC_*):
 # "f16x3" = fp32-accurate split-f16 MFMA, "fp32" = f32 MFMA
 DEFAULT_PRECISION = "f16x3"
+
+_CACHE_LOCK = threading.Lock()  # creation of per-device cache entries (DataParallel threads)
 
 
 class RAFT(nn.Module):
@@ -97,9 +103,39 @@ class RAFT(nn.Module):
         # conv arithmetic: "fp32" | "f16x3" | "f16"; args.mixed_precision (the
         # reference's fp16 autocast, core/raft.py:156) selects "f16"
         self.conv_precision = getattr(args, "conv_precision", None)
-        self._packed = {}           # precision -> (weights key, PackedRaft)
-        self._plans = OrderedDict()
-        self._pending = deque()     # deferred range-guard checks ("fallback"), oldest first
+        # packed weights and plans per device: {str(device): {"packed": {precision: (weights key,
+        # PackedRaft)}, "plans": OrderedDict}}; nn.DataParallel replicas share their source's
+        # (_replicate_for_data_parallel), each replica touching only its own device's entry
+        self._caches = {}
+        self._pending = deque()     # deferred range-guard checks ("deferred"), oldest first
+
+    def _replicate_for_data_parallel(self):
+        """nn.DataParallel (the reference's multi-GPU API, train.py:172, evaluate.py:179) re-replicates
+        the module on every forward by shallow-copying __dict__.  A replica keeps the per-device caches
+        of its SOURCE module (so packing and graph capture happen once per device, not per forward;
+        the weights key is the source's, whose values every replica copies) and a range-guard queue of
+        its own; replicas on different devices never touch the same cache entry."""
+        replica = super()._replicate_for_data_parallel()
+        replica.__dict__["_dp_source"] = self.__dict__.get("_dp_source") or self
+        replica.__dict__["_pending"] = deque()
+        return replica
+
+    def _source(self):
+        return self.__dict__.get("_dp_source") or self
+
+    def _dev_cache(self, device):
+        caches = self._source().__dict__["_caches"]
+        d = str(torch.device(device))
+        c = caches.get(d)
+        if c is None:
+            with _CACHE_LOCK:
+                c = caches.setdefault(d, {"packed": {}, "plans": OrderedDict()})
+        return c
+
+    @property
+    def _plans(self):
+        """The plans of the device this module's parameters are on (inspection / tests)."""
+        return self._dev_cache(next(self.parameters()).device)["plans"]
 
     def freeze_bn(self):
         for m in self.modules():
@@ -140,16 +176,20 @@ class RAFT(nn.Module):
     def packed(self, device, prec=None):
         from . import _lib
         prec = prec or self.resolved_precision()
-        key = (self._weights_key(), str(device))
-        got = self._packed.get(prec)
+        # (a DataParallel replica's parameters are this forward's copies of its source's: the
+        # source's key names the values)
+        key = (self._source()._weights_key(), str(device))
+        cache = self._dev_cache(device)
+        packs = cache["packed"]
+        got = packs.get(prec)
         if got is None or got[0] != key:
-            if got is not None or any(k != key for k, _ in self._packed.values()):
-                # new weights (or device): every packed form and plan is stale
-                self._packed.clear()
-                self.release_plans()
+            if got is not None or any(k != key for k, _ in packs.values()):
+                # new weights: every packed form and plan of this device is stale
+                packs.clear()
+                self._release(cache["plans"])
             with torch.no_grad():
                 got = (key, PackedRaft(self, device, _lib.PRECISIONS[prec]))
-            self._packed[prec] = got
+            packs[prec] = got
         return got[1]
 
     def plan(self, batch, height, width, iters, test_mode=True, flow_init=False, device=None, prec=None):
@@ -160,28 +200,33 @@ class RAFT(nn.Module):
         knobs = (os.environ.get("RAFT_CTX_SIDE", "1"), os.environ.get("RAFT_FLOW_SIDE", "1"),
                  os.environ.get("RAFT_CONV_PAIR", "1"), os.environ.get("RAFT_FUSE_CONVF1", "1"),
                  os.environ.get("RAFT_FUSE_CONVC1", "1"), os.environ.get("RAFT_EPI_STATS", "1"),
-                 os.environ.get("RAFT_IN_NORM", "1"), os.environ.get("RAFT_CHAIN", "0"), os.environ.get("RAFT_RESIDENT", "0"),
-                 os.environ.get("RAFT_HALO_KS", "1"), os.environ.get("RAFT_CORR_BUILD3", "0"))
+                 os.environ.get("RAFT_IN_NORM", "1"))
         guard = self.range_guard != "off"  # "off": no device-side checks either
         key = (batch, height, width, iters, bool(test_mode), bool(self.args.alternate_corr), bool(flow_init), prec,
                knobs, guard)
-        pl = self._plans.get(key)
+        plans = self._dev_cache(device)["plans"]
+        pl = plans.get(key)
         if pl is None:
-            while len(self._plans) >= max(1, self.max_plans):
-                self._plans.popitem(last=False)[1].release()
+            while len(plans) >= max(1, self.max_plans):
+                plans.popitem(last=False)[1].release()
             pl = RaftPlan(pk, batch, height, width, iters, test_mode=test_mode,
                           alternate=bool(self.args.alternate_corr), flow_init=flow_init, device=device,
                           range_guard=guard)
-            self._plans[key] = pl
+            plans[key] = pl
         else:
-            self._plans.move_to_end(key)
+            plans.move_to_end(key)
         return pl
 
+    @staticmethod
+    def _release(plans, keep=None):
+        for k in list(plans):
+            if plans[k] is not keep:
+                plans.pop(k).release()
+
     def release_plans(self, keep=None):
-        """Free the cached plans' device memory and graphs (all but `keep`)."""
-        for k in list(self._plans):
-            if self._plans[k] is not keep:
-                self._plans.pop(k).release()
+        """Free the cached plans' device memory and graphs (all but `keep`), on every device."""
+        for cache in list(self._source().__dict__["_caches"].values()):
+            self._release(cache["plans"], keep)
 
     # -- deferred range guard ------------------------------------------------
     _MAX_PENDING = 2  # forwards whose flag may be unread: the third waits for the oldest
@@ -200,8 +245,9 @@ class RAFT(nn.Module):
                 self._guard_fallback(rec)
 
     def _guard_fallback(self, rec):
-        msg = ("f16x3 range guard: an activation exceeded 2^15 in magnitude, outside the exact range "
-               "of the split-f16 conv arithmetic")
+        msg = ("f16x3 range guard (deferred): an activation of an earlier forward exceeded 2^15 in "
+               "magnitude, outside the exact range of the split-f16 conv arithmetic; values read from its "
+               "outputs before this point were inexact")
         ins = [x for x in rec["inputs"] if x is not None]
         if any(x._version != v for x, v in zip(ins, rec["versions"])):
             warnings.warn(msg + "; the inputs of that forward were modified in place since, so its outputs "
@@ -236,6 +282,8 @@ class RAFT(nn.Module):
         pl = self.plan(b, H, W, iters, test_mode, flow_init is not None, image1.device, prec=_prec)
         pl.set_inputs(image1, image2, flow_init)
         mode = self.range_guard
+        if mode == "deferred" and self.__dict__.get("_is_replica", False):
+            mode = "fallback"  # a DataParallel replica lives for one forward: nothing can be deferred
         guard = pl.guarded and mode != "off"
         if guard:
             pl.range_flag.zero_()
@@ -246,7 +294,7 @@ class RAFT(nn.Module):
         outs = pl.outputs(clone=True)
         if not guard:
             return outs
-        if mode in ("sync", "raise"):
+        if mode != "deferred":  # "fallback" (default), "sync", "raise"
             if int(pl.range_flag.item()):
                 msg = ("f16x3 range guard: an activation exceeded 2^15 in magnitude, outside the exact range "
                        "of the split-f16 conv arithmetic")
@@ -255,7 +303,9 @@ class RAFT(nn.Module):
                 warnings.warn(msg + "; this forward was re-run with exact f32 MFMA convs", RuntimeWarning)
                 return self.forward(image1, image2, iters, flow_init, upsample, test_mode, _prec="fp32")
             return outs
-        # "fallback": the flag travels to pinned host memory behind the forward; read later
+        # "deferred": the flag travels to pinned host memory behind the forward; read later
+        if not self._pending:
+            _register_exit_check(self)
         flag = torch.empty(1, dtype=torch.int32, pin_memory=True)
         flag.copy_(pl.range_flag, non_blocking=True)
         ev = torch.cuda.Event()
@@ -267,3 +317,22 @@ class RAFT(nn.Module):
         if len(self._pending) > self._MAX_PENDING:
             self.check_range_guard(block=False)
         return outs
+
+
+def _register_exit_check(model):
+    """Resolve a model's deferred range-guard checks at interpreter exit (a weak reference: the
+    hook keeps no model alive)."""
+    if getattr(model, "_exit_hook", False):
+        return
+    ref = weakref.ref(model)
+
+    def _flush():
+        m = ref()
+        if m is not None and m._pending:
+            try:
+                m.check_range_guard(block=True)
+            except Exception as e:  # noqa: BLE001 (the GPU context may already be gone)
+                warnings.warn(f"range guard: deferred checks could not be resolved at exit: {e}", RuntimeWarning)
+
+    atexit.register(_flush)
+    model.__dict__["_exit_hook"] = True

@@ -184,13 +184,28 @@ def test_block_plans_cached_per_shape():
     with torch.no_grad():
         for m, mk in cases:
             a = m(*mk(1))
-            plan = m.__dict__["_hip_plan"][2]
+            plan = cur_plan(m)
             m(*mk(7))
             a2 = m(*mk(1))
-            assert m.__dict__["_hip_plan"][2] is plan
+            assert cur_plan(m) is plan
             for x, y in zip(a if isinstance(a, tuple) else (a,), a2 if isinstance(a2, tuple) else (a2,)):
                 assert (x is None and y is None) or torch.equal(x, y)
             # a new shape rebuilds the plan
             big = tuple(t.repeat(1, 1, 2, 1) if t.dim() == 4 else t for t in mk(3))
             m(*big)
-            assert m.__dict__["_hip_plan"][2] is not plan
+            assert cur_plan(m) is not plan
+            # another stream gets buffers of its own; back on the first stream, its plan is reused
+            s2 = torch.cuda.Stream()
+            s2.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s2):
+                b2 = m(*mk(1))
+            s2.synchronize()
+            assert cur_plan(m, s2) is not cur_plan(m)
+            for x, y in zip(a if isinstance(a, tuple) else (a,), b2 if isinstance(b2, tuple) else (b2,)):
+                assert (x is None and y is None) or torch.equal(x, y)
+
+
+def cur_plan(m, stream=None):
+    """The block's cached plan for `stream` (default: the current stream), kernels.cached_plan."""
+    sid = (stream or torch.cuda.current_stream()).cuda_stream
+    return m.__dict__["_hip_plan"][sid][2]

@@ -127,3 +127,65 @@ def test_rccl_world1_broadcast_and_gather_on_device():
     print(f"RCCL world 1: broadcast {nbytes / 1e6:.1f} MB, gather on device {on_dev}")
     assert nbytes > 20e6 and same
     assert n == 1 and on_dev and err == 0.0 and tmax == 1.5
+
+
+@pytest.mark.timeout(300)
+def test_bench_gpus2_spawns_two_ranks():
+    """`bench.py --gpus 2` as the driver invokes it (no launcher): the script spawns the two ranks
+    itself (here in the one-GPU rehearsal mode, RAFT_BENCH_REHEARSE_1GPU=1: both on cuda:0, gloo), and
+    rank 0's JSON line reports both GPUs' pairs."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RAFT_BENCH_REHEARSE_1GPU="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "-u", os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "2",
+                        "--warmup", "1", "--height", "128", "--width", "192", "--iters", "4", "--no-cpu-baseline",
+                        "--no-fp32-exact"], env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 2 and out["value"] > 0
+
+
+@pytest.mark.timeout(300)
+def test_dataparallel_forward_equals_unwrapped():
+    """The reference's own multi-GPU API (nn.DataParallel, demo.py:45, train.py:172): DataParallel(RAFT)
+    on the box's GPU gives the unwrapped forward's flow, and explicit replicas (what DataParallel makes
+    per forward on >1 GPU) reuse the source's packed weights and plans across forwards and match it
+    too, run from a worker thread as parallel_apply does."""
+    import threading
+    from torch.nn.parallel import replicate
+    from raft_optical_flow_amd import RAFT
+    from raft_optical_flow_amd.init import seeded_state_dict, smooth_images
+    m = RAFT(argparse.Namespace(small=False, mixed_precision=False, alternate_corr=False))
+    m.load_state_dict(seeded_state_dict(m, 0))
+    m = m.cuda().eval()
+    i1, i2 = smooth_images(2, H, W, seed=5)
+    i1, i2 = i1.cuda(), i2.cuda()
+    with torch.no_grad():
+        ref_low, ref_up = m(i1, i2, iters=ITERS, test_mode=True)
+        dp = torch.nn.DataParallel(m, device_ids=[0])
+        low, up = dp(i1, i2, iters=ITERS, test_mode=True)
+    assert torch.equal(low, ref_low) and torch.equal(up, ref_up)
+    packed = m.packed(torch.device("cuda", 0))
+    res, errs = [], []
+
+    def run(rep):
+        try:
+            with torch.no_grad(), torch.cuda.device(0):
+                res.append(rep(i1, i2, iters=ITERS, test_mode=True))
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    for _ in range(2):  # two forwards, each with a fresh replica (as DataParallel does)
+        rep = replicate(m, [0])[0]
+        th = threading.Thread(target=run, args=(rep,))
+        th.start()
+        th.join()
+        assert not errs, errs
+        assert rep.packed(torch.device("cuda", 0)) is packed  # no re-pack per replica
+    for lo, u in res:
+        assert torch.equal(lo, ref_low) and torch.equal(u, ref_up)

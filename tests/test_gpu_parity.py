@@ -962,9 +962,10 @@ def test_raft_small_demo_frames_golden():
 def test_f16x3_range_guard_falls_back_to_fp32():
     """Activations beyond f16's range (fnet head scaled so |fmap| ~ 1e5 > 65504): the split-f16
     arithmetic alone would turn them into inf; the range guard (raft_hip.h, RAFT_RANGE_LIMIT) is
-    raised by the fnet head's epilogue and the lookups, and RAFT.forward re-runs the forward on
-    exact f32 MFMA (same result as conv_precision="fp32"), raises with range_guard="raise", and
-    with the guard off shows the hole it closes."""
+    raised by the fnet head's epilogue and the lookups, and RAFT.forward (the default "fallback"
+    mode) returns the re-run on exact f32 MFMA (same result as conv_precision="fp32"); "deferred"
+    corrects the returned tensors at check_range_guard(); "raise" raises; with the guard off the
+    hole it closes shows."""
     import warnings
     g = load_golden("raft_full_rand_b1_128x192_i32.npz")
     m, _ = make_model(False, 0)
@@ -978,16 +979,17 @@ def test_f16x3_range_guard_falls_back_to_fp32():
         fm = ref_m.fnet(i1)
         assert float(fm.abs().max()) > 65504.0
         rlow, rup = ref_m(i1, i2, iters=4, test_mode=True)
-        # "fallback" (default): the check is deferred; check_range_guard() resolves it and the
-        # returned tensors then hold the exact-f32 re-run's result
-        low, up = m(i1, i2, iters=4, test_mode=True)
-        with pytest.warns(RuntimeWarning, match="range guard"):
-            m.check_range_guard()
-        assert maxabs(low, rlow) == 0.0 and maxabs(up, rup) == 0.0
-        # "sync": forward() itself waits for the flag and returns the re-run's result
-        m.range_guard = "sync"
+        # "fallback" (default): forward() itself waits for the flag and returns the re-run's result
+        assert m.range_guard == "fallback"
         with pytest.warns(RuntimeWarning, match="range guard"):
             low, up = m(i1, i2, iters=4, test_mode=True)
+        assert maxabs(low, rlow) == 0.0 and maxabs(up, rup) == 0.0
+        # "deferred": the check waits; check_range_guard() resolves it and the returned tensors
+        # then hold the exact-f32 re-run's result
+        m.range_guard = "deferred"
+        low, up = m(i1, i2, iters=4, test_mode=True)
+        with pytest.warns(RuntimeWarning, match="inexact"):
+            m.check_range_guard()
         assert maxabs(low, rlow) == 0.0 and maxabs(up, rup) == 0.0
         m.range_guard = "raise"
         with pytest.raises(FloatingPointError):
@@ -1000,13 +1002,14 @@ def test_f16x3_range_guard_falls_back_to_fp32():
 
 
 def test_range_guard_deferred_forwards_queue_without_host_sync():
-    """"fallback" mode: back-to-back forwards enqueue without waiting for the GPU (the flag is read
+    """"deferred" mode: back-to-back forwards enqueue without waiting for the GPU (the flag is read
     once its copy has landed): behind a ~50 ms spin kernel, two forward() calls return while the
     stream is still busy; the deferred checks resolve quietly in range, and a forward whose inputs
     were modified in place before a raised flag is read warns that it cannot be corrected."""
     import warnings
     g = load_golden("raft_full_rand_b1_128x192_i32.npz")
     m, _ = make_model(False, 0)
+    m.range_guard = "deferred"
     i1, i2 = t(g["image1"]), t(g["image2"])
     with torch.no_grad(), warnings.catch_warnings():
         warnings.simplefilter("error")

@@ -121,3 +121,50 @@ def test_pfm_reader(tmp_path):
     p = tmp_path / "a.pfm"
     p.write_bytes(b"Pf\n4 3\n-1.0\n" + np.flipud(img).astype("<f4").tobytes())
     assert np.array_equal(rio.readPFM(str(p)), img)
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """bench.py --gpus N spawns N ranks itself (one per GPU); with fewer GPUs visible it fails loudly
+    before starting any, and a launcher's WORLD_SIZE that disagrees with --gpus is an error."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    env.pop("WORLD_SIZE", None)
+    env.pop("RAFT_BENCH_REHEARSE_1GPU", None)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "3"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "--gpus 3 but only" in r.stderr
+    env["WORLD_SIZE"] = "2"
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "3"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=2 but --gpus 3" in r.stderr
+
+
+class _FakePlan:
+    def __init__(self):
+        self.released = False
+
+    def release(self):
+        self.released = True
+
+
+def test_dataparallel_replicas_keep_per_device_caches():
+    """nn.DataParallel re-replicates the model on every forward (reference train.py:172,
+    evaluate.py:179) by shallow-copying __dict__: each replica must reach its SOURCE's cache of its
+    own device (packed weights and plans survive across forwards), have its own range-guard queue,
+    and never clear or evict another device's plans."""
+    m = RAFT(argparse.Namespace(small=False, mixed_precision=False, alternate_corr=False)).eval()
+    r0 = m._replicate_for_data_parallel()
+    r1 = m._replicate_for_data_parallel()
+    r1b = r1._replicate_for_data_parallel()  # a replica of a replica still points at the source
+    assert r0._source() is m and r1._source() is m and r1b._source() is m
+    assert r0._pending is not m._pending and r1._pending is not r0._pending
+    c0, c1 = r0._dev_cache("cuda:0"), r1._dev_cache("cuda:1")
+    assert c0 is not c1
+    assert c0 is m._dev_cache("cuda:0") and c1 is m._dev_cache("cuda:1") and r1b._dev_cache("cuda:1") is c1
+    p0, p1 = _FakePlan(), _FakePlan()
+    c0["plans"]["k"] = p0
+    c1["plans"]["k"] = p1
+    # new weights seen on device 1 clear only device 1's entries
+    r1._release(c1["plans"])
+    assert p1.released and not p0.released and "k" in c0["plans"]
+    m.release_plans()
+    assert p0.released and not c0["plans"]

@@ -20,7 +20,6 @@ ap.add_argument("H", nargs="?", type=int, default=55)
 ap.add_argument("W", nargs="?", type=int, default=128)
 ap.add_argument("--orders", default="-")
 ap.add_argument("--reps", type=int, default=20)
-ap.add_argument("--ws", type=int, default=1, help="1: raft_corr_build_ws (the forward's call), 0: raft_corr_build_prec")
 args = ap.parse_args()
 B, H, W, C, L = args.B, args.H, args.W, 256, 4
 dev = "cuda"
@@ -32,17 +31,11 @@ pyr = torch.empty(K.pyramid_floats(B, H, W, L), device=dev)
 
 fm = torch.cat([f1, f2])
 f1, f2 = fm[: B * H * W], fm[B * H * W:]
-wsb = int(_lib.load().raft_corr_build_ws_bytes(B, H, W, C))
-ws = torch.empty((wsb + 3) // 4, device=dev)
 
 
 def launch():
-    if args.ws:
-        _lib.call("raft_corr_build_ws", f1.data_ptr(), f2.data_ptr(), C, B, H, W, C, L, K.sqrt_c(C), _lib.PREC_F16X3,
-                  ws.data_ptr(), wsb, pyr.data_ptr(), K.stream_handle())
-    else:
-        _lib.call("raft_corr_build_prec", f1.data_ptr(), f2.data_ptr(), C, B, H, W, C, L, K.sqrt_c(C),
-                  _lib.PREC_F16X3, pyr.data_ptr(), K.stream_handle())
+    _lib.call("raft_corr_build_prec", f1.data_ptr(), f2.data_ptr(), C, B, H, W, C, L, K.sqrt_c(C),
+              _lib.PREC_F16X3, pyr.data_ptr(), K.stream_handle())
 
 
 orders = args.orders.split(";")
@@ -77,5 +70,5 @@ for _ in range(5):
         best[i] = min(best[i], e0.elapsed_time(e1) / args.reps * 1e3)
 mb = K.pyramid_floats(B, H, W, L) * 4 / 1e6
 for o, t in zip(orders, best):
-    print(f"corr build (+ pooling, ws={args.ws}) B={B} {H}x{W} order {o}: {t:.1f} us per launch, {mb:.0f} MB pyramid "
+    print(f"corr build (+ pooling) B={B} {H}x{W} order {o}: {t:.1f} us per launch, {mb:.0f} MB pyramid "
           f"({mb / t:.2f} TB/s)")
