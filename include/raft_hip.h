@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define RAFT_HIP_ABI_VERSION 15
+#define RAFT_HIP_ABI_VERSION 16
 
 /* Negative return codes (argument errors, raised before any launch). */
 #define RAFT_E_INVALID (-1)   /* bad size / null pointer / unsupported shape */
@@ -303,6 +303,13 @@ typedef struct raft_conv2d_params {
                                                raft_instnorm_stats / _merge), act = relu if
                                                in_norm_relu; zero padding stays zero.  Only where
                                                raft_conv2d_in_norm_ok says so. */
+  const void* weight_s;                     /* optional (NULL = off), RAFT_PREC_F16X3 only: the
+                                               column-scaled split of the same weight
+                                               (raft_conv2d_split_weight_scaled).  With it, multi-
+                                               round stride-1 3x3 convs run on 256-pixel x 64-
+                                               column tiles whose three products share one
+                                               accumulator; without it they keep the 128-pixel
+                                               tiles.  Same results to fp32 rounding. */
 } raft_conv2d_params;
 
 /* f16x3 range guard.  RAFT_PREC_F16X3 splits every activation x as hi = f16(x), which is
@@ -347,6 +354,14 @@ int raft_conv2d_pair(const raft_conv2d_params* p0, const raft_conv2d_params* p1,
  * per row and 32-wide K-step, 32 f16 hi then 32 f16 lo (lo scaled by 2048);
  * out holds n_pad*k_pad*4 bytes, like the input. */
 int raft_conv2d_split_weight(const float* w, void* out, int n_pad, int k_pad, raft_stream_t stream);
+/* Column-scaled f16x3 split (raft_conv2d_params.weight_s): per output row n a power of two
+ * S_n = 2^(14 - e_n), e_n = the binary exponent of max_k |w[n][k]| (so |w * S_n| < 2^14; S_n = 1 for
+ * a zero row), then per K-step 32 f16 hi = f16(w S_n) and 32 f16 lo = f16(w S_n - hi), both at
+ * the scale S_n, followed by the n_pad floats 1 / S_n.  hi*hi + hi*lo + lo*hi then sum in one
+ * fp32 chain and the epilogue multiplies by 1 / S_n (exact).  out holds
+ * raft_conv2d_split_scaled_bytes(n_pad, k_pad) bytes, 16-byte aligned. */
+size_t raft_conv2d_split_scaled_bytes(int n_pad, int k_pad);
+int raft_conv2d_split_weight_scaled(const float* w, void* out, int n_pad, int k_pad, raft_stream_t stream);
 /* The split form for a given precision: RAFT_PREC_F16X3 / RAFT_PREC_F16 as above;
  * RAFT_PREC_BF16: per row and K-step 32 bf16 hi = bf16(x) then 32 bf16 lo = bf16(x - hi). */
 int raft_conv2d_split_weight_prec(const float* w, void* out, int n_pad, int k_pad, int precision,

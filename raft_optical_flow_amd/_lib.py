@@ -29,7 +29,7 @@ PREC_F16 = 2     # single f16 product (mixed precision)
 PREC_BF16 = 3    # single bf16 product on v_mfma_f32_32x32x16_bf16 (bf16 mixed precision)
 PRECISIONS = {"fp32": PREC_FP32, "f16x3": PREC_F16X3, "f16": PREC_F16, "bf16": PREC_BF16}
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 RANGE_LIMIT = 32768.0  # RAFT_RANGE_LIMIT: |x| above it raises the f16x3 range guard
 
 EPI_LINEAR = 0
@@ -63,6 +63,7 @@ class ConvParams(ctypes.Structure):
         ("range_flag", P),
         ("stats_part", P), ("stats_ld", c_int),
         ("in_norm", P), ("in_norm_relu", c_int),
+        ("weight_s", P),
     ]
 
 
@@ -109,6 +110,8 @@ _PROTOS = {
     "raft_instnorm_merge": (c_int, [P, c_int, c_int, c_int, c_int, c_float, P, P]),
     "raft_conv2d_split_weight": (c_int, [P, P, c_int, c_int, P]),
     "raft_conv2d_split_weight_prec": (c_int, [P, P, c_int, c_int, c_int, P]),
+    "raft_conv2d_split_scaled_bytes": (c_size_t, [c_int, c_int]),
+    "raft_conv2d_split_weight_scaled": (c_int, [P, P, c_int, c_int, P]),
     "raft_instnorm_workspace_floats": (c_size_t, [c_int, c_int, c_int]),
     "raft_instnorm_stats": (c_int, [P, c_int, c_int, c_int, c_int, c_float, P, P, P]),
     "raft_groupnorm_stats": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_float, P, P]),

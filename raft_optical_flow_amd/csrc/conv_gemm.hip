@@ -694,6 +694,32 @@ __global__ void split_weight_bf16_kernel(const float* __restrict__ w, __bf16* __
   out[blk * 64 + k] = h;
   out[blk * 64 + 32 + k] = (__bf16)(x - (float)h);
 }
+// fp32 packed weight -> the column-scaled split (raft_conv2d_split_weight_scaled): one block per row
+__global__ __launch_bounds__(256) void split_weight_scaled_kernel(const float* __restrict__ w, _Float16* __restrict__ out,
+                                                                  float* __restrict__ inv, int k_pad) {
+  const int n = blockIdx.x;
+  const float* row = w + (long)n * k_pad;
+  float mx = 0.f;
+  for (int k = threadIdx.x; k < k_pad; k += 256) mx = fmaxf(mx, fabsf(row[k]));
+  __shared__ float red[4];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  int e = 0;
+  if (mx > 0.f) frexpf(mx, &e);  // mx = f * 2^e, f in [0.5, 1): mx < 2^e
+  e = mx > 0.f ? max(min(14 - e, 100), -100) : 0;
+  const float sc = ldexpf(1.0f, e);
+  for (int k = threadIdx.x; k < k_pad; k += 256) {
+    const float x = row[k] * sc;  // exact (a power of two, no overflow / underflow in range)
+    const _Float16 h = (_Float16)x;
+    const long blk = ((long)n * k_pad + k) >> 5, kk = k & 31;
+    out[blk * 64 + kk] = h;
+    out[blk * 64 + 32 + kk] = (_Float16)(x - (float)h);
+  }
+  if (threadIdx.x == 0) inv[n] = ldexpf(1.0f, -e);
+}
 }  // namespace
 
 #ifdef STAMPS
@@ -709,6 +735,21 @@ extern "C" int raft_conv2d_split_weight(const float* w, void* out, int n_pad, in
   hipLaunchKernelGGL(split_weight_kernel, dim3((unsigned)cdiv_l(total, 256)), dim3(256), 0, as_stream(stream), w,
                      reinterpret_cast<_Float16*>(out), total);
   return check_launch("raft_conv2d_split_weight");
+}
+
+extern "C" size_t raft_conv2d_split_scaled_bytes(int n_pad, int k_pad) {
+  if (n_pad <= 0 || k_pad <= 0 || k_pad % BK) return 0;
+  return (size_t)n_pad * k_pad * 4 + (size_t)n_pad * 4;
+}
+
+extern "C" int raft_conv2d_split_weight_scaled(const float* w, void* out, int n_pad, int k_pad, raft_stream_t stream) {
+  RAFT_REQUIRE(w && out && n_pad > 0 && k_pad > 0 && k_pad % BK == 0, "raft_conv2d_split_weight_scaled: bad args");
+  RAFT_REQUIRE((const void*)w != out && ((uintptr_t)out & 15) == 0,
+               "raft_conv2d_split_weight_scaled: out must be a separate 16-byte aligned buffer");
+  _Float16* o = reinterpret_cast<_Float16*>(out);
+  float* inv = reinterpret_cast<float*>(reinterpret_cast<char*>(out) + (size_t)n_pad * k_pad * 4);
+  hipLaunchKernelGGL(split_weight_scaled_kernel, dim3((unsigned)n_pad), dim3(256), 0, as_stream(stream), w, o, inv, k_pad);
+  return check_launch("raft_conv2d_split_weight_scaled");
 }
 
 extern "C" int raft_conv2d_split_weight_prec(const float* w, void* out, int n_pad, int k_pad, int precision,

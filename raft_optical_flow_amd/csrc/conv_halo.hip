@@ -46,11 +46,13 @@ namespace raft {
 namespace {
 
 constexpr int HTW = 16;              // tile width (pixels)
-constexpr int HTH = 8;               // tile height: 128 GEMM rows per work-group
+constexpr int HTH = 8;               // tile height of the one-round tiles: 128 GEMM rows per work-group
+constexpr int HTH_BIG = 16;          // tile height of the multi-round tiles (halo_big): 256 rows
 constexpr int HALO_LDS = 160 * 1024;  // LDS per CU (one work-group per CU)
 
 struct HaloArgs {
   raft_conv2d_params p;
+  const float* inv_scale;  // big f16x3 tiles: per output column 1 / S_n of the scaled weight (weight_s)
   int K;           // packed weight row length (floats)
   int nch;         // 32-channel chunks
   int nk;          // K-steps = nch * taps
@@ -87,13 +89,14 @@ constexpr int halo_lds_bytes(int T, int U, int D, int BNT, int PI, int WR) {
   return U * (D + 1) * BNT * WR + patch_slots(T, U, D) * PI * 1024;
 }
 
-// WR: bytes per weight row in LDS (128: f16x3 hi | lo; 64: the one-product modes' hi half)
-template <int KH, int KW, int BNT, int WR = 128>
+// WR: bytes per weight row in LDS (128: f16x3 hi | lo; 64: the one-product modes' hi half);
+// TH: tile rows (HTH, or HTH_BIG for the multi-round tiles)
+template <int KH, int KW, int BNT, int WR = 128, int TH = HTH>
 struct HaloCfg {
   static constexpr int T = KH * KW;
   static constexpr int U = (BNT == 32 && T > 1) ? 4 : 2;  // K-steps per super-step
   static constexpr int LB = HALO_LDS;
-  static constexpr int PH = HTH + KH - 1, PW = HTW + KW - 1, NPIX = PH * PW;
+  static constexpr int PH = TH + KH - 1, PW = HTW + KW - 1, NPIX = PH * PW;
   static constexpr int PI = (NPIX + 7) / 8;  // 1-KiB DMA pieces per patch
   // load sets in flight ahead of the super-step: 3, or 2 where 3 does not fit
 #ifdef HALO_D  // dev builds: deeper load rings where they fit
@@ -128,15 +131,19 @@ __device__ __forceinline__ unsigned long long hstamp_now() {
 }
 #endif
 
-// The tile body (one 8x16-pixel x BNT-column tile of the conv `a`, tile index q within it; smem =
+// The tile body (one TH x 16-pixel x BNT-column tile of the conv `a`, tile index q within it; smem =
 // the work-group's LDS).  ENC: the encoder features (InstanceNorm partial statistics in the
 // epilogue, the input's InstanceNorm applied by the 3x3 loaders); separate instantiations, so the
-// update block's convs compile exactly as without them.
-template <int KH, int KW, int BNT, int PREC, bool ENC = false>
+// update block's convs compile exactly as without them.  TH = HTH_BIG: the multi-round tiles
+// (256 pixels x 64 columns, each compute wave 64 x 64 as 2 x 2 MFMA blocks: 2/3 of the LDS
+// fragment bytes per MFMA and half the weight bytes per pixel of the 128-pixel tiles); in f16x3
+// they run on the column-scaled weight (raft_conv2d_split_weight_scaled: w*S_n = hi + lo, both
+// at one scale), so the three products share ONE accumulator chain per block (SC).
+template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH>
 __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q, char* smem) {
   constexpr bool X3 = PREC == RAFT_PREC_F16X3;
   constexpr bool BF = PREC == RAFT_PREC_BF16;
-  using C = HaloCfg<KH, KW, BNT, X3 ? 128 : 64>;
+  using C = HaloCfg<KH, KW, BNT, X3 ? 128 : 64, TH>;
   constexpr int T = C::T, U = C::U, D = C::D, PW = C::PW, NPIX = C::NPIX, PI = C::PI, PA = C::PA, SB = C::SB;
   // Weight rows in LDS: f16x3 the packed K-step row as it is (32 hi then 32 lo halves, 128 B);
   // the one-product modes (F16, BF16) read only hi, so only the 64-B hi half of each row
@@ -148,15 +155,19 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
   constexpr int RPP = 1024 / WROW;             // rows per 1-KiB DMA piece
   constexpr int NBI = BNT / RPP;    // 1-KiB DMA pieces per weight block (one K-step)
   constexpr int NWP = U * NBI / 4;  // weight pieces per loader wave per load set
-  // Compute waves: BNT <= 64: 4 waves along M, each 32 pixels (tile rows 2w, 2w+1) x all BNT
-  // columns; BNT = 128 (the one-product modes' wide tiles): 2 x 2 waves, each 64 pixels (MF = 2
-  // MFMA row blocks) x 64 columns, half the LDS fragment bytes per MFMA
-  constexpr int MF = BNT == 128 ? 2 : 1;  // 32-pixel MFMA row blocks per compute wave
-  constexpr int WVM = 4 / MF;             // compute waves along M
-  constexpr int WCOL = BNT / MF;          // columns per compute wave
+  // Compute waves (32-pixel MFMA row blocks = two tile rows): TH = 8, BNT <= 64: 4 waves along M,
+  // each one block (tile rows 2w, 2w+1) x all BNT columns; TH = 8, BNT = 128 (the one-product
+  // modes' wide tiles): 2 x 2 waves, each 2 blocks (64 pixels) x 64 columns; TH = 16, BNT = 64:
+  // 4 waves along M, each 2 blocks (tile rows 4w .. 4w+3) x 64 columns
+  constexpr int WN = BNT == 128 ? 2 : 1;  // compute waves along N
+  constexpr int WVM = 4 / WN;             // compute waves along M
+  constexpr int MF = TH / 2 / WVM;        // 32-pixel MFMA row blocks per compute wave
+  constexpr int WCOL = BNT / WN;          // columns per compute wave
   constexpr int NSUB = WCOL / 32;         // 32-column MFMA subtiles per compute wave
-  static_assert(!ENC || MF == 1, "the InstanceNorm partials are per 32-pixel wave");
-  static_assert(!(X3 && MF > 1), "f16x3 wide tiles exceed the register budget");
+  constexpr bool SC = X3 && TH == HTH_BIG;  // one accumulator on the column-scaled weight
+  static_assert(MF >= 1 && MF * WVM * 2 == TH, "tile rows");
+  static_assert(!(X3 && MF > 1) || SC, "f16x3 2 x 2 blocks need the one-accumulator (scaled) form");
+  static_assert(!ENC || WN == 1, "the InstanceNorm partials are per 32-pixel block of all columns");
 
   // LSPLIT: the loaders stage each patch through registers and store it
   // pre-split (f16 hi | lo, the weight-row format), so the MFMA waves read
@@ -185,7 +196,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
   const int nt = q % a.gn, st = q / a.gn;
   const int per = a.tx_n * a.ty_n;
   const int b = st / per, sr = st - b * per;
-  const int y0 = (sr / a.tx_n) * HTH, x0 = (sr % a.tx_n) * HTW;
+  const int y0 = (sr / a.tx_n) * TH, x0 = (sr % a.tx_n) * HTW;
   const int n0 = nt * BNT;
   const int nk = a.nk, nch = a.nch;
   const int ns = (nk + U - 1) / U;
@@ -445,14 +456,17 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
 #pragma unroll
   for (int f = 0; f < MF; ++f) ppbase[f] = (2 * (wm * MF + f) + (m >> 4)) * PW + (m & 15);
   const int bsw = X3 ? (m >> 1) & 7 : (m >> 2) & 3;  // swizzle of weight row cb + sb*32 + m
-  f32x16 acc[MF][NSUB], accx[MF][NSUB];
+  // accx: the hi * (2048 lo) chain of the unscaled f16x3 form (not used by SC or one-product modes)
+  constexpr int AXF = X3 && !SC ? MF : 1, AXS = X3 && !SC ? NSUB : 1;
+  f32x16 acc[MF][NSUB], accx[AXF][AXS];
 #pragma unroll
   for (int f = 0; f < MF; ++f)
 #pragma unroll
-    for (int sb = 0; sb < NSUB; ++sb) {
-      acc[f][sb] = f32x16{};
-      accx[f][sb] = f32x16{};
-    }
+    for (int sb = 0; sb < NSUB; ++sb) acc[f][sb] = f32x16{};
+#pragma unroll
+  for (int f = 0; f < AXF; ++f)
+#pragma unroll
+    for (int sb = 0; sb < AXS; ++sb) accx[f][sb] = f32x16{};
   // Fragment reads run ahead of the MFMAs: the B fragments of K-step j+1 and
   // the A (activation) values of K-step j+2 are read while K-step j's MFMAs
   // run, and A of j+1 (read one K-step earlier) is split to f16 behind them,
@@ -549,7 +563,18 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
           for (int sb = 0; sb < NSUB; ++sb)
             acc[f][sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.ah[f][qq], F.bh[sb][qq], acc[f][sb], 0, 0, 0);
       }
-      if constexpr (X3) {
+      if constexpr (SC) {  // hi * lo and lo * hi at the scale of hi * hi: the same chain
+#pragma unroll
+        for (int f = 0; f < MF; ++f)
+#pragma unroll
+          for (int sb = 0; sb < NSUB; ++sb)
+            acc[f][sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.ah[f][qq], F.bl[sb][qq], acc[f][sb], 0, 0, 0);
+#pragma unroll
+        for (int f = 0; f < MF; ++f)
+#pragma unroll
+          for (int sb = 0; sb < NSUB; ++sb)
+            acc[f][sb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(F.al[f][qq], F.bh[sb][qq], acc[f][sb], 0, 0, 0);
+      } else if constexpr (X3) {
 #pragma unroll
         for (int f = 0; f < MF; ++f)
 #pragma unroll
@@ -629,7 +654,16 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
 #ifdef STAMPS
   const unsigned long long c_epi = hstamp_now();
 #endif
-  if constexpr (X3) {
+  if constexpr (SC) {  // undo the column scale S_n (a power of two: exact)
+#pragma unroll
+    for (int sb = 0; sb < NSUB; ++sb) {
+      const float is = a.inv_scale[n0 + cb + sb * 32 + m];
+#pragma unroll
+      for (int f = 0; f < MF; ++f)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[f][sb][r] *= is;
+    }
+  } else if constexpr (X3) {
 #pragma unroll
     for (int f = 0; f < MF; ++f)
 #pragma unroll
@@ -650,9 +684,10 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
 #pragma unroll
     for (int sb = 0; sb < NSUB; ++sb) tile_epilogue<false>(p, rows, n0 + cb + sb * 32 + m, acc[f][sb]);
     if constexpr (ENC) {
-      if (p.stats_part) {  // InstanceNorm partials of the raw output (slot: spatial tile x 4 + wave)
+      if (p.stats_part) {  // InstanceNorm partials of the raw output (slot: spatial tile x 4 MF + block)
 #pragma unroll
-        for (int sb = 0; sb < NSUB; ++sb) tile_stats(p, rows, n0 + sb * 32 + m, acc[f][sb], (long)st * 4 + w);
+        for (int sb = 0; sb < NSUB; ++sb)
+          tile_stats(p, rows, n0 + sb * 32 + m, acc[f][sb], (long)st * (4 * MF) + w * MF + f);
       }
     }
   }
@@ -675,20 +710,29 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
 }
 
 // One conv (or an independent pair, raft_conv2d_pair) per launch: one tile per work-group.
-template <int KH, int KW, int BNT, int PREC, bool ENC = false>
+template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH>
 __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
-  using C = HaloCfg<KH, KW, BNT, PREC == RAFT_PREC_F16X3 ? 128 : 64>;
+  using C = HaloCfg<KH, KW, BNT, PREC == RAFT_PREC_F16X3 ? 128 : 64, TH>;
   constexpr int NORM_BYTES = (ENC && KH == 3 && KW == 3 && C::D == 3) ? 256 * 8 : 0;
   __shared__ __attribute__((aligned(1024))) char smem[C::LDS_B + C::LDS_A + NORM_BYTES];
   int q = xcd_tile(blockIdx.x, gridDim.x);
   const int prob = q >= hl.tiles0 ? 1 : 0;
   q -= prob * hl.tiles0;
-  halo_body<KH, KW, BNT, PREC, ENC>(hl.a, prob, q, smem);
+  halo_body<KH, KW, BNT, PREC, ENC, TH>(hl.a, prob, q, smem);
 }
 
 template <int KH, int KW, int PREC>
-void launch_halo_p(const HaloLaunch& l, int bn, dim3 grid, hipStream_t s) {
+void launch_halo_p(const HaloLaunch& l, int bn, int th, dim3 grid, hipStream_t s) {
   const raft_conv2d_params& p = l.a[0].p;
+  if constexpr (KH == 3 && KW == 3) {
+    if (th == HTH_BIG) {  // (halo_pick: N tile 64)
+      if (p.stats_part || p.in_norm)
+        hipLaunchKernelGGL((conv_halo_kernel<3, 3, 64, PREC, true, HTH_BIG>), grid, dim3(512), 0, s, l);
+      else
+        hipLaunchKernelGGL((conv_halo_kernel<3, 3, 64, PREC, false, HTH_BIG>), grid, dim3(512), 0, s, l);
+      return;
+    }
+  }
   if constexpr (PREC != RAFT_PREC_F16X3) {
     if (bn == 128) {  // (conv_halo_launch picks it only without stats_part / in_norm)
       hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 128, PREC>), grid, dim3(512), 0, s, l);
@@ -710,14 +754,14 @@ void launch_halo_p(const HaloLaunch& l, int bn, dim3 grid, hipStream_t s) {
     hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 32, PREC>), grid, dim3(512), 0, s, l);
 }
 template <int KH, int KW>
-void launch_halo_k(const HaloLaunch& l, int bn, dim3 grid, hipStream_t s) {
+void launch_halo_k(const HaloLaunch& l, int bn, int th, dim3 grid, hipStream_t s) {
   const int prec = l.a[0].p.precision;
   if (prec == RAFT_PREC_F16X3)
-    launch_halo_p<KH, KW, RAFT_PREC_F16X3>(l, bn, grid, s);
+    launch_halo_p<KH, KW, RAFT_PREC_F16X3>(l, bn, th, grid, s);
   else if (prec == RAFT_PREC_BF16)
-    launch_halo_p<KH, KW, RAFT_PREC_BF16>(l, bn, grid, s);
+    launch_halo_p<KH, KW, RAFT_PREC_BF16>(l, bn, th, grid, s);
   else
-    launch_halo_p<KH, KW, RAFT_PREC_F16>(l, bn, grid, s);
+    launch_halo_p<KH, KW, RAFT_PREC_F16>(l, bn, th, grid, s);
 }
 
 bool halo_enabled() {
@@ -739,6 +783,7 @@ bool halo_problem(const HaloOperands& o, HaloArgs& a) {
   if (!shape || p.pad_h != (kh - 1) / 2 || p.pad_w != (kw - 1) / 2) return false;
   if (p.out_h != p.in_h || p.out_w != p.in_w || p.n <= 4) return false;
   a.p = p;
+  a.inv_scale = nullptr;
   a.K = o.k_pad;
   a.nch = o.k_pad / (kh * kw) / 32;
   a.nk = a.nch * kh * kw;
@@ -753,17 +798,50 @@ bool halo_problem(const HaloOperands& o, HaloArgs& a) {
 
 long halo_spatial(const HaloArgs& a) { return (long)a.p.batch * a.tx_n * a.ty_n; }
 
-void launch_halo(const HaloLaunch& l, int bn, long tiles, hipStream_t s) {
+// The multi-round tiles (TH = HTH_BIG, N tile 64) for 3x3 convs whose big-tile grid still has
+// RAFT_HALO_BIG_MIN (default 512: two rounds of 256 CUs) work-groups; f16x3 needs the scaled
+// weight (raft_conv2d_params.weight_s).  RAFT_HALO_BIG_MIN=0 turns them off.
+long halo_big_min() {
+  static const long v = [] {
+    const char* e = getenv("RAFT_HALO_BIG_MIN");
+    return e ? atol(e) : 512L;
+  }();
+  return v;
+}
+bool halo_big_ok(const HaloOperands& o) {
+  const raft_conv2d_params& p = o.p;
+  return p.kh == 3 && p.kw == 3 && o.n_pad % 64 == 0 && (p.precision != RAFT_PREC_F16X3 || p.weight_s != nullptr);
+}
+long halo_big_tiles(const HaloOperands& o) {
+  const raft_conv2d_params& p = o.p;
+  return (long)p.batch * cdiv(p.out_h, HTH_BIG) * cdiv(p.out_w, HTW) * (o.n_pad / 64);
+}
+// Tile rows of a conv's launch: HTH_BIG where the big tiles qualify and (the one-product modes
+// without encoder features) the 128-column tiles do not apply
+int halo_pick_th(const HaloOperands& o, bool wide) {
+  const long mn = halo_big_min();
+  return !wide && mn > 0 && halo_big_ok(o) && halo_big_tiles(o) >= mn ? HTH_BIG : HTH;
+}
+// the big tiles' operands: spatial tiles of TH_BIG rows; f16x3 reads the scaled weight
+void halo_set_th(const HaloOperands& o, HaloArgs& a, int th) {
+  a.ty_n = cdiv(a.p.out_h, th);
+  if (th == HTH_BIG && a.p.precision == RAFT_PREC_F16X3) {
+    a.p.weight = reinterpret_cast<const float*>(o.p.weight_s);
+    a.inv_scale = reinterpret_cast<const float*>(reinterpret_cast<const char*>(o.p.weight_s) + (size_t)o.w_bytes);
+  }
+}
+
+void launch_halo(const HaloLaunch& l, int bn, int th, long tiles, hipStream_t s) {
   const raft_conv2d_params& p = l.a[0].p;
   dim3 grid((unsigned)tiles);
   if (p.kh == 1 && p.kw == 1)
-    launch_halo_k<1, 1>(l, bn, grid, s);
+    launch_halo_k<1, 1>(l, bn, th, grid, s);
   else if (p.kh == 3)
-    launch_halo_k<3, 3>(l, bn, grid, s);
+    launch_halo_k<3, 3>(l, bn, th, grid, s);
   else if (p.kh == 1)
-    launch_halo_k<1, 5>(l, bn, grid, s);
+    launch_halo_k<1, 5>(l, bn, th, grid, s);
   else
-    launch_halo_k<5, 1>(l, bn, grid, s);
+    launch_halo_k<5, 1>(l, bn, th, grid, s);
 }
 
 
@@ -787,9 +865,11 @@ bool conv_halo_norm_ok(const HaloOperands& o) {
 int conv_halo_stats_slots(const HaloOperands& o) {
   HaloArgs a;
   if (!halo_enabled() || !halo_problem(o, a)) return 0;
-  // only the ENC instantiations (1x1 and 3x3, launch_halo_p) write InstanceNorm partials
+  // only the ENC instantiations (1x1 and 3x3, launch_halo_p) write InstanceNorm partials: one slot
+  // per 32-pixel block of a spatial tile (the tile rows of conv_halo_launch's pick)
   if (!((o.p.kh == 1 && o.p.kw == 1) || (o.p.kh == 3 && o.p.kw == 3))) return 0;
-  return a.tx_n * a.ty_n * 4;
+  const int th = halo_pick_th(o, false);  // (ENC convs never take the 128-column tiles)
+  return a.tx_n * cdiv(o.p.out_h, th) * (th / 2);
 }
 
 // Launches the halo kernel when the conv is one it covers; returns 1 without launching
@@ -813,13 +893,15 @@ int conv_halo_launch(const HaloOperands& o, hipStream_t s) {
   // leaves two rounds of work-groups (configs 3 - 5; RAFT_HALO_WIDE=0: never)
   const bool wide = p.precision != RAFT_PREC_F16X3 && !p.stats_part && !p.in_norm && o.n_pad % 128 == 0 &&
                     spatial * (o.n_pad / 128) >= 512 && halo_wide_enabled();
-  const int bn = wide ? 128 : spatial * (o.n_pad / 64) > 128 ? 64 : 32;
+  const int th = halo_pick_th(o, wide);
+  const int bn = th == HTH_BIG ? 64 : wide ? 128 : spatial * (o.n_pad / 64) > 128 ? 64 : 32;
+  halo_set_th(o, l.a[0], th);
   l.a[0].gn = o.n_pad / bn;
-  const long tiles = spatial * l.a[0].gn;
+  const long tiles = halo_spatial(l.a[0]) * l.a[0].gn;
   if (tiles >= (1L << 31)) return 1;
   l.a[1] = l.a[0];
   l.tiles0 = (int)tiles;
-  launch_halo(l, bn, tiles, s);
+  launch_halo(l, bn, th, tiles, s);
   return 0;
 }
 
@@ -831,15 +913,22 @@ int conv_halo_launch_pair(const HaloOperands& o0, const HaloOperands& o1, hipStr
   if (!halo_enabled() || !halo_problem(o0, l.a[0]) || !halo_problem(o1, l.a[1])) return 1;
   const raft_conv2d_params &p0 = o0.p, &p1 = o1.p;
   if (p0.kh != p1.kh || p0.kw != p1.kw || p0.precision != p1.precision) return 1;
+  // the big tiles when both convs qualify and their tiles together reach RAFT_HALO_BIG_MIN
+  const long mn = halo_big_min();
+  const int th = mn > 0 && halo_big_ok(o0) && halo_big_ok(o1) && halo_big_tiles(o0) + halo_big_tiles(o1) >= mn
+                     ? HTH_BIG
+                     : HTH;
+  halo_set_th(o0, l.a[0], th);
+  halo_set_th(o1, l.a[1], th);
   const long s0 = halo_spatial(l.a[0]), s1 = halo_spatial(l.a[1]);
-  const int bn = s0 * (o0.n_pad / 64) + s1 * (o1.n_pad / 64) > 128 ? 64 : 32;
+  const int bn = th == HTH_BIG ? 64 : s0 * (o0.n_pad / 64) + s1 * (o1.n_pad / 64) > 128 ? 64 : 32;
   if (o0.n_pad % bn || o1.n_pad % bn) return 1;
   l.a[0].gn = o0.n_pad / bn;
   l.a[1].gn = o1.n_pad / bn;
   const long t0 = s0 * l.a[0].gn, tiles = t0 + s1 * l.a[1].gn;
   if (tiles >= (1L << 31)) return 1;
   l.tiles0 = (int)t0;
-  launch_halo(l, bn, tiles, s);
+  launch_halo(l, bn, th, tiles, s);
   return 0;
 }
 

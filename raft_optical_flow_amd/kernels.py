@@ -84,6 +84,7 @@ class PackedConv:
     precision: int = _lib.PREC_FP32
     split: torch.Tensor | None = None   # hi/lo f16 (F16X3 / F16) or bf16 (BF16) form of `weight`, made on first use
     split_prec: int = -1
+    split_s: torch.Tensor | None = None  # column-scaled f16x3 split (raft_conv2d_split_weight_scaled), on first use
 
     def launch_precision(self) -> int:
         # N <= 4 convs run on the VALU kernel, which reads the fp32 weight
@@ -101,6 +102,20 @@ class PackedConv:
                       fmt, stream_handle())
             self.split_prec = fmt
         return self.split
+
+    def launch_weight_s(self) -> torch.Tensor | None:
+        """The column-scaled f16x3 split (raft_conv2d_params.weight_s) for the convs the halo kernel may
+        run on its multi-round tiles (stride-1 3x3, VEC mode, f16x3); None otherwise."""
+        if not (self.precision == _lib.PREC_F16X3 and self.n > 4 and self.kh == 3 and self.kw == 3
+                and self.stride == (1, 1) and self.mode == _lib.RAFT_CONV_VEC):
+            return None
+        if self.split_s is None:
+            w = self.weight
+            nbytes = int(_lib.load().raft_conv2d_split_scaled_bytes(w.shape[0], w.shape[1]))
+            self.split_s = torch.empty(nbytes // 4, device=w.device, dtype=torch.float32)
+            _lib.call("raft_conv2d_split_weight_scaled", w.data_ptr(), self.split_s.data_ptr(), w.shape[0], w.shape[1],
+                      stream_handle())
+        return self.split_s
 
 
 def set_precision(obj, precision: int, _seen=None):
@@ -203,6 +218,8 @@ def conv_params(pc: PackedConv, src0: Rows, batch: int, in_h: int, in_w: int, ou
     p.kh, p.kw, p.stride_h, p.stride_w, p.pad_h, p.pad_w = pc.kh, pc.kw, sh, sw, ph, pw
     p.mode = pc.mode
     p.weight = pc.launch_weight().data_ptr()
+    ws = pc.launch_weight_s()
+    p.weight_s = ws.data_ptr() if ws is not None else None
     p.precision = pc.launch_precision()
     p.bias = pc.bias.data_ptr() if pc.bias is not None else None
     p.n = pc.n

@@ -56,6 +56,7 @@ def make_model(small, seed=0, alternate=False, precision=None):
     dict(cin=64, cout=64, k=3, stride=1, pad=1, H=37, W=53, B=2, mode=None),   # halo 3x3, ragged tiles
     dict(cin=96, cout=96, k=1, stride=1, pad=0, H=20, W=33, B=2, mode=None),   # halo 1x1
     dict(cin=3, cout=64, k=7, stride=2, pad=3, H=90, W=150, B=2, mode="gather"),  # the stem
+    dict(cin=64, cout=64, k=3, stride=1, pad=1, H=220, W=512, B=2, mode=None),  # big tiles (fnet layer1)
 ])
 @pytest.mark.parametrize("prec", ["f16x3", "bf16"])
 def test_conv_epilogue_instnorm_stats(case, prec):
@@ -96,7 +97,8 @@ def test_conv_epilogue_instnorm_stats(case, prec):
     assert float(((got[0][..., 1].double() - rstd) / rstd).abs().max()) < 1e-5
 
 
-@pytest.mark.parametrize("cin,cout,H,W,B,relu", [(64, 64, 37, 53, 2, 1), (128, 96, 23, 30, 1, 0), (96, 96, 16, 16, 1, 1)])
+@pytest.mark.parametrize("cin,cout,H,W,B,relu", [(64, 64, 37, 53, 2, 1), (128, 96, 23, 30, 1, 0), (96, 96, 16, 16, 1, 1),
+                                                (64, 64, 220, 512, 2, 1)])   # (the last: big tiles)
 @pytest.mark.parametrize("prec", ["f16x3", "bf16"])
 def test_conv_in_norm_loader(cin, cout, H, W, B, relu, prec):
     """raft_conv2d_params.in_norm: the 3x3 halo conv reads act((x - mean) * rstd) of its raw input
@@ -660,6 +662,77 @@ def test_conv_halo_wide_tiles_multi_round(cin, cout, kh, kw, H, W, prec):
         ref = torch.relu(F.conv2d(x[i:i + 1].double(), w.double(), b.double(), 1, pad))
         assert maxabs(y[i:i + 1], ref) < CONV_TOL[prec] * max(1.0, float(ref.abs().max())), i
     assert bool((out.t[:, cout:] == -7.0).all())
+
+
+@pytest.mark.parametrize("prec", ["f16x3", "bf16", "f16"])
+@pytest.mark.parametrize("cin,cout,H,W,B", [
+    (64, 64, 220, 512, 2),    # fnet layer1 at config 2 (896 big tiles)
+    (256, 192, 61, 70, 8),    # ragged tiles in both axes, N padded to 256 (640 big tiles)
+    (128, 256, 68, 120, 8),   # config 4's flow-head conv1 shape
+])
+def test_conv_halo_big_tiles_multi_round(cin, cout, H, W, B, prec):
+    """The multi-round 3x3 halo tiles (16 x 16 pixels x 64 columns, each compute wave 2 x 2 MFMA blocks;
+    f16x3 on the column-scaled weight with one accumulator) vs torch fp64 on the first and last image,
+    and vs the 128-pixel tiles of the same conv (RAFT_HALO_BIG_MIN is read once per process, so the
+    small-tile reference is the same conv without weight_s in f16x3, or at fp64 in the other modes);
+    the output row padding stays untouched."""
+    from raft_optical_flow_amd import kernels as K
+    from raft_optical_flow_amd import _lib
+    g = torch.Generator().manual_seed(cin + cout + H)
+    x = torch.randn(B, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / np.sqrt(cin * 9)
+    w[:, :, 1, 1] *= 1e-4  # small weights beside large ones in every column (the scaled lo's range)
+    b = torch.randn(cout, generator=g)
+    pc = K.pack_conv(w, b, 1, 1, device=DEV)
+    pc.precision = _lib.PRECISIONS[prec]
+    src = K.Rows(K.nchw_to_rows(x.to(DEV)))
+    out = K.Rows(torch.full((B * H * W, cout + 4), -7.0, device=DEV), 0, cout)
+    p = K.conv_params(pc, src, B, H, W, out, epilogue=_lib.EPI_RELU)
+    assert (p.weight_s is not None) == (prec == "f16x3")
+    K.conv_launch(p)(K.stream_handle())
+    y = K.rows_to_nchw(out, B, H, W)
+    for i in (0, B - 1):
+        ref = torch.relu(F.conv2d(x[i:i + 1].double(), w.double(), b.double(), 1, 1))
+        assert maxabs(y[i:i + 1], ref) < CONV_TOL[prec] * max(1.0, float(ref.abs().max())), i
+    assert bool((out.t[:, cout:] == -7.0).all())
+    if prec == "f16x3":
+        out2 = K.Rows(torch.full((B * H * W, cout + 4), -7.0, device=DEV), 0, cout)
+        p2 = K.conv_params(pc, src, B, H, W, out2, epilogue=_lib.EPI_RELU)
+        p2.weight_s = None  # the 128-pixel tiles, unscaled two-chain form
+        K.conv_launch(p2)(K.stream_handle())
+        ref2 = out2.t[:, :cout]
+        assert maxabs(out.t[:, :cout], ref2) < 2e-5 * max(1.0, float(ref2.abs().max()))
+
+
+def test_conv2d_split_weight_scaled_layout():
+    """raft_conv2d_split_weight_scaled: per row a power of two S_n with max |w S_n| in [2^13, 2^14), per
+    K-step 32 f16 hi = f16(w S_n) then 32 f16 lo = f16(w S_n - hi), then the n_pad floats 1 / S_n; a zero
+    row gets S_n = 1."""
+    from raft_optical_flow_amd import _lib
+    g = torch.Generator().manual_seed(13)
+    w = (torch.randn(64, 96, generator=g) * 0.05)
+    w[5] *= 1e-6
+    w[7] = 0.0
+    w = w.to(DEV)
+    nbytes = int(_lib.load().raft_conv2d_split_scaled_bytes(64, 96))
+    assert nbytes == 64 * 96 * 4 + 64 * 4
+    out = torch.empty(nbytes // 4, device=DEV)
+    _lib.call("raft_conv2d_split_weight_scaled", w.data_ptr(), out.data_ptr(), 64, 96, 0)
+    torch.cuda.synchronize()
+    inv = out[64 * 96:].cpu().double()
+    h = out[: 64 * 96].view(torch.float16).view(64, 3, 2, 32).cpu()
+    wc = w.cpu().double()
+    mx = wc.abs().max(1).values
+    sc = 1.0 / inv
+    assert bool((torch.log2(sc) == torch.round(torch.log2(sc))).all())
+    nz = mx > 0
+    assert bool(((mx * sc)[nz] < 2 ** 14).all()) and bool(((mx * sc)[nz] >= 2 ** 13).all()) and float(sc[7]) == 1.0
+    ws = (wc * sc[:, None]).view(64, 3, 32)
+    hi = ws.float().half()
+    lo = (ws - hi.double()).float().half()
+    assert torch.equal(h[:, :, 0], hi) and torch.equal(h[:, :, 1], lo)
+    rec = (h[:, :, 0].double() + h[:, :, 1].double()) * inv[:, None, None]
+    assert float(((rec - wc.view(64, 3, 32)).abs() / mx[:, None, None].clamp_min(1e-30)).max()) < 2.0 ** -21
 
 
 @pytest.mark.parametrize("prec", ["f16x3", "bf16"])
