@@ -338,6 +338,13 @@ int raft_conv2d_stats_slots(const raft_conv2d_params* p);
 int raft_conv2d_in_norm_ok(const raft_conv2d_params* p);
 int raft_instnorm_merge(const float* part, int slots_per_image, int B, int C, int stats_ld, float eps,
                         float* stats, raft_stream_t stream);
+/* raft_instnorm_merge over many slots, spread over the CUs: level 1 sums groups of 32 slots per
+ * channel relative to slot 0's mean (coalesced 1-KiB slot rows, no division), level 2 combines the
+ * groups in order (deterministic).  ws: raft_instnorm_merge_ws_floats(slots_per_image, B, C) floats,
+ * 8-byte aligned; the same {mean, rstd} as raft_instnorm_merge to double rounding. */
+size_t raft_instnorm_merge_ws_floats(int slots_per_image, int B, int C);
+int raft_instnorm_merge_ws(const float* part, int slots_per_image, int B, int C, int stats_ld, float eps, void* ws,
+                           float* stats, raft_stream_t stream);
 
 /* Packed weight geometry for a conv (n_pad, k_pad in floats per row). */
 int raft_conv2d_packed_shape(int mode, int n, int kh, int kw, int cin, int* n_pad, int* k_pad);

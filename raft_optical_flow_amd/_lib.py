@@ -108,6 +108,8 @@ _PROTOS = {
     "raft_conv2d_stats_slots": (c_int, [ctypes.POINTER(ConvParams)]),
     "raft_conv2d_in_norm_ok": (c_int, [ctypes.POINTER(ConvParams)]),
     "raft_instnorm_merge": (c_int, [P, c_int, c_int, c_int, c_int, c_float, P, P]),
+    "raft_instnorm_merge_ws_floats": (c_size_t, [c_int, c_int, c_int]),
+    "raft_instnorm_merge_ws": (c_int, [P, c_int, c_int, c_int, c_int, c_float, P, P, P]),
     "raft_conv2d_split_weight": (c_int, [P, P, c_int, c_int, P]),
     "raft_conv2d_split_weight_prec": (c_int, [P, P, c_int, c_int, c_int, P]),
     "raft_conv2d_split_scaled_bytes": (c_size_t, [c_int, c_int]),

@@ -294,9 +294,8 @@ __device__ __forceinline__ void tile_epilogue(const raft_conv2d_params& p, const
 // InstanceNorm partial statistics of one wave's 32x32 accumulator tile (raft_conv2d_stats_slots):
 // for column n, (count, mean, M2) of v = acc + bias over the wave's valid rows; lanes n and n + 32
 // hold 16 rows each.  M2 is taken around the wave's own mean (well conditioned in fp32).
-__device__ __forceinline__ void tile_stats_b(const raft_conv2d_params& p, const int (&rows)[16], int n,
-                                             const f32x16& acc, long slot, float bias) {
-  const bool ncol = n < p.n;
+// (count, mean, M2) of one 32-pixel block's rows of column n (every lane of the wave gets them)
+__device__ __forceinline__ f32x4 tile_stats_vals(const int (&rows)[16], const f32x16& acc, float bias) {
   float s = 0.f, c = 0.f;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -313,8 +312,23 @@ __device__ __forceinline__ void tile_stats_b(const raft_conv2d_params& p, const 
     m2 += rows[r] >= 0 ? d * d : 0.f;
   }
   m2 += __shfl_xor(m2, 32);
-  if (ncol && (threadIdx.x & 32) == 0)
-    *reinterpret_cast<f32x4*>(p.stats_part + (slot * p.stats_ld + n) * 4) = f32x4{c, mean, m2, 0.f};
+  return f32x4{c, mean, m2, 0.f};
+}
+// Chan's combination of two (count, mean, M2) partials
+__device__ __forceinline__ f32x4 stats_combine(const f32x4& a, const f32x4& b) {
+  const float n = a[0] + b[0];
+  if (b[0] <= 0.f) return a;
+  if (a[0] <= 0.f) return b;
+  const float d = b[1] - a[1];
+  return f32x4{n, a[1] + d * (b[0] / n), a[2] + b[2] + d * d * (a[0] * b[0] / n), 0.f};
+}
+__device__ __forceinline__ void stats_write(const raft_conv2d_params& p, int n, long slot, const f32x4& v) {
+  if (n < p.n && (threadIdx.x & 32) == 0)
+    *reinterpret_cast<f32x4*>(p.stats_part + (slot * p.stats_ld + n) * 4) = v;
+}
+__device__ __forceinline__ void tile_stats_b(const raft_conv2d_params& p, const int (&rows)[16], int n,
+                                             const f32x16& acc, long slot, float bias) {
+  stats_write(p, n, slot, tile_stats_vals(rows, acc, bias));
 }
 __device__ __forceinline__ void tile_stats(const raft_conv2d_params& p, const int (&rows)[16], int n,
                                            const f32x16& acc, long slot) {

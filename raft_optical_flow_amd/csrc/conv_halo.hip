@@ -672,6 +672,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
         for (int r = 0; r < 16; ++r) acc[f][sb][r] += accx[f][sb][r] * (1.0f / SPLIT_SCALE);
   }
   // ---- epilogue: register r of block f holds row m = (r&3) + 8(r>>2) + 4h of its 32 pixels
+  f32x4 stv[NSUB];  // ENC: the wave's InstanceNorm partials per column (its MF blocks combined)
 #pragma unroll
   for (int f = 0; f < MF; ++f) {
     int rows[16];
@@ -684,10 +685,14 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
 #pragma unroll
     for (int sb = 0; sb < NSUB; ++sb) tile_epilogue<false>(p, rows, n0 + cb + sb * 32 + m, acc[f][sb]);
     if constexpr (ENC) {
-      if (p.stats_part) {  // InstanceNorm partials of the raw output (slot: spatial tile x 4 MF + block)
+      if (p.stats_part) {  // InstanceNorm partials of the raw output, per wave (slot: spatial tile x 4 + wave)
 #pragma unroll
-        for (int sb = 0; sb < NSUB; ++sb)
-          tile_stats(p, rows, n0 + sb * 32 + m, acc[f][sb], (long)st * (4 * MF) + w * MF + f);
+        for (int sb = 0; sb < NSUB; ++sb) {
+          const int n = n0 + sb * 32 + m;
+          const f32x4 v = tile_stats_vals(rows, acc[f][sb], p.bias ? p.bias[n < p.n ? n : 0] : 0.f);
+          stv[sb] = f == 0 ? v : stats_combine(stv[sb], v);
+          if (f == MF - 1) stats_write(p, n, (long)st * 4 + w, stv[sb]);
+        }
       }
     }
   }
@@ -866,10 +871,10 @@ int conv_halo_stats_slots(const HaloOperands& o) {
   HaloArgs a;
   if (!halo_enabled() || !halo_problem(o, a)) return 0;
   // only the ENC instantiations (1x1 and 3x3, launch_halo_p) write InstanceNorm partials: one slot
-  // per 32-pixel block of a spatial tile (the tile rows of conv_halo_launch's pick)
+  // per compute wave of a spatial tile (the tile rows of conv_halo_launch's pick)
   if (!((o.p.kh == 1 && o.p.kw == 1) || (o.p.kh == 3 && o.p.kw == 3))) return 0;
   const int th = halo_pick_th(o, false);  // (ENC convs never take the 128-column tiles)
-  return a.tx_n * cdiv(o.p.out_h, th) * (th / 2);
+  return a.tx_n * cdiv(o.p.out_h, th) * 4;
 }
 
 // Launches the halo kernel when the conv is one it covers; returns 1 without launching

@@ -385,6 +385,71 @@ __global__ __launch_bounds__(256) void instnorm_merge_kernel(const float* part, 
   stats[2 * (b * C + c) + 1] = (float)(1.0 / sqrt(var + (double)eps));
 }
 
+// raft_instnorm_merge_ws, level 1: block (channel group of 64, image, slot group g) sums its <= 32
+// slots per channel relative to a shift K = the mean of slot 0 (sums only, no division: a fixed
+// order, deterministic): n = sum c_i, s1 = sum c_i (m_i - K), s2 = sum M2_i + c_i (m_i - K)^2.
+// Lane = channel (a wave's load of one slot is 1 KiB contiguous); wave w takes slots w, w+4, ...
+constexpr int MERGE_SPG = 32;  // slots per level-1 group (4 waves x 8 loads in flight per lane)
+__global__ __launch_bounds__(256) void instnorm_merge1_kernel(const float* part, int slots, int C, int ld,
+                                                              double* ws, int G) {
+  __shared__ double red[4][3][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane, b = blockIdx.y, g = blockIdx.z;
+  const bool cok = c < C;
+  const float* pb = part + ((long)b * slots * ld + (cok ? c : 0)) * 4;
+  const float K = cok ? pb[1] : 0.f;  // slot 0's mean (slot 0 always holds pixels)
+  f32x4 v[MERGE_SPG / 4];
+#pragma unroll
+  for (int i = 0; i < MERGE_SPG / 4; ++i) {
+    const int k = g * MERGE_SPG + w + 4 * i;
+    v[i] = (cok && k < slots) ? *reinterpret_cast<const f32x4*>(pb + (long)k * ld * 4) : f32x4{};
+  }
+  double n = 0.0, s1 = 0.0, s2 = 0.0;
+#pragma unroll
+  for (int i = 0; i < MERGE_SPG / 4; ++i) {
+    const double cnt = v[i][0], d = (double)v[i][1] - (double)K;
+    n += cnt;
+    s1 += cnt * d;
+    s2 += (double)v[i][2] + cnt * d * d;
+  }
+  red[w][0][lane] = n;
+  red[w][1][lane] = s1;
+  red[w][2][lane] = s2;
+  __syncthreads();
+  if (w == 0 && cok) {
+    double* o = ws + (((long)b * G + g) * C + c) * 3;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) o[q] = ((red[0][q][lane] + red[1][q][lane]) + red[2][q][lane]) + red[3][q][lane];
+  }
+}
+// level 2: one lane per (image, channel) sums the G groups in order and writes {mean, rstd}
+__global__ __launch_bounds__(64) void instnorm_merge2_kernel(const float* part, int slots, int C, int ld,
+                                                             const double* ws, int G, float eps, float* stats) {
+  const int c = blockIdx.x * 64 + threadIdx.x, b = blockIdx.y;
+  if (c >= C) return;
+  const double K = part[((long)b * slots * ld + c) * 4 + 1];
+  double n = 0.0, s1 = 0.0, s2 = 0.0;
+  const double* p = ws + ((long)b * G * C + c) * 3;
+  for (int g0 = 0; g0 < G; g0 += 8) {
+    double t[8][3];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) t[i][q] = g0 + i < G ? p[((long)(g0 + i) * C) * 3 + q] : 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      n += t[i][0];
+      s1 += t[i][1];
+      s2 += t[i][2];
+    }
+  }
+  const double mean = n > 0.0 ? K + s1 / n : 0.0;
+  const double m2 = n > 0.0 ? fmax(s2 - s1 * s1 / n, 0.0) : 0.0;
+  const double var = n > 0.0 ? m2 / n : 0.0;
+  stats[2 * ((long)b * C + c)] = (float)mean;
+  stats[2 * ((long)b * C + c) + 1] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
 // nn.GroupNorm statistics (core/extractor.py:23-25, the blocks' norm_fn='group'): one block per
 // (group, image); mean, then the variance around it, over the group's C/G channels x HW pixels in
 // double with a fixed-order tree (deterministic); written per (image, channel) as the {mean, rstd}
@@ -577,6 +642,26 @@ extern "C" int raft_instnorm_merge(const float* part, int slots_per_image, int B
   hipLaunchKernelGGL(instnorm_merge_kernel, dim3(C, B), dim3(256), 0, as_stream(stream), part, slots_per_image, C,
                      stats_ld, eps, stats);
   return check_launch("raft_instnorm_merge");
+}
+
+extern "C" size_t raft_instnorm_merge_ws_floats(int slots_per_image, int B, int C) {
+  if (slots_per_image <= 0 || B <= 0 || C <= 0) return 0;
+  return (size_t)B * cdiv(slots_per_image, MERGE_SPG) * C * 3 * 2;  // doubles
+}
+
+extern "C" int raft_instnorm_merge_ws(const float* part, int slots_per_image, int B, int C, int stats_ld, float eps,
+                                      void* ws, float* stats, raft_stream_t stream) {
+  RAFT_REQUIRE(part && ws && stats && slots_per_image > 0 && B > 0 && C > 0 && stats_ld >= C && B < 65536,
+               "raft_instnorm_merge_ws: bad arguments");
+  RAFT_REQUIRE(aligned16(part) && ((uintptr_t)ws & 7) == 0, "raft_instnorm_merge_ws: part 16-B, ws 8-B aligned");
+  const int G = cdiv(slots_per_image, MERGE_SPG);
+  RAFT_REQUIRE(G < 65536, "raft_instnorm_merge_ws: too many slots");
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(instnorm_merge1_kernel, dim3(cdiv(C, 64), B, G), dim3(256), 0, s, part, slots_per_image, C,
+                     stats_ld, reinterpret_cast<double*>(ws), G);
+  hipLaunchKernelGGL(instnorm_merge2_kernel, dim3(cdiv(C, 64), B), dim3(64), 0, s, part, slots_per_image, C, stats_ld,
+                     reinterpret_cast<const double*>(ws), G, eps, stats);
+  return check_launch("raft_instnorm_merge_ws");
 }
 
 extern "C" int raft_instnorm_apply(const float* x, int ld, const float* stats, const float* resid, int resid_ld,

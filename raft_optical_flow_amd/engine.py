@@ -220,7 +220,9 @@ def _conv_in(L, A: Arena, pc: PackedConv, src: Rows, n_img, h, w, out: Rows, src
         p.stats_part, p.stats_ld = part.data_ptr(), out.c
         L.append(conv_launch(p))
         st = A.flat(2 * n_img * out.c)
-        L.append(Launch("raft_instnorm_merge", part.data_ptr(), slots, n_img, out.c, out.c, 1e-5, st.data_ptr()))
+        ws = A.flat(_lib.load().raft_instnorm_merge_ws_floats(slots, n_img, out.c))
+        L.append(Launch("raft_instnorm_merge_ws", part.data_ptr(), slots, n_img, out.c, out.c, 1e-5, ws.data_ptr(),
+                        st.data_ptr()))
         return st
     L.append(conv_launch(p))
     return _in_stats(L, A, out, n_img, ho * wo)

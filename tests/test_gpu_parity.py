@@ -90,11 +90,21 @@ def test_conv_epilogue_instnorm_stats(case, prec):
                   K.stream_handle())
         got.append(st.view(B, case["cout"], 2).cpu())
     assert torch.equal(got[0], got[1])
+    # the two-level merge the forward runs (raft_instnorm_merge_ws): run to run bit-identical too
+    nws = int(_lib.load().raft_instnorm_merge_ws_floats(slots, B, case["cout"]))
+    ws = torch.full((nws,), float("nan"), device=DEV)
+    for _ in range(2):
+        st = torch.empty(2 * B * case["cout"], device=DEV)
+        _lib.call("raft_instnorm_merge_ws", part.data_ptr(), slots, B, case["cout"], case["cout"], 1e-5, ws.data_ptr(),
+                  st.data_ptr(), K.stream_handle())
+        got.append(st.view(B, case["cout"], 2).cpu())
+    assert torch.equal(got[2], got[3])
     y = out.t.view(B, ho * wo, case["cout"]).cpu().double()
     mean = y.mean(1)
     rstd = 1.0 / torch.sqrt(y.var(1, unbiased=False) + 1e-5)
-    assert float((got[0][..., 0].double() - mean).abs().max()) < 1e-5 * max(1.0, float(mean.abs().max()))
-    assert float(((got[0][..., 1].double() - rstd) / rstd).abs().max()) < 1e-5
+    for gg in (got[0], got[2]):
+        assert float((gg[..., 0].double() - mean).abs().max()) < 1e-5 * max(1.0, float(mean.abs().max()))
+        assert float(((gg[..., 1].double() - rstd) / rstd).abs().max()) < 1e-5
 
 
 @pytest.mark.parametrize("cin,cout,H,W,B,relu", [(64, 64, 37, 53, 2, 1), (128, 96, 23, 30, 1, 0), (96, 96, 16, 16, 1, 1),
