@@ -32,8 +32,8 @@ The line also carries
                 as a replayed graph (MFMA-bound; fp32-equivalent peak per conv arithmetic:
                 f32 MFMA 157.3 TF, f16x3 = f16 MFMA / 3, f16 / bf16 2.5 PF);
   dominant_kernel  the step's dominant kernel, conv_halo_kernel<3,3,64> (convc2 and
-                the flow-head conv1), with its committed MFMA-busy PMC
-                (profiles/r02_halo_pmc.json) while conv_halo.hip is unchanged;
+                the flow-head conv1), with the MFMA-busy PMC of the newest committed
+                profiles/rNN_halo_pmc.json taken on the current conv_halo.hip;
   fp32_exact    with the default f16x3 conv arithmetic: the same run with exact
                 f32 MFMA convs (value, ms_per_step), rank 0, N = 1;
   cpu_baseline  the reference's CPU path restated with the same torch CPU operators
@@ -112,6 +112,45 @@ def inforward_launch_us(plan, name):
     return sum(a.elapsed_time(b) for a, b in pairs) / len(pairs) * 1e3, len(pairs)
 
 
+def inforward_graph_us(plan, name, reps=5):
+    """Per-dispatch duration of the launches called `name` INSIDE the graph-replayed forward: the
+    plan's whole launch list captured as one hipGraph with timing events (external event-record
+    nodes) around each such launch on the main stream, replayed `reps` times; the mean over the
+    last replay's pairs.  The other launches run as in the forward (caches in the forward's state).
+    Returns (us, pairs), or None when events cannot be captured."""
+    from raft_optical_flow_amd import kernels as K
+    try:
+        side = plan.side_stream or torch.cuda.Stream(device=plan.device)
+        pairs = []
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            cur = torch.cuda.current_stream()
+            for l in plan.launches:
+                if l is K.FORK:
+                    side.wait_stream(cur)
+                elif l is K.JOIN:
+                    cur.wait_stream(side)
+                elif not l.side and l.name == name:
+                    a = torch.cuda.Event(enable_timing=True, external=True)
+                    b = torch.cuda.Event(enable_timing=True, external=True)
+                    a.record(cur)
+                    l(cur.cuda_stream)
+                    b.record(cur)
+                    pairs.append((a, b))
+                else:
+                    l(side.cuda_stream if l.side else cur.cuda_stream)
+        for _ in range(reps):
+            g.replay()
+        torch.cuda.synchronize()
+        us = sum(a.elapsed_time(b) for a, b in pairs) / len(pairs) * 1e3
+        del g
+        return us, len(pairs)
+    except Exception:  # noqa: BLE001 (event capture unsupported: the caller falls back)
+        torch.cuda.synchronize()
+        return None
+
+
 def time_kernel_events(fn, reps):
     """Average GPU duration of fn() (kernel launches on the current stream): the reps
     launches are captured in one hipGraph and timed with HIP events around its replay
@@ -187,18 +226,20 @@ def rotated_lookup(plan, batch, h8, w8, nrot, reps):
                       f"({nrot * nfl * 4 / 2**30:.1f} GiB; cache-cold), the forward's final coords"}
 
 
-def load_pmc(name, source):
-    """A committed PMC summary (profiles/<name>) if it was taken on the current kernel source:
-    its source_sha must equal the sha1 of that .hip file (else the counters are stale)."""
+def load_pmc(kind, source):
+    """The newest committed PMC summary profiles/r<NN>_<kind> taken on the current kernel source: its
+    source_sha must equal the sha1 of that .hip file (else the counters are stale and None is
+    returned).  Returns (summary, file name) or (None, None)."""
+    import glob
     import hashlib
-    path = os.path.join(ROOT, "profiles", name)
-    if not os.path.exists(path):
-        return None
-    with open(path) as f:
-        d = json.load(f)
     with open(os.path.join(ROOT, "raft_optical_flow_amd", "csrc", source), "rb") as f:
         sha = hashlib.sha1(f.read()).hexdigest()
-    return d if d.get("source_sha") == sha else None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_{kind}")), reverse=True):
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("source_sha") == sha:
+            return d, os.path.basename(path)
+    return None, None
 
 
 def cpu_baseline(args, budget_s=12.0):
@@ -378,7 +419,7 @@ def main():
     if not args.alternate_corr:
         # 16 pyramids: 16 x 28 MB of windows per rotation at B=1 (> the 256 MiB Infinity Cache)
         lookup_b1 = rotated_lookup(plan, args.batch, h8, w8, nrot=max(3, -(-16 // args.batch)), reps=4)
-        pmc = load_pmc("r03_lookup_pmc.json", "corr_pyramid.hip")
+        pmc, _ = load_pmc("lookup_pmc.json", "corr_pyramid.hip")
         # the committed PMC pass is of config 2 (B=1, 440x1024) on the current kernel source
         lookup_b1["traffic"] = (pmc["hbm_bytes_per_launch"] if pmc and [args.batch, H, W] == pmc["shape_bhw"]
                                 else None)
@@ -400,11 +441,11 @@ def main():
                 "algorithmic_bytes_per_launch": alg, "launch_us": round(us, 2),
                 "timing": f"HIP event pairs around each of the {n} launches of an eagerly enqueued forward (queued "
                           f"behind a spin so the GPU runs them back to back)"}
-        fpmc = load_pmc("r03_lookup_conv_pmc.json", src)
+        fpmc, fname = load_pmc("lookup_conv_pmc.json" if src == "lookup_conv.hip" else "lookup_pmc.json", src)
         roof["traffic"] = (fpmc["hbm_bytes_per_launch"] if fpmc and [args.batch, H, W] == fpmc["shape_bhw"]
                            else None)
         if roof["traffic"] is not None:
-            roof["traffic_source"] = "profiles/r03_lookup_conv_pmc.json (in-forward FETCH_SIZE/WRITE_SIZE)"
+            roof["traffic_source"] = f"profiles/{fname} (in-forward FETCH_SIZE/WRITE_SIZE)"
     else:
         # alternate corr: FP32 VALU-bound, 2*P*L*(2r+2)^2*C flops over the L per-level launches
         nl = plan.pk.levels
@@ -448,19 +489,27 @@ def main():
         rest = [l for l in it_all if getattr(l, "name", "") != "raft_corr_lookup_conv"]
         lk = [l for l in it_all if getattr(l, "name", "") == "raft_corr_lookup_conv"][0]
         t_rest = time_kernel_events(lambda: [l(K.stream_handle()) for l in rest], 20)
-        # the forward's own launch (its pyramid, final coords and outputs) 32 times back to back in
-        # one graph: per-dispatch time as rocprofv3 reports it (event pairs around single launches
-        # add their own ~3-4 us; so does a graph boundary)
-        us = time_kernel_events(lambda: [lk(K.stream_handle()) for _ in range(32)], 4) / 32 * 1e6
+        # the forward's own launch 32 times back to back in one graph (warm caches: a lower bound)
+        b2b = time_kernel_events(lambda: [lk(K.stream_handle()) for _ in range(32)], 4) / 32 * 1e6
         roof["event_pair_us"] = roof["launch_us"]
         roof["iteration_delta_us"] = round((t_it - t_rest) * 1e6, 2)
+        roof["back_to_back_us"] = round(b2b, 2)
+        # the figure: the launch's per-dispatch time inside the graph-replayed forward (event-record
+        # nodes around its 32 dispatches), as rocprofv3's in-forward mean reports it; without event
+        # capture the iteration delta (also in-forward, and the larger figure)
+        ig = inforward_graph_us(plan, "raft_corr_lookup_conv")
+        us, how = ((ig[0], f"HIP event-record nodes around each of the {ig[1]} dispatches inside the captured forward "
+                           f"graph, mean of the last replay") if ig else
+                   (roof["iteration_delta_us"], "one iteration's graph with minus without the launch"))
         roof["launch_us"] = round(us, 2)
         roof["achieved"] = round(roof["algorithmic_bytes_per_launch"] / us / 1e3, 1)
         roof["frac"] = round(roof["achieved"] / HBM_PEAK_GBS, 4)
-        roof["timing"] = ("HIP events around a hipGraph of 4 x 32 back-to-back replays of the forward's own fused lookup "
-                          "launch (its pyramid, the final coords); event_pair_us: HIP event pairs around each of the 32 "
-                          "launches of an eager forward; iteration_delta_us: one iteration's graph with minus without "
-                          "the launch")
+        roof["limiter"] = ("per-CU L2 ingest + latency (one 2x16-pixel work-group per CU streams the whole 360 KB split "
+                           "convc1 weight; PMC: profiles/*lookup_conv_pmc.json): priced against the HBM roofline its "
+                           "algorithmic bytes define")
+        roof["timing"] = (how + "; event_pair_us: HIP event pairs around each launch of an eager forward; "
+                          "iteration_delta_us: one iteration's graph with minus without the launch; back_to_back_us: "
+                          "32 back-to-back replays of the forward's own launch (warm caches)")
     it_convs = [plan.launches[i] for i in range(lk_idx[per_it] + 1, lk_idx[2 * per_it])
                 if getattr(plan.launches[i], "name", "") in ("raft_conv2d", "raft_conv2d_pair", "raft_conv2d_chain")
                 and not plan.launches[i].side]
@@ -500,10 +549,11 @@ def main():
                     "frac": round(dfl / dt / 1e12 / peak, 4), "launches": len(dom),
                     "launch_us": round(dt / len(dom) * 1e6, 2), "flops_per_launch": dfl // len(dom),
                     "timing": "HIP events around a hipGraph of 50 replays of those launches"}
-        hpmc = load_pmc("r03_halo_pmc.json", "conv_halo.hip")
+        hpmc, hname = load_pmc("halo_pmc.json", "conv_halo.hip")
         if hpmc:
-            dominant["mfma_busy"] = (hpmc.get("conv_halo_kernel<3, 3, 64, 1, false>")
-                                     or hpmc.get("conv_halo_kernel<3, 3, 64, 1>") or {}).get("mfma_busy")
+            dominant["mfma_busy"] = (hpmc.get("conv_halo_kernel<3, 3, 64, 1, false, 8>")
+                                     or hpmc.get("conv_halo_kernel<3, 3, 64, 1, false>") or {}).get("mfma_busy")
+            dominant["mfma_busy_source"] = f"profiles/{hname}"
 
     exact = None
     if prec != "fp32" and world == 1 and not args.no_fp32_exact:
