@@ -714,6 +714,32 @@ def test_conv_halo_big_tiles_multi_round(cin, cout, H, W, B, prec):
         assert maxabs(out.t[:, :cout], ref2) < 2e-5 * max(1.0, float(ref2.abs().max()))
 
 
+@pytest.mark.parametrize("prec", ["bf16", "f16"])
+@pytest.mark.parametrize("cin,cout,kh,kw,H,W,B", [
+    (256, 256, 1, 5, 68, 120, 4),   # the GRU z|r conv at config 4's map (big tiles: 1x5, 16 x 20 patch)
+    (256, 128, 5, 1, 61, 70, 8),    # q at ragged tiles (big tiles: 5x1, 20 x 16 patch)
+])
+def test_conv_halo_big_tiles_1x5_5x1(cin, cout, kh, kw, H, W, B, prec):
+    """The one-product modes' 1x5 / 5x1 convs on the multi-round 16 x 16 tiles vs torch fp64."""
+    from raft_optical_flow_amd import kernels as K
+    from raft_optical_flow_amd import _lib
+    g = torch.Generator().manual_seed(cin + cout + kh * 7)
+    x = torch.randn(B, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, kh, kw, generator=g) / np.sqrt(cin * kh * kw)
+    b = torch.randn(cout, generator=g)
+    pad = ((kh - 1) // 2, (kw - 1) // 2)
+    pc = K.pack_conv(w, b, 1, pad, device=DEV)
+    pc.precision = _lib.PRECISIONS[prec]
+    src = K.Rows(K.nchw_to_rows(x.to(DEV)))
+    out = K.Rows(torch.full((B * H * W, cout + 4), -7.0, device=DEV), 0, cout)
+    K.conv2d_rows(pc, src, B, H, W, out, epilogue=_lib.EPI_LINEAR)
+    y = K.rows_to_nchw(out, B, H, W)
+    for i in (0, B - 1):
+        ref = F.conv2d(x[i:i + 1].double(), w.double(), b.double(), 1, pad)
+        assert maxabs(y[i:i + 1], ref) < CONV_TOL[prec] * max(1.0, float(ref.abs().max())), i
+    assert bool((out.t[:, cout:] == -7.0).all())
+
+
 def test_conv2d_split_weight_scaled_layout():
     """raft_conv2d_split_weight_scaled: per row a power of two S_n with max |w S_n| in [2^13, 2^14), per
     K-step 32 f16 hi = f16(w S_n) then 32 f16 lo = f16(w S_n - hi), then the n_pad floats 1 / S_n; a zero
