@@ -737,9 +737,10 @@ void launch_halo_p(const HaloLaunch& l, int bn, int th, dim3 grid, hipStream_t s
         hipLaunchKernelGGL((conv_halo_kernel<3, 3, 64, PREC, false, HTH_BIG>), grid, dim3(512), 0, s, l);
       return;
     }
-  } else if constexpr (PREC != RAFT_PREC_F16X3 && KH * KW == 5) {
-    // 1x5 / 5x1 big tiles in the one-product modes only: their 64-B weight rows leave LDS for the
-    // three pre-split 16 x 20 patches the T = 5 ring needs (f16x3's 128-B rows do not)
+  } else if constexpr (KH * KW == 5) {
+    // 1x5 / 5x1 big tiles: the one-product modes' 64-B weight rows leave LDS for the three pre-split
+    // 16 x 20 patches the T = 5 ring needs (D = 3); f16x3's 128-B rows do not, so it runs D = 2 with
+    // fp32 patches split by the compute waves (216 / 232 VGPRs)
     if (th == HTH_BIG) {
       hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 64, PREC, false, HTH_BIG>), grid, dim3(512), 0, s, l);
       return;
@@ -824,8 +825,8 @@ bool halo_big_ok(const HaloOperands& o) {
   const raft_conv2d_params& p = o.p;
   if (o.n_pad % 64) return false;
   if (p.kh == 3 && p.kw == 3) return p.precision != RAFT_PREC_F16X3 || p.weight_s != nullptr;
-  // 1x5 / 5x1: one-product modes, no encoder features (launch_halo_p)
-  return p.kh * p.kw == 5 && p.precision != RAFT_PREC_F16X3 && !p.stats_part && !p.in_norm;
+  // 1x5 / 5x1: no encoder features (launch_halo_p)
+  return p.kh * p.kw == 5 && (p.precision != RAFT_PREC_F16X3 || p.weight_s != nullptr) && !p.stats_part && !p.in_norm;
 }
 long halo_big_tiles(const HaloOperands& o) {
   const raft_conv2d_params& p = o.p;

@@ -105,8 +105,8 @@ class PackedConv:
 
     def launch_weight_s(self) -> torch.Tensor | None:
         """The column-scaled f16x3 split (raft_conv2d_params.weight_s) for the convs the halo kernel may
-        run on its multi-round tiles (stride-1 3x3, VEC mode, f16x3); None otherwise."""
-        if not (self.precision == _lib.PREC_F16X3 and self.n > 4 and self.kh == 3 and self.kw == 3
+        run on its multi-round tiles (stride-1 3x3 / 1x5 / 5x1, VEC mode, f16x3); None otherwise."""
+        if not (self.precision == _lib.PREC_F16X3 and self.n > 4 and (self.kh, self.kw) in ((3, 3), (1, 5), (5, 1))
                 and self.stride == (1, 1) and self.mode == _lib.RAFT_CONV_VEC):
             return None
         if self.split_s is None:

@@ -714,13 +714,14 @@ def test_conv_halo_big_tiles_multi_round(cin, cout, H, W, B, prec):
         assert maxabs(out.t[:, :cout], ref2) < 2e-5 * max(1.0, float(ref2.abs().max()))
 
 
-@pytest.mark.parametrize("prec", ["bf16", "f16"])
+@pytest.mark.parametrize("prec", ["f16x3", "bf16", "f16"])
 @pytest.mark.parametrize("cin,cout,kh,kw,H,W,B", [
     (256, 256, 1, 5, 68, 120, 4),   # the GRU z|r conv at config 4's map (big tiles: 1x5, 16 x 20 patch)
     (256, 128, 5, 1, 61, 70, 8),    # q at ragged tiles (big tiles: 5x1, 20 x 16 patch)
 ])
 def test_conv_halo_big_tiles_1x5_5x1(cin, cout, kh, kw, H, W, B, prec):
-    """The one-product modes' 1x5 / 5x1 convs on the multi-round 16 x 16 tiles vs torch fp64."""
+    """1x5 / 5x1 convs on the multi-round 16 x 16 tiles vs torch fp64 (f16x3: the scaled split, D = 2 with
+    fp32 patches; one-product modes: pre-split patches, D = 3)."""
     from raft_optical_flow_amd import kernels as K
     from raft_optical_flow_amd import _lib
     g = torch.Generator().manual_seed(cin + cout + kh * 7)
