@@ -241,6 +241,13 @@ def test_bf16_1080x1920_vs_reference_autocast():
     with torch.no_grad():
         m = make_model(int(g["seed"]), precision="bf16")
         low, up = m(i1.to(DEV), i2.to(DEV), iters=int(g["iters"]), test_mode=True)
+        # config 5 names the hipGraph-captured loop: the second call captures the forward and
+        # replays it; the replay must give the eager (first) call's flow bit for bit
+        pl = m.plan(1, 1080, 1920, int(g["iters"]), True)
+        assert pl.graph is None
+        low2, up2 = m(i1.to(DEV), i2.to(DEV), iters=int(g["iters"]), test_mode=True)
+        assert pl.graph is not None
+    assert torch.equal(low2, low) and torch.equal(up2, up)
     assert torch.isfinite(up).all()
     lo = low.cpu().double().numpy()
     u8 = up[:, :, ::8].cpu().double().numpy()

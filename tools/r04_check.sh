@@ -2,7 +2,7 @@
 # Round-4 GPU round trip: targeted tests, the full GPU suite, the config-2 bench line, configs 4 / 5,
 # and a kernel trace of a config-2 forward with its phase summary.  Every GPU step has its own time
 # limit and the chain stops at the first failure.
-#   TAG        output name suffix (default r04)
+#   TAG        output name suffix (default r04);  FIRST / FIRST_K: test files / -k expression run first
 #   TESTS=0    skip the full suite;  SWEEP=0 skip configs 4 / 5;  TRACE=0 skip the trace
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -10,7 +10,7 @@ TAG=${TAG:-r04}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 if [ -n "$FIRST" ]; then
-  timeout -k 10 400 python -u -m pytest $FIRST -x -q --timeout 240 --timeout-method thread > gpurun_out/t_${TAG}_first.log 2>&1
+  timeout -k 10 400 python -u -m pytest $FIRST ${FIRST_K:+-k "$FIRST_K"} -x -q --timeout 240 --timeout-method thread > gpurun_out/t_${TAG}_first.log 2>&1
   rc=$?; tail -4 gpurun_out/t_${TAG}_first.log; [ $rc -eq 0 ] || exit $rc
 fi
 if [ "${TESTS:-1}" != 0 ]; then

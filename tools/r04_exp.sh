@@ -17,4 +17,17 @@ run python tools/conv_bench.py 1
 run env RAFT_HIP_LIB=variants/hst/libraft_hip.so HSTAMPS=1 python tools/conv_bench.py 1 convc2,conv,zr_split,q_split,fh1
 run env RAFT_HIP_LIB=variants/hst/libraft_hip.so HSTAMPS=1 SHAPESET=enc python tools/conv_bench.py 1
 run env RAFT_HIP_LIB=variants/lcst/libraft_hip.so python tools/lc_stamps.py
+if [ -n "$ALT" ]; then  # config 3's alternate lookup: MFMA box GEMM vs the VALU tile kernel, and its phase stamps
+  for sp in 0 1; do
+    run python tools/alt_bench.py 8 $sp
+    run env RAFT_ALT_MFMA=0 python tools/alt_bench.py 8 $sp
+  done
+  run env RAFT_HIP_LIB=variants/altst/libraft_hip.so python tools/alt_stamps.py 8 1
+fi
+if [ -n "$AB_CONFIGS" ]; then  # the forward with the big tiles off, same box (A/B against r04_check's sweep)
+  for a in "--batch 8 --height 540 --width 960" "--batch 1 --height 1080 --width 1920 --precision bf16" ""; do
+    echo "== RAFT_HALO_BIG_MIN=0 bench $a" >> $O
+    RAFT_HALO_BIG_MIN=0 timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-fp32-exact $a >> $O 2>> gpurun_out/exp_${TAG}.err || { echo failed; exit 1; }
+  done
+fi
 cat $O
