@@ -811,13 +811,15 @@ bool halo_problem(const HaloOperands& o, HaloArgs& a) {
 
 long halo_spatial(const HaloArgs& a) { return (long)a.p.batch * a.tx_n * a.ty_n; }
 
-// The multi-round tiles (TH = HTH_BIG, N tile 64) for 3x3 convs whose big-tile grid still has
-// RAFT_HALO_BIG_MIN (default 512: two rounds of 256 CUs) work-groups; f16x3 needs the scaled
-// weight (raft_conv2d_params.weight_s).  RAFT_HALO_BIG_MIN=0 turns them off.
+// The big tiles (TH = HTH_BIG, N tile 64) for 3x3 / 1x5 / 5x1 convs whose big-tile grid still has
+// RAFT_HALO_BIG_MIN (default 256: one full round of 256 CUs) work-groups: a round of big tiles
+// does the work of two rounds of 128-pixel tiles, so from one full round on they cost no CUs;
+// below it (a frame pair's update convs) they would leave CUs idle.  f16x3 needs the scaled weight
+// (raft_conv2d_params.weight_s).  RAFT_HALO_BIG_MIN=0 turns them off.
 long halo_big_min() {
   static const long v = [] {
     const char* e = getenv("RAFT_HALO_BIG_MIN");
-    return e ? atol(e) : 512L;
+    return e ? atol(e) : 256L;
   }();
   return v;
 }

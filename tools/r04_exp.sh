@@ -9,7 +9,7 @@ O=gpurun_out/exp_${TAG}.txt
 mkdir -p gpurun_out
 : > $O
 run() { echo "== $*" >> $O; timeout -k 10 200 "$@" >> $O 2>&1 || { echo "failed: $*"; tail -30 $O; exit 1; }; }
-for big in 0 512; do
+for big in 0 256 512; do
   run env RAFT_HALO_BIG_MIN=$big SHAPESET=enc python tools/conv_bench.py 1
   run env RAFT_HALO_BIG_MIN=$big python tools/conv_bench.py 8 convc2,conv,zr_split,q_split,fh1
 done
