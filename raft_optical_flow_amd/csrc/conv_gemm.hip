@@ -783,6 +783,7 @@ int conv_prepare(const raft_conv2d_params* pp, ConvArgs& a, HaloOperands& o) {
   RAFT_REQUIRE(pp != nullptr, "raft_conv2d: null params");
   const raft_conv2d_params& p = *pp;
   RAFT_REQUIRE(p.in0 && p.weight && p.out, "raft_conv2d: null in0/weight/out");
+  RAFT_REQUIRE(((uintptr_t)p.weight_s & 15) == 0, "raft_conv2d: weight_s must be 16-byte aligned");
   RAFT_REQUIRE(p.batch > 0 && p.in_h > 0 && p.in_w > 0 && p.out_h > 0 && p.out_w > 0 && p.n > 0,
                "raft_conv2d: bad sizes");
   RAFT_REQUIRE(p.kh > 0 && p.kw > 0 && p.stride_h > 0 && p.stride_w > 0 && p.pad_h >= 0 && p.pad_w >= 0,
