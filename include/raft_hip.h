@@ -333,6 +333,9 @@ typedef struct raft_conv2d_params {
  * raft_conv2d_stats_slots returns slots_per_image for such a conv and 0 otherwise (raft_conv2d
  * then rejects stats_part). */
 int raft_conv2d_stats_slots(const raft_conv2d_params* p);
+/* Tile rows of the halo kernel's launch of this conv: 8 (128-pixel tiles), 16 (the multi-round
+ * 256-pixel tiles), 0 when the halo kernel does not run it (inspection / tests). */
+int raft_conv2d_halo_tile_rows(const raft_conv2d_params* p);
 /* 1 when the conv can apply its input's InstanceNorm in its loaders (in_norm above: the halo
  * kernel's 3x3 convs over <= 256 channels), else 0. */
 int raft_conv2d_in_norm_ok(const raft_conv2d_params* p);

@@ -106,6 +106,7 @@ _PROTOS = {
     "raft_conv2d": (c_int, [ctypes.POINTER(ConvParams), P]),
     "raft_conv2d_pair": (c_int, [ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), P]),
     "raft_conv2d_stats_slots": (c_int, [ctypes.POINTER(ConvParams)]),
+    "raft_conv2d_halo_tile_rows": (c_int, [ctypes.POINTER(ConvParams)]),
     "raft_conv2d_in_norm_ok": (c_int, [ctypes.POINTER(ConvParams)]),
     "raft_instnorm_merge": (c_int, [P, c_int, c_int, c_int, c_int, c_float, P, P]),
     "raft_instnorm_merge_ws_floats": (c_size_t, [c_int, c_int, c_int]),

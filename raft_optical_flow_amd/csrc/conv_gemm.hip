@@ -980,6 +980,14 @@ extern "C" int raft_conv2d_in_norm_ok(const raft_conv2d_params* pp) {
   return pp->mode == RAFT_CONV_VEC && pp->n > 4 && conv_halo_norm_ok(o) ? 1 : 0;
 }
 
+extern "C" int raft_conv2d_halo_tile_rows(const raft_conv2d_params* pp) {
+  ConvArgs a;
+  HaloOperands o;
+  if (!pp || conv_prepare(pp, a, o)) return 0;
+  if (pp->mode != RAFT_CONV_VEC || small_n(*pp)) return 0;
+  return conv_halo_tile_rows(o);
+}
+
 extern "C" int raft_conv2d_stats_slots(const raft_conv2d_params* pp) {
   ConvArgs a;
   HaloOperands o;

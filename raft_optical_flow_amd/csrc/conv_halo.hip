@@ -811,15 +811,36 @@ bool halo_problem(const HaloOperands& o, HaloArgs& a) {
 
 long halo_spatial(const HaloArgs& a) { return (long)a.p.batch * a.tx_n * a.ty_n; }
 
-// The big tiles (TH = HTH_BIG, N tile 64) for 3x3 / 1x5 / 5x1 convs whose big-tile grid still has
-// RAFT_HALO_BIG_MIN (default 256: one full round of 256 CUs) work-groups: a round of big tiles
-// does the work of two rounds of 128-pixel tiles, so from one full round on they cost no CUs;
-// below it (a frame pair's update convs) they would leave CUs idle.  f16x3 needs the scaled weight
-// (raft_conv2d_params.weight_s).  RAFT_HALO_BIG_MIN=0 turns them off.
+// The big tiles (TH = HTH_BIG, N tile 64) for 3x3 / 1x5 / 5x1 convs.  A big tile does the work of two
+// 128-pixel tiles at ~0.85-0.9 of their cost per pixel (the K loop runs closer to the MFMA rate, but
+// its prologue and the epilogue's store burst are twice as long), and every launch runs in whole
+// rounds of one work-group per CU, so the choice counts rounds: big tiles iff
+//   ceil(T_big / CUs) * RAFT_HALO_BIG_COST (1.8 = 2 x 0.9) < ceil(T_128 / CUs)
+// (tools/conv_bench.py on one box: convc2 at B=8 156.5 vs 175.1 us, 3 vs 6 rounds; fh1 at B=8
+// 116.1 vs 112.9 us, 4 vs 7 rounds; config 5's bf16 convs with 3 vs 4 and 2 vs 2 rounds 34 %
+// slower as big tiles).  RAFT_HALO_BIG_MIN=0 turns them off (default 1: no other floor).
+// f16x3 needs the scaled weight (raft_conv2d_params.weight_s).
 long halo_big_min() {
   static const long v = [] {
     const char* e = getenv("RAFT_HALO_BIG_MIN");
-    return e ? atol(e) : 256L;
+    return e ? atol(e) : 1L;
+  }();
+  return v;
+}
+double halo_big_cost() {
+  static const double v = [] {
+    const char* e = getenv("RAFT_HALO_BIG_COST");
+    return e ? atof(e) : 1.8;
+  }();
+  return v;
+}
+long halo_cus() {
+  static const long v = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      return 256L;
+    return (long)cus;
   }();
   return v;
 }
@@ -834,11 +855,20 @@ long halo_big_tiles(const HaloOperands& o) {
   const raft_conv2d_params& p = o.p;
   return (long)p.batch * cdiv(p.out_h, HTH_BIG) * cdiv(p.out_w, HTW) * (o.n_pad / 64);
 }
-// Tile rows of a conv's launch: HTH_BIG where the big tiles qualify and (the one-product modes
-// without encoder features) the 128-column tiles do not apply
+long halo_small_tiles(const HaloOperands& o) {  // 128-pixel x 64-column tiles
+  const raft_conv2d_params& p = o.p;
+  return (long)p.batch * cdiv(p.out_h, HTH) * cdiv(p.out_w, HTW) * (o.n_pad / 64);
+}
+// the rounds rule above for a launch of big_tiles vs small_tiles work-groups
+bool halo_big_pays(long big_tiles, long small_tiles) {
+  const long mn = halo_big_min(), cus = halo_cus();
+  if (mn <= 0 || big_tiles < mn) return false;
+  return (double)cdiv_l(big_tiles, cus) * halo_big_cost() < (double)cdiv_l(small_tiles, cus);
+}
+// Tile rows of a conv's launch: HTH_BIG where the big tiles qualify and pay, and (the one-product
+// modes without encoder features) the 128-column tiles do not apply
 int halo_pick_th(const HaloOperands& o, bool wide) {
-  const long mn = halo_big_min();
-  return !wide && mn > 0 && halo_big_ok(o) && halo_big_tiles(o) >= mn ? HTH_BIG : HTH;
+  return !wide && halo_big_ok(o) && halo_big_pays(halo_big_tiles(o), halo_small_tiles(o)) ? HTH_BIG : HTH;
 }
 // the big tiles' operands: spatial tiles of TH_BIG rows; f16x3 reads the scaled weight
 void halo_set_th(const HaloOperands& o, HaloArgs& a, int th) {
@@ -880,6 +910,24 @@ bool conv_halo_norm_ok(const HaloOperands& o) {
   return p.kh == 3 && p.kw == 3 && p.in0_c <= 256 && HaloCfg<3, 3, 64>::D == 3 && HaloCfg<3, 3, 32>::D == 3;
 }
 
+bool halo_wide_enabled() {
+  static const bool enabled = [] {
+    const char* e = getenv("RAFT_HALO_WIDE");
+    return !(e && e[0] == '0');
+  }();
+  return enabled;
+}
+
+// tile rows conv_halo_launch picks for the conv (HTH or HTH_BIG), 0 when the halo kernel does not run it
+int conv_halo_tile_rows(const HaloOperands& o) {
+  HaloArgs a;
+  if (!halo_enabled() || !halo_problem(o, a)) return 0;
+  const raft_conv2d_params& p = o.p;
+  const bool wide = p.precision != RAFT_PREC_F16X3 && !p.stats_part && !p.in_norm && o.n_pad % 128 == 0 &&
+                    halo_spatial(a) * (o.n_pad / 128) >= 512 && halo_wide_enabled();
+  return halo_pick_th(o, wide);
+}
+
 int conv_halo_stats_slots(const HaloOperands& o) {
   HaloArgs a;
   if (!halo_enabled() || !halo_problem(o, a)) return 0;
@@ -892,13 +940,6 @@ int conv_halo_stats_slots(const HaloOperands& o) {
 
 // Launches the halo kernel when the conv is one it covers; returns 1 without launching
 // otherwise.  Arguments are already validated by raft_conv2d.
-bool halo_wide_enabled() {
-  static const bool enabled = [] {
-    const char* e = getenv("RAFT_HALO_WIDE");
-    return !(e && e[0] == '0');
-  }();
-  return enabled;
-}
 
 int conv_halo_launch(const HaloOperands& o, hipStream_t s) {
   HaloLaunch l;
@@ -931,9 +972,9 @@ int conv_halo_launch_pair(const HaloOperands& o0, const HaloOperands& o1, hipStr
   if (!halo_enabled() || !halo_problem(o0, l.a[0]) || !halo_problem(o1, l.a[1])) return 1;
   const raft_conv2d_params &p0 = o0.p, &p1 = o1.p;
   if (p0.kh != p1.kh || p0.kw != p1.kw || p0.precision != p1.precision) return 1;
-  // the big tiles when both convs qualify and their tiles together reach RAFT_HALO_BIG_MIN
-  const long mn = halo_big_min();
-  const int th = mn > 0 && halo_big_ok(o0) && halo_big_ok(o1) && halo_big_tiles(o0) + halo_big_tiles(o1) >= mn
+  // the big tiles when both convs qualify and pay for the two together (the rounds rule)
+  const int th = halo_big_ok(o0) && halo_big_ok(o1) &&
+                         halo_big_pays(halo_big_tiles(o0) + halo_big_tiles(o1), halo_small_tiles(o0) + halo_small_tiles(o1))
                      ? HTH_BIG
                      : HTH;
   halo_set_th(o0, l.a[0], th);

@@ -68,3 +68,36 @@ def test_argument_errors_are_reported_without_launch():
     assert rc == -1 and b"multiple of 32" in lib.raft_hip_last_error()
     rc = lib.raft_convf1_flow(16, 0, 1, 8, 8, 16, None, 128, 5, 0, 16, 128, None, None)
     assert rc == -1 and b"kernel size must be 7" in lib.raft_hip_last_error()
+
+
+def test_halo_tile_rule_host_side():
+    """The halo kernel's tile choice (raft_conv2d_halo_tile_rows: host logic only, no launch): the
+    rounds rule takes the 256-pixel tiles only where ceil(T_big / CUs) * 1.8 < ceil(T_128 / CUs)
+    (256 CUs without a device): a frame pair's update convs and config 5's 1/8-res convs keep the
+    128-pixel tiles, fnet layer2 at config 2 and convc2 at B = 8 take the big ones."""
+    import ctypes
+    import torch
+    from raft_optical_flow_amd import _lib
+    from raft_optical_flow_amd import kernels as K
+    lib = _lib.load()
+    fake = 1 << 20  # 16-byte aligned stand-in pointers: the query never dereferences them
+
+    def rows(cin, cout, kh, kw, B, H, W, prec="f16x3", scaled=True):
+        pc = K.pack_conv(torch.zeros(cout, cin, kh, kw), None, 1, ((kh - 1) // 2, (kw - 1) // 2))
+        p = _lib.ConvParams()
+        p.in0, p.in0_ld, p.in0_c = fake, cin, cin
+        p.batch, p.in_h, p.in_w, p.out_h, p.out_w = B, H, W, H, W
+        p.kh, p.kw, p.stride_h, p.stride_w, p.pad_h, p.pad_w = kh, kw, 1, 1, (kh - 1) // 2, (kw - 1) // 2
+        p.mode, p.weight, p.n, p.out, p.out_ld = pc.mode, fake, cout, fake, cout
+        p.precision = _lib.PRECISIONS[prec]
+        p.weight_s = fake if (scaled and prec == "f16x3") else None
+        return lib.raft_conv2d_halo_tile_rows(ctypes.byref(p))
+
+    assert rows(256, 192, 3, 3, 1, 55, 128) == 8          # config 2 convc2 (B = 1)
+    assert rows(96, 96, 3, 3, 2, 110, 256) == 16          # fnet layer2 at config 2
+    assert rows(256, 192, 3, 3, 8, 55, 128) == 16         # convc2 at B = 8
+    assert rows(256, 192, 3, 3, 8, 55, 128, scaled=False) == 8   # f16x3 without the scaled weight
+    assert rows(128, 256, 3, 3, 8, 68, 120) == 8          # config 4's fh1: 5 vs 9 rounds
+    assert rows(256, 128, 3, 3, 1, 135, 240, "bf16") == 8  # config 5's conv (bf16): 2 vs 2 rounds
+    assert rows(256, 128, 1, 5, 8, 55, 128) == 16         # q (1x5) at B = 8
+    assert rows(64, 64, 3, 3, 1, 16, 16) == 8

@@ -56,7 +56,7 @@ def make_model(small, seed=0, alternate=False, precision=None):
     dict(cin=64, cout=64, k=3, stride=1, pad=1, H=37, W=53, B=2, mode=None),   # halo 3x3, ragged tiles
     dict(cin=96, cout=96, k=1, stride=1, pad=0, H=20, W=33, B=2, mode=None),   # halo 1x1
     dict(cin=3, cout=64, k=7, stride=2, pad=3, H=90, W=150, B=2, mode="gather"),  # the stem
-    dict(cin=64, cout=64, k=3, stride=1, pad=1, H=220, W=512, B=2, mode=None),  # big tiles (fnet layer1)
+    dict(cin=96, cout=96, k=3, stride=1, pad=1, H=110, W=256, B=2, mode=None),  # big tiles (fnet layer2)
 ])
 @pytest.mark.parametrize("prec", ["f16x3", "bf16"])
 def test_conv_epilogue_instnorm_stats(case, prec):
@@ -108,7 +108,7 @@ def test_conv_epilogue_instnorm_stats(case, prec):
 
 
 @pytest.mark.parametrize("cin,cout,H,W,B,relu", [(64, 64, 37, 53, 2, 1), (128, 96, 23, 30, 1, 0), (96, 96, 16, 16, 1, 1),
-                                                (64, 64, 220, 512, 2, 1)])   # (the last: big tiles)
+                                                (96, 96, 110, 256, 2, 1)])   # (the last: big tiles)
 @pytest.mark.parametrize("prec", ["f16x3", "bf16"])
 def test_conv_in_norm_loader(cin, cout, H, W, B, relu, prec):
     """raft_conv2d_params.in_norm: the 3x3 halo conv reads act((x - mean) * rstd) of its raw input
@@ -676,11 +676,12 @@ def test_conv_halo_wide_tiles_multi_round(cin, cout, kh, kw, H, W, prec):
 
 @pytest.mark.parametrize("prec", ["f16x3", "bf16", "f16"])
 @pytest.mark.parametrize("cin,cout,H,W,B", [
-    (64, 64, 220, 512, 2),    # fnet layer1 at config 2 (896 big tiles)
-    (256, 192, 61, 70, 8),    # ragged tiles in both axes, N padded to 256 (640 big tiles)
-    (128, 256, 68, 120, 8),   # config 4's flow-head conv1 shape
+    (96, 96, 110, 256, 2),    # fnet layer2 at config 2 (448 big tiles, N padded to 128)
+    (256, 192, 61, 70, 8),    # ragged tiles in both axes (480 big tiles)
+    (256, 192, 55, 128, 8),   # convc2 at B = 8
 ])
 def test_conv_halo_big_tiles_multi_round(cin, cout, H, W, B, prec):
+    import ctypes
     """The multi-round 3x3 halo tiles (16 x 16 pixels x 64 columns, each compute wave 2 x 2 MFMA blocks;
     f16x3 on the column-scaled weight with one accumulator) vs torch fp64 on the first and last image,
     and vs the 128-pixel tiles of the same conv (RAFT_HALO_BIG_MIN is read once per process, so the
@@ -699,6 +700,7 @@ def test_conv_halo_big_tiles_multi_round(cin, cout, H, W, B, prec):
     out = K.Rows(torch.full((B * H * W, cout + 4), -7.0, device=DEV), 0, cout)
     p = K.conv_params(pc, src, B, H, W, out, epilogue=_lib.EPI_RELU)
     assert (p.weight_s is not None) == (prec == "f16x3")
+    assert _lib.load().raft_conv2d_halo_tile_rows(ctypes.byref(p)) == 16  # the rounds rule picks big tiles
     K.conv_launch(p)(K.stream_handle())
     y = K.rows_to_nchw(out, B, H, W)
     for i in (0, B - 1):
@@ -716,8 +718,8 @@ def test_conv_halo_big_tiles_multi_round(cin, cout, H, W, B, prec):
 
 @pytest.mark.parametrize("prec", ["f16x3", "bf16", "f16"])
 @pytest.mark.parametrize("cin,cout,kh,kw,H,W,B", [
-    (256, 256, 1, 5, 68, 120, 4),   # the GRU z|r conv at config 4's map (big tiles: 1x5, 16 x 20 patch)
-    (256, 128, 5, 1, 61, 70, 8),    # q at ragged tiles (big tiles: 5x1, 20 x 16 patch)
+    (256, 128, 1, 5, 55, 128, 8),   # q (1x5) at B = 8: 512 big tiles, 16 x 20 patch
+    (256, 128, 5, 1, 50, 120, 8),   # q (5x1), ragged rows: 512 big tiles, 20 x 16 patch
 ])
 def test_conv_halo_big_tiles_1x5_5x1(cin, cout, kh, kw, H, W, B, prec):
     """1x5 / 5x1 convs on the multi-round 16 x 16 tiles vs torch fp64 (f16x3: the scaled split, D = 2 with
@@ -733,7 +735,10 @@ def test_conv_halo_big_tiles_1x5_5x1(cin, cout, kh, kw, H, W, B, prec):
     pc.precision = _lib.PRECISIONS[prec]
     src = K.Rows(K.nchw_to_rows(x.to(DEV)))
     out = K.Rows(torch.full((B * H * W, cout + 4), -7.0, device=DEV), 0, cout)
-    K.conv2d_rows(pc, src, B, H, W, out, epilogue=_lib.EPI_LINEAR)
+    import ctypes
+    p = K.conv_params(pc, src, B, H, W, out, epilogue=_lib.EPI_LINEAR)
+    assert _lib.load().raft_conv2d_halo_tile_rows(ctypes.byref(p)) == 16
+    K.conv_launch(p)(K.stream_handle())
     y = K.rows_to_nchw(out, B, H, W)
     for i in (0, B - 1):
         ref = F.conv2d(x[i:i + 1].double(), w.double(), b.double(), 1, pad)
