@@ -467,7 +467,7 @@ __device__ __noinline__ void alt_pixel_ni(const AltArgs& a, long gid, bool valid
 }
 
 #ifdef ALT_STAMPS  // dev-only phase timing (tools/alt_stamps.py with a -DALT_STAMPS variant)
-__device__ unsigned long long g_altstamp[16 * 8 * 4096];
+__device__ unsigned long long g_altstamp[24 * 8 * 4096];
 __device__ __forceinline__ unsigned long long alt_clock() {
   unsigned long long t;
   __builtin_amdgcn_sched_barrier(0);
@@ -489,7 +489,7 @@ __device__ __forceinline__ unsigned long long alt_clock() {
 template <int R>
 __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevels lvs) {
 #ifdef ALT_STAMPS
-  unsigned long long alt_t[12] = {}, alt_prev = alt_clock();
+  unsigned long long alt_t[16] = {}, alt_prev = alt_clock();
   const unsigned long long alt_start = alt_prev;
   int alt_bands = 0;
 #endif
@@ -710,11 +710,13 @@ __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevel
       if (t < NT) ts[lane * (NT + 1) + t] = tap[j];
     }
     __syncthreads();
+    ALT_ST(11);  // tap sums -> LDS + sync
     // the next level's box and first band go out before this level's binning
     if (l + 1 < lvs.n) {
       setup(l + 1, nxt);
       if (nxt.fits) load_band(l + 1, nxt, 0);
     }
+    ALT_ST(12);  // next level setup + first band issue
     // bin (core/corr.py + correlation_kernel.cu:95-116: the bilinear weights of frac(coords) over
     // each bin's four integer taps, then / scale), the arithmetic of alt_bin_store
     const float sdiv = a0.scale_div;
@@ -761,21 +763,22 @@ __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevel
         out[(bn * (RD * RD) + o) * P1 + p] = val;
       }
     }
+    ALT_ST(13);  // binning + output stores
     if (a0.range_flag && big) *a0.range_flag = 1;
     if (valid && l == 0 && a0.flow && g == 0) {
       a0.flow[((long)b * P1 + p) * a0.flow_ld + 0] = cur.x * cdiv - (float)(p % a0.W1);
       a0.flow[((long)b * P1 + p) * a0.flow_ld + 1] = cur.y * cdiv - (float)(p / a0.W1);
     }
     __syncthreads();  // the tap sums are read: the band region takes the next level
-    ALT_ST(11);  // tap sums -> LDS, binning, output stores
+    ALT_ST(14);  // flags, flow, final sync
     cur = nxt;
   }
 #ifdef ALT_STAMPS
   if (lane == 0 && blockIdx.x < 4096) {
-    unsigned long long* gs = g_altstamp + ((long)blockIdx.x * 8 + g) * 16;
-    for (int k = 0; k < 12; ++k) gs[k] = alt_t[k];
-    gs[12] = alt_clock() - alt_start;
-    gs[13] = (unsigned long long)alt_bands;
+    unsigned long long* gs = g_altstamp + ((long)blockIdx.x * 8 + g) * 24;
+    for (int k = 0; k < 16; ++k) gs[k] = alt_t[k];
+    gs[16] = alt_clock() - alt_start;
+    gs[17] = (unsigned long long)alt_bands;
   }
 #endif
 }

@@ -45,14 +45,15 @@ torch.cuda.synchronize()
 lib = _lib.load()
 lib.raft_debug_altstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 nwg = B * (-(-h // 8)) * (-(-w // 8))
-buf = np.zeros(nwg * 8 * 16, dtype=np.uint64)
+buf = np.zeros(nwg * 8 * 24, dtype=np.uint64)
 lib.raft_debug_altstamps(buf.ctypes.data, buf.size)
-st = buf.reshape(nwg, 8, 16).astype(np.float64)
+st = buf.reshape(nwg, 8, 24).astype(np.float64)
 names = ["F1 tile", "level setup + band 0 issue", "band split + store (load wait)", "sync 1", "next band issue",
-         "MFMAs", "sync 2", "S stores", "sync 3", "tap picks", "sync 4", "tap sums + binning + stores"]
-print(f"alt mfma stamps B={B} spread={spread}: {nwg} work-groups, bands per WG mean {st[:, 0, 13].mean():.2f}")
+         "MFMAs", "sync 2", "S stores", "sync 3", "tap picks", "sync 4", "tap sums -> LDS + sync",
+         "next level setup + issue", "binning + output stores", "flags, flow, final sync"]
+print(f"alt mfma stamps B={B} spread={spread}: {nwg} work-groups, bands per WG mean {st[:, 0, 17].mean():.2f}")
 for wv in (0, 7):
-    tot = st[:, wv, 12].mean()
+    tot = st[:, wv, 16].mean()
     print(f"  wave {wv}: total {tot:.0f} cyc")
     for k, n in enumerate(names):
         print(f"    {n:34s} {st[:, wv, k].mean():9.0f} cyc  {100 * st[:, wv, k].mean() / tot:5.1f} %")
