@@ -385,11 +385,11 @@ __global__ __launch_bounds__(256) void instnorm_merge_kernel(const float* part, 
   stats[2 * (b * C + c) + 1] = (float)(1.0 / sqrt(var + (double)eps));
 }
 
-// raft_instnorm_merge_ws, level 1: block (channel group of 64, image, slot group g) sums its <= 32
+// raft_instnorm_merge_ws, level 1: block (channel group of 64, image, slot group g) sums its <= 64
 // slots per channel relative to a shift K = the mean of slot 0 (sums only, no division: a fixed
 // order, deterministic): n = sum c_i, s1 = sum c_i (m_i - K), s2 = sum M2_i + c_i (m_i - K)^2.
 // Lane = channel (a wave's load of one slot is 1 KiB contiguous); wave w takes slots w, w+4, ...
-constexpr int MERGE_SPG = 32;  // slots per level-1 group (4 waves x 8 loads in flight per lane)
+constexpr int MERGE_SPG = 64;  // slots per level-1 group (4 waves x 16 loads in flight per lane)
 __global__ __launch_bounds__(256) void instnorm_merge1_kernel(const float* part, int slots, int C, int ld,
                                                               double* ws, int G) {
   __shared__ double red[4][3][64];
@@ -422,20 +422,27 @@ __global__ __launch_bounds__(256) void instnorm_merge1_kernel(const float* part,
     for (int q = 0; q < 3; ++q) o[q] = ((red[0][q][lane] + red[1][q][lane]) + red[2][q][lane]) + red[3][q][lane];
   }
 }
-// level 2: one lane per (image, channel) sums the G groups in order and writes {mean, rstd}
-__global__ __launch_bounds__(64) void instnorm_merge2_kernel(const float* part, int slots, int C, int ld,
-                                                             const double* ws, int G, float eps, float* stats) {
-  const int c = blockIdx.x * 64 + threadIdx.x, b = blockIdx.y;
-  if (c >= C) return;
-  const double K = part[((long)b * slots * ld + c) * 4 + 1];
+// level 2: block (channel group of 64, image), 16 waves: wave w sums groups w, w + 16, ... (8 loads
+// in flight per lane: one memory round trip per 128 groups), then wave 0 adds the 16 wave sums in
+// order (deterministic) and writes {mean, rstd}
+constexpr int MERGE2_WAVES = 16;
+__global__ __launch_bounds__(64 * MERGE2_WAVES) void instnorm_merge2_kernel(const float* part, int slots, int C,
+                                                                           int ld, const double* ws, int G, float eps,
+                                                                           float* stats) {
+  __shared__ double red[MERGE2_WAVES][3][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane, b = blockIdx.y;
+  const bool cok = c < C;
   double n = 0.0, s1 = 0.0, s2 = 0.0;
-  const double* p = ws + ((long)b * G * C + c) * 3;
-  for (int g0 = 0; g0 < G; g0 += 8) {
+  const double* p = ws + ((long)b * G * C + (cok ? c : 0)) * 3;
+  for (int g0 = w; g0 < G; g0 += 8 * MERGE2_WAVES) {
     double t[8][3];
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i) {
+      const int g = g0 + MERGE2_WAVES * i;
 #pragma unroll
-      for (int q = 0; q < 3; ++q) t[i][q] = g0 + i < G ? p[((long)(g0 + i) * C) * 3 + q] : 0.0;
+      for (int q = 0; q < 3; ++q) t[i][q] = (cok && g < G) ? p[((long)g * C) * 3 + q] : 0.0;
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       n += t[i][0];
@@ -443,6 +450,19 @@ __global__ __launch_bounds__(64) void instnorm_merge2_kernel(const float* part, 
       s2 += t[i][2];
     }
   }
+  red[w][0][lane] = n;
+  red[w][1][lane] = s1;
+  red[w][2][lane] = s2;
+  __syncthreads();
+  if (w != 0 || !cok) return;
+  n = s1 = s2 = 0.0;
+#pragma unroll
+  for (int k = 0; k < MERGE2_WAVES; ++k) {
+    n += red[k][0][lane];
+    s1 += red[k][1][lane];
+    s2 += red[k][2][lane];
+  }
+  const double K = part[((long)b * slots * ld + c) * 4 + 1];
   const double mean = n > 0.0 ? K + s1 / n : 0.0;
   const double m2 = n > 0.0 ? fmax(s2 - s1 * s1 / n, 0.0) : 0.0;
   const double var = n > 0.0 ? m2 / n : 0.0;
@@ -659,7 +679,7 @@ extern "C" int raft_instnorm_merge_ws(const float* part, int slots_per_image, in
   hipStream_t s = as_stream(stream);
   hipLaunchKernelGGL(instnorm_merge1_kernel, dim3(cdiv(C, 64), B, G), dim3(256), 0, s, part, slots_per_image, C,
                      stats_ld, reinterpret_cast<double*>(ws), G);
-  hipLaunchKernelGGL(instnorm_merge2_kernel, dim3(cdiv(C, 64), B), dim3(64), 0, s, part, slots_per_image, C, stats_ld,
+  hipLaunchKernelGGL(instnorm_merge2_kernel, dim3(cdiv(C, 64), B), dim3(64 * MERGE2_WAVES), 0, s, part, slots_per_image, C, stats_ld,
                      reinterpret_cast<const double*>(ws), G, eps, stats);
   return check_launch("raft_instnorm_merge_ws");
 }
