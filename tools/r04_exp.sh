@@ -21,7 +21,7 @@ run env RAFT_HIP_LIB=variants/hst/libraft_hip.so HSTAMPS=1 python tools/conv_ben
 run env RAFT_HIP_LIB=variants/hst/libraft_hip.so HSTAMPS=1 SHAPESET=enc python tools/conv_bench.py 1
 run env RAFT_HIP_LIB=variants/lcst/libraft_hip.so python tools/lc_stamps.py
 fi
-if [ -n "$ALT" ]; then  # config 3's alternate lookup: MFMA box GEMM vs the VALU tile kernel, and its phase stamps
+if [ "${ALT:-0}" != 0 ]; then  # config 3's alternate lookup: MFMA box GEMM vs the VALU tile kernel, and its phase stamps
   for sp in 0 1; do
     run python tools/alt_bench.py 8 $sp
     run env RAFT_ALT_MFMA=0 python tools/alt_bench.py 8 $sp
@@ -36,7 +36,7 @@ if [ -n "$AB_CONFIGS" ]; then  # the forward with the big tiles off, same box (A
 fi
 if [ -n "$TRACE5" ]; then  # kernel trace + phase summary of a config-5 forward (1080x1920 bf16, B=1)
   export TMPDIR=/tmp
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/fp5_${TAG} -o run --output-format csv -- python tools/fwd_profile.py 1 1080 1920 bf16 > gpurun_out/fp5_${TAG}.log 2>&1 || { echo trace5 failed; exit 1; }
+  ALT=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/fp5_${TAG} -o run --output-format csv -- python tools/fwd_profile.py 1 1080 1920 bf16 > gpurun_out/fp5_${TAG}.log 2>&1 || { echo trace5 failed; exit 1; }
   python tools/phase_summary.py gpurun_out/fp5_${TAG}/run_kernel_trace.csv > gpurun_out/phase5_${TAG}.txt 2>&1
 fi
 cat $O
