@@ -88,6 +88,15 @@ int raft_corr_build(const float* fmap1, const float* fmap2, int ld, int B, int H
  * 5x the MFMA rate).  The RAFT forward uses F16X3 unless conv_precision="fp32". */
 int raft_corr_build_prec(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C,
                          int num_levels, float sqrt_c, int precision, float* pyramid, raft_stream_t stream);
+/* raft_corr_build_prec with a workspace (the forward's build): in RAFT_PREC_F16X3 with C % 16 == 0,
+ * 64 <= C <= 1024, both fmaps are split once into f16 hi | lo maps in ws and the volume is built on
+ * 256 x 256 tiles (one fp32 accumulator chain for hi*hi, lo*hi, hi*lo; same ~2^-22 relative
+ * accuracy); otherwise it is raft_corr_build_prec.  ws: >= raft_corr_build_ws_bytes(B, H, W, C)
+ * bytes, 16-byte aligned.  RAFT_CORR_BUILD4=0: always raft_corr_build_prec. */
+size_t raft_corr_build_ws_bytes(int B, int H, int W, int C);
+int raft_corr_build_ws(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C,
+                       int num_levels, float sqrt_c, int precision, float* pyramid, void* ws, size_t ws_bytes,
+                       raft_stream_t stream);
 /* Row-major copy of one level, out [B*H*W][H_l][W_l] (the reference's corr_pyramid[l]). */
 int raft_corr_pyramid_level(const float* pyramid, int B, int H, int W, int num_levels, int level,
                             float* out, raft_stream_t stream);
@@ -336,6 +345,10 @@ int raft_conv2d_stats_slots(const raft_conv2d_params* p);
 /* Tile rows of the halo kernel's launch of this conv: 8 (128-pixel tiles), 16 (the multi-round
  * 256-pixel tiles), 0 when the halo kernel does not run it (inspection / tests). */
 int raft_conv2d_halo_tile_rows(const raft_conv2d_params* p);
+/* Tiles each work-group of the halo kernel's launch of this conv runs back to back (1, or
+ * ceil(tiles / CUs) for a launch of more tiles than CUs: the loaders run on into the next tile while
+ * the compute waves store the last one), 0 when the halo kernel does not run it (inspection / tests). */
+int raft_conv2d_halo_tiles_per_wg(const raft_conv2d_params* p);
 /* 1 when the conv can apply its input's InstanceNorm in its loaders (in_norm above: the halo
  * kernel's 3x3 convs over <= 256 channels), else 0. */
 int raft_conv2d_in_norm_ok(const raft_conv2d_params* p);

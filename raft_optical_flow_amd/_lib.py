@@ -77,6 +77,8 @@ _PROTOS = {
     "raft_corr_pyramid_floats": (c_size_t, [c_int, c_int, c_int, c_int]),
     "raft_corr_build": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, P, P]),
     "raft_corr_build_prec": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, P, P]),
+    "raft_corr_build_ws_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "raft_corr_build_ws": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, P, P, c_size_t, P]),
     "raft_corr_pyramid_level": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "raft_corr_lookup": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, c_int, c_int, P, c_int, P, P]),
     "raft_corr_lookup_convf1": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, c_int, c_int, P, c_int, P,
@@ -107,6 +109,7 @@ _PROTOS = {
     "raft_conv2d_pair": (c_int, [ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), P]),
     "raft_conv2d_stats_slots": (c_int, [ctypes.POINTER(ConvParams)]),
     "raft_conv2d_halo_tile_rows": (c_int, [ctypes.POINTER(ConvParams)]),
+    "raft_conv2d_halo_tiles_per_wg": (c_int, [ctypes.POINTER(ConvParams)]),
     "raft_conv2d_in_norm_ok": (c_int, [ctypes.POINTER(ConvParams)]),
     "raft_instnorm_merge": (c_int, [P, c_int, c_int, c_int, c_int, c_float, P, P]),
     "raft_instnorm_merge_ws_floats": (c_size_t, [c_int, c_int, c_int]),

@@ -988,6 +988,14 @@ extern "C" int raft_conv2d_halo_tile_rows(const raft_conv2d_params* pp) {
   return conv_halo_tile_rows(o);
 }
 
+extern "C" int raft_conv2d_halo_tiles_per_wg(const raft_conv2d_params* pp) {
+  ConvArgs a;
+  HaloOperands o;
+  if (!pp || conv_prepare(pp, a, o)) return 0;
+  if (pp->mode != RAFT_CONV_VEC || small_n(*pp)) return 0;
+  return conv_halo_tiles_per_wg(o);
+}
+
 extern "C" int raft_conv2d_stats_slots(const raft_conv2d_params* pp) {
   ConvArgs a;
   HaloOperands o;

@@ -40,6 +40,8 @@
 // three independent accumulator chains.  F16 (mixed precision) runs hi*hi;
 // BF16 rounds activations and weights to bf16 and runs one
 // v_mfma_f32_32x32x16_bf16 product (bf16 mixed precision).
+#include <type_traits>
+
 #include "conv_common.hpp"
 
 namespace raft {
@@ -62,10 +64,15 @@ struct HaloArgs {
 };
 
 // One launch runs the tiles of one conv, or of two independent convs of the same shape
-// class (raft_conv2d_pair): tiles [0, tiles0) are a[0]'s, the rest a[1]'s.
+// class (raft_conv2d_pair): work-groups [0, grid0) run a[0]'s tiles, the rest a[1]'s.  A work-group
+// runs up to m spatial tiles of one N-tile (halo_body): logical work-group g of a conv takes N-tile
+// g % gn and spatial tiles (g / gn) * m .. + m-1, so the gn work-groups that share a spatial tile's
+// input patch run side by side (and, xcd_tile, on one XCD) as with one tile per work-group.
 struct HaloLaunch {
   HaloArgs a[2];
-  int tiles0;
+  int sp0, sp1;  // the convs' spatial tiles
+  int m;         // spatial tiles per work-group (halo_body)
+  int grid0;     // work-groups of a[0] (gn * cdiv(sp0, m))
 };
 
 // Smallest patch ring such that chunk c's patch never lands in the slot of a
@@ -131,16 +138,35 @@ __device__ __forceinline__ unsigned long long hstamp_now() {
 }
 #endif
 
-// The tile body (one TH x 16-pixel x BNT-column tile of the conv `a`, tile index q within it; smem =
-// the work-group's LDS).  ENC: the encoder features (InstanceNorm partial statistics in the
-// epilogue, the input's InstanceNorm applied by the 3x3 loaders); separate instantiations, so the
-// update block's convs compile exactly as without them.  TH = HTH_BIG: the multi-round tiles
-// (256 pixels x 64 columns, each compute wave 64 x 64 as 2 x 2 MFMA blocks: 2/3 of the LDS
-// fragment bytes per MFMA and half the weight bytes per pixel of the 128-pixel tiles); in f16x3
-// they run on the column-scaled weight (raft_conv2d_split_weight_scaled: w*S_n = hi + lo, both
+// The tile body: N-tile nt of spatial tiles st0 .. st0 + ntl - 1 of the conv `a` (each a TH x 16-pixel x BNT-column tile;
+// smem = the work-group's LDS), one after the other.  With ntl > 1 the K loops of consecutive tiles
+// form one stream of super-steps: the loaders run D load sets ahead straight across a tile boundary
+// (the next tile's first sets land while the compute waves store the last tile's outputs), so only
+// the first tile pays the prologue and the output stores leave in the background of the next tile's
+// MFMAs instead of in one burst of every CU at once.  Each tile then runs nkp K-steps, nk rounded up
+// to lcm(U, T) so that its chunks start on the patch ring where one tile alone would (the host takes
+// ntl > 1 only where that padding is small).  ENC: the encoder features (InstanceNorm partial
+// statistics in the epilogue, the input's InstanceNorm applied by the 3x3 loaders); separate
+// instantiations, so the update block's convs compile exactly as without them.  TH = HTH_BIG: the
+// multi-round tiles (256 pixels x 64 columns, each compute wave 64 x 64 as 2 x 2 MFMA blocks: 2/3
+// of the LDS fragment bytes per MFMA and half the weight bytes per pixel of the 128-pixel tiles); in
+// f16x3 they run on the column-scaled weight (raft_conv2d_split_weight_scaled: w*S_n = hi + lo, both
 // at one scale), so the three products share ONE accumulator chain per block (SC).
+constexpr int gcd_c(int a, int b) { return b == 0 ? a : gcd_c(b, a % b); }
+// K-steps per tile of a work-group that runs several (see halo_body)
+__host__ __device__ inline int halo_nkp(int nk, int U, int T, bool multi) {
+  const int l = multi ? U / gcd_c(U, T) * T : U;
+  return cdiv(nk, l) * l;
+}
+template <int KH, int KW, int BNT, int PREC, bool ENC>
+constexpr int halo_norm_bytes(int LDS_B, int LDS_A, int D) {
+  // the input InstanceNorm tables ({mean, 1/std} per channel) of the images a work-group's tiles
+  // cover, in the LDS the rings leave (3x3 split-patch path only)
+  return (ENC && KH == 3 && KW == 3 && D == 3) ? ((HALO_LDS - LDS_B - LDS_A) & ~1023) : 0;
+}
+
 template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH>
-__device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q, char* smem) {
+__device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt, int st0, int ntl, char* smem) {
   constexpr bool X3 = PREC == RAFT_PREC_F16X3;
   constexpr bool BF = PREC == RAFT_PREC_BF16;
   using C = HaloCfg<KH, KW, BNT, X3 ? 128 : 64, TH>;
@@ -177,9 +203,8 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
   static_assert(D >= 2 && C::LDS_B + C::LDS_A <= C::LB, "LDS budget");
   static_assert(NWP >= 1 && NBI % NWP == 0, "a wave's weight pieces lie in one K-step");
   static_assert(U % 2 == 0 && (T == 1 || T >= U), "fragment parity; at most one chunk start per load set");
-  // (+ the input InstanceNorm table of the 3x3 convs: {mean, 1/std} of <= 256 channels)
-  constexpr int NORM_BYTES = (ENC && KH == 3 && KW == 3 && D == 3) ? 256 * 8 : 0;
-  static_assert(C::LDS_B + C::LDS_A + NORM_BYTES <= C::LB, "LDS budget with the norm table");
+  constexpr int NORM_BYTES = halo_norm_bytes<KH, KW, BNT, PREC, ENC>(C::LDS_B, C::LDS_A, D);
+  static_assert(NORM_BYTES == 0 || NORM_BYTES >= 256 * 8, "room for one image's norm table");
 
 #ifdef STAMPS
   const unsigned long long r_entry = hstamp_real(), c_entry = hstamp_now();
@@ -190,20 +215,33 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
   const int lw = w & 3;
   const int wc = w & 3;  // compute waves: block index
 
-  // tile (N fastest: an output tile's N-tiles share its input patch in L2)
   const HaloArgs& a = args[prob];
   const raft_conv2d_params& p = a.p;
-  const int nt = q % a.gn, st = q / a.gn;
   const int per = a.tx_n * a.ty_n;
-  const int b = st / per, sr = st - b * per;
-  const int y0 = (sr / a.tx_n) * TH, x0 = (sr % a.tx_n) * HTW;
-  const int n0 = nt * BNT;
+  // tile k of this work-group (N fastest: an output tile's N-tiles share its input patch in L2)
+  struct Tile {
+    int b, y0, x0, n0, st;
+  };
+  auto tile_at = [&](int k) {
+    Tile t;
+    t.st = st0 + k;
+    t.b = t.st / per;
+    const int sr = t.st - t.b * per;
+    t.y0 = (sr / a.tx_n) * TH;
+    t.x0 = (sr % a.tx_n) * HTW;
+    t.n0 = nt * BNT;
+    return t;
+  };
   const int nk = a.nk, nch = a.nch;
-  const int ns = (nk + U - 1) / U;
+  const int nkp = halo_nkp(nk, U, T, ntl > 1);  // K-steps per tile (multiple of U)
+  const int ns_t = nkp / U;                     // super-steps per tile
+  const int NS = ntl * ns_t;                    // super-steps of the work-group
+  const int nchp = nkp / T;                     // patch-ring chunks per tile (ntl > 1: exact)
 
   // Weight pieces of wave lw (a loader, or in the prologue the MFMA wave of the
   // same index): NWP consecutive 8-row pieces of the block of K-step ew of
-  // every load set.
+  // every load set.  Load set u (counted over the work-group's tiles) is set u % ns_t of
+  // tile u / ns_t; sets past the last tile load zeros.
   const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(p.weight, a.w_bytes);
   const int ew = (lw * NWP) / NBI, wpc0 = (lw * NWP) % NBI;
   unsigned wvoff[NWP];
@@ -211,25 +249,33 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
   for (int k = 0; k < NWP; ++k) {
     const int r = RPP * (wpc0 + k) + lane / QPR;
     const int qd = X3 ? (lane & 7) ^ ((r >> 1) & 7) : (lane & 3) ^ ((r >> 2) & 3);
-    wvoff[k] = (unsigned)(n0 + r) * ((unsigned)a.K * 4u) + (unsigned)qd * 16u;
+    wvoff[k] = (unsigned)r * ((unsigned)a.K * 4u) + (unsigned)qd * 16u;
   }
   auto issue_weights = [&](int u) {
-    const int j = U * u + ew;
-    const bool in = j < nk;
+    const int kt = u / ns_t, ul = u - kt * ns_t;
+    const int j = U * ul + ew;
+    const bool in = j < nk && kt < ntl;
     const int c = j / T, t = j - c * T;
-    const unsigned soff = in ? (unsigned)(t * nch + c) * 128u : 0u;  // packed K-step (tap, chunk)
+    const int n0 = in ? nt * BNT : 0;
+    // packed K-step (tap, chunk) of the tile's N-tile rows
+    const unsigned soff = in ? (unsigned)(t * nch + c) * 128u + (unsigned)n0 * ((unsigned)a.K * 4u) : 0u;
     char* dst = smem + (U * (u % (D + 1)) + ew) * (BNT * WROW) + wpc0 * 1024;
 #pragma unroll
     for (int k = 0; k < NWP; ++k) dma16(rs_w, dst + k * 1024, in ? wvoff[k] : OFF_INVALID, soff);
   };
 
   // the input's InstanceNorm (raft_conv2d_params.in_norm: relu((x - mean) / std) applied as the
-  // loaders split the patch): this image's table into LDS, one barrier for every wave
+  // loaders split the patch): the tables of the images of this work-group's tiles into LDS (the
+  // host checks that they fit), one barrier for every wave
   float* norm_tab = reinterpret_cast<float*>(smem + C::LDS_B + C::LDS_A);
+  int b_first = 0;
   if constexpr (NORM_BYTES > 0) {
     if (p.in_norm) {
+      b_first = tile_at(0).b;
+      const int nb = tile_at(ntl - 1).b - b_first + 1;
       if (loader)
-        for (int i = 64 * lw + lane; i < 2 * p.in0_c; i += 256) norm_tab[i] = p.in_norm[(long)b * 2 * p.in0_c + i];
+        for (int i = 64 * lw + lane; i < nb * 2 * p.in0_c; i += 256)
+          norm_tab[i] = p.in_norm[(long)b_first * 2 * p.in0_c + i];
       __syncthreads();
     }
   }
@@ -244,35 +290,40 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
     const int in0_c = p.in0_c, in1_c = p.in1_c;
     const unsigned ld0 = p.in0_ld, ld1 = p.in1_c ? p.in1_ld : p.in0_ld;
     const int in_h = p.in_h, in_w = p.in_w;
-    const unsigned pb = (unsigned)b * (unsigned)(in_h * in_w);
-    // Patch pieces of this loader: i = lw, lw+4, ... (< PI), pixels 8i .. 8i+7.
-    // Everything per lane is fixed by the tile, so the DMA addresses are
-    // precomputed once; per chunk only the channel offset changes.
-    constexpr int PK = (PI + 3) / 4;
-    unsigned ppix[PK];  // input pixel index, or OFF_INVALID outside the image / patch
-    unsigned pq4[PK];   // the lane's channel quad within a chunk (swizzled source), x 4
-#pragma unroll
-    for (int k = 0; k < PK; ++k) {
-      const int pp = 8 * (lw + 4 * k) + (lane >> 3);
+    // input pixel of patch pixel pp of tile t, or OFF_INVALID outside the image / patch
+    auto patch_pix = [&](const Tile& t, int pp) -> unsigned {
       const int py = pp / PW, px = pp - py * PW;
-      const int qd = (lane & 7) ^ ((px >> 1) & 7);
-      const int iy = y0 + py - (KH - 1) / 2, ix = x0 + px - (KW - 1) / 2;
+      const int iy = t.y0 + py - (KH - 1) / 2, ix = t.x0 + px - (KW - 1) / 2;
       const bool ok = pp < NPIX && (unsigned)iy < (unsigned)in_h && (unsigned)ix < (unsigned)in_w;
-      ppix[k] = ok ? pb + (unsigned)iy * (unsigned)in_w + (unsigned)ix : OFF_INVALID;
-      pq4[k] = 4u * (unsigned)qd;
-    }
+      return ok ? (unsigned)t.b * (unsigned)(in_h * in_w) + (unsigned)iy * (unsigned)in_w + (unsigned)ix : OFF_INVALID;
+    };
+    // the chunk starting in load set u: its tile kt and chunk c within the tile (at most one: T >= U)
+    auto set_chunk = [&](int u, int& kt, int& c) -> bool {
+      kt = u / ns_t;
+      const int ul = u - kt * ns_t;
+      c = (U * ul + T - 1) / T;
+      return kt < ntl && c * T < U * ul + U;
+    };
+    // Patch pieces of this loader: i = lw, lw+4, ... (< PI), pixels 8i .. 8i+7; per chunk the
+    // tile's pixel offsets plus the channel offset
+    constexpr int PK = (PI + 3) / 4;
     const int pcw = PI > lw ? (PI - 1 - lw) / 4 + 1 : 0;  // this wave's pieces per patch
-    auto issue_patch = [&](int c) {  // chunks past the end load zeros
+    // chunk c of tile kt into patch ring slot (kt * nchp + c) % PA (chunks past nch load zeros)
+    auto issue_patch = [&](int kt, int c) {
+      const Tile t = tile_at(kt);
       const bool s0 = 32 * c < in0_c;  // uniform: the chunk lies in one segment
       const unsigned cb = (unsigned)(s0 ? 32 * c : 32 * c - in0_c);
       const unsigned lim = (unsigned)(s0 ? in0_c : in1_c);
       const unsigned ld = s0 ? ld0 : ld1;
-      char* base = smem + C::LDS_B + (c % PA) * (PI * 1024);
+      char* base = smem + C::LDS_B + ((kt * nchp + c) % PA) * (PI * 1024);
 #pragma unroll
       for (int k = 0; k < PK; ++k) {
         if (lw + 4 * k < PI) {
-          const unsigned ch = cb + pq4[k];
-          const unsigned voff = (ppix[k] != OFF_INVALID && ch < lim) ? (ppix[k] * ld + ch) * 4u : OFF_INVALID;
+          const int pp = 8 * (lw + 4 * k) + (lane >> 3);
+          const unsigned pix = patch_pix(t, pp);
+          const unsigned qd = (unsigned)((lane & 7) ^ (((pp % PW) >> 1) & 7));
+          const unsigned ch = cb + 4u * qd;
+          const unsigned voff = (pix != OFF_INVALID && ch < lim) ? (pix * ld + ch) * 4u : OFF_INVALID;
           dma16(s0 ? rs0 : rs1, base + (lw + 4 * k) * 1024, voff, 0);
         }
       }
@@ -285,13 +336,15 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
         n = NWP;
       }
       if constexpr (T == 1) {
+        const int kt = u / ns_t, ul = u - kt * ns_t;
+        if (kt >= ntl) return n;
 #pragma unroll
-        for (int e = 0; e < U; ++e) issue_patch(U * u + e);
+        for (int e = 0; e < U; ++e) issue_patch(kt, U * ul + e);
         return n + U * pcw;
       } else {
-        const int c = (U * u + T - 1) / T;  // the chunk starting in this set, if any (zeros past nch)
-        if (c * T < U * u + U) {
-          issue_patch(c);
+        int kt, c;
+        if (set_chunk(u, kt, c)) {
+          issue_patch(kt, c);
           return n + pcw;
         }
         return n;
@@ -303,81 +356,86 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
       // the super-step that issues its load set and split + stored in the next one
       // (still a super-step before its first read; its slot was free already).
       constexpr int NT = 4 * NPIX, TI = (NT + 255) / 256;
-      unsigned tpix[TI];  // input pixel, or OFF_INVALID
-      unsigned tg8[TI];   // channel offset 8g within the chunk
-      int tlds[TI];       // byte offset of the task's hi quad in a patch slot (lo: ^ 64), -1 past NT
+      const unsigned tg8 = 8u * (unsigned)(lane & 3);  // channel offset 8g within the chunk (g = t & 3 = lane & 3)
+      int tlds[TI];  // byte offset of the task's hi quad in a patch slot (lo: ^ 64), -1 past NT
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         const int t = 64 * lw + lane + 256 * i;
         const int pp = t >> 2, g = t & 3;
-        const int py = pp / PW, px = pp - py * PW;
-        const int iy = y0 + py - (KH - 1) / 2, ix = x0 + px - (KW - 1) / 2;
-        const bool ok = t < NT && (unsigned)iy < (unsigned)in_h && (unsigned)ix < (unsigned)in_w;
-        tpix[i] = ok ? pb + (unsigned)iy * (unsigned)in_w + (unsigned)ix : OFF_INVALID;
-        tg8[i] = 8u * (unsigned)g;
+        const int px = pp % PW;
         tlds[i] = t < NT ? pp * 128 + ((g ^ ((px >> 1) & 7)) << 4) : -1;
       }
       using Staged = f32x4[TI][2];
-      auto load_patch = [&](int c, Staged& dst) {  // chunks past the end load zeros
+      auto load_patch = [&](int kt, int c, Staged& dst) {  // chunks past the end load zeros
+        const Tile tt = tile_at(kt);
         const bool s0 = 32 * c < in0_c;
         const unsigned cb = (unsigned)(s0 ? 32 * c : 32 * c - in0_c);
         const unsigned lim = (unsigned)(s0 ? in0_c : in1_c);
         const unsigned ld = s0 ? ld0 : ld1;
 #pragma unroll
-        for (int i = 0; i < TI; ++i)
+        for (int i = 0; i < TI; ++i) {
+          const unsigned pix = patch_pix(tt, (64 * lw + lane + 256 * i) >> 2);
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
-            const unsigned ch = cb + tg8[i] + 4u * q;
-            const unsigned voff = (tpix[i] != OFF_INVALID && ch < lim) ? (tpix[i] * ld + ch) * 4u : OFF_INVALID;
+            const unsigned ch = cb + tg8 + 4u * q;
+            const unsigned voff = (pix != OFF_INVALID && ch < lim) ? (pix * ld + ch) * 4u : OFF_INVALID;
             dst[i][q] = buf_load4<0>(s0 ? rs0 : rs1, voff, 0);
           }
+        }
       };
       const bool nrm = NORM_BYTES > 0 && p.in_norm != nullptr;
-      auto store_patch = [&](int c, const Staged& src) {
-        char* base = smem + C::LDS_B + (c % PA) * (PI * 1024);
+      auto store_patch = [&](int kt, int c, const Staged& src) {
+        char* base = smem + C::LDS_B + ((kt * nchp + c) % PA) * (PI * 1024);
         const bool s0 = 32 * c < in0_c;  // (the norm applies to segment 0)
+        if (nrm && s0) {
+          const Tile tt = tile_at(kt);
+          const float2* tab = reinterpret_cast<const float2*>(norm_tab) + (tt.b - b_first) * in0_c;
 #pragma unroll
-        for (int i = 0; i < TI; ++i) {
-          if (tlds[i] >= 0) {
-            h8 hi, lo;
-            if (nrm && s0) {
+          for (int i = 0; i < TI; ++i) {
+            if (tlds[i] >= 0) {
               // channels 32c + 8g .. +7: (x - mean) * rstd, relu; padding (no pixel, or past in0_c) stays 0
-              const int ch = 32 * c + (int)tg8[i];
+              const bool pix_ok = patch_pix(tt, (64 * lw + lane + 256 * i) >> 2) != OFF_INVALID;
+              const int ch = 32 * c + (int)tg8;
               float e[8] = {src[i][0][0], src[i][0][1], src[i][0][2], src[i][0][3],
                             src[i][1][0], src[i][1][1], src[i][1][2], src[i][1][3]};
 #pragma unroll
               for (int j = 0; j < 8; ++j) {
-                const bool ok = tpix[i] != OFF_INVALID && ch + j < in0_c;
-                const float2 mr = reinterpret_cast<const float2*>(norm_tab)[ok ? ch + j : 0];
+                const bool ok = pix_ok && ch + j < in0_c;
+                const float2 mr = tab[ok ? ch + j : 0];
                 const float v = (e[j] - mr.x) * mr.y;
                 e[j] = ok ? (p.in_norm_relu ? fmaxf(v, 0.f) : v) : 0.f;
               }
+              h8 hi, lo;
               split8<X3, BF>(f32x4{e[0], e[1], e[2], e[3]}, f32x4{e[4], e[5], e[6], e[7]}, hi, lo);
-            } else {
-              split8<X3, BF>(src[i][0], src[i][1], hi, lo);
+              *reinterpret_cast<h8*>(base + tlds[i]) = hi;
+              if constexpr (X3) *reinterpret_cast<h8*>(base + (tlds[i] ^ 64)) = lo;
             }
+          }
+          return;
+        }
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          if (tlds[i] >= 0) {
+            h8 hi, lo;
+            split8<X3, BF>(src[i][0], src[i][1], hi, lo);
             *reinterpret_cast<h8*>(base + tlds[i]) = hi;
             if constexpr (X3) *reinterpret_cast<h8*>(base + (tlds[i] ^ 64)) = lo;
           }
         }
       };
-      // the chunk starting in load set u, or -1 (at most one: T >= U)
-      auto chunk_of = [&](int u) {
-        const int c = (U * u + T - 1) / T;
-        return c * T < U * u + U ? c : -1;
-      };
       constexpr int PMAX = (U * D + T - 1) / T + 1;  // chunk starts in the prologue's sets
       Staged pv[PMAX];
-      int pcs[PMAX];
+      int pks[PMAX], pcs[PMAX];
       int nst = 0;
 #pragma unroll
       for (int u = 0; u < D; ++u) {
-        const int c = chunk_of(u);
-        if (c >= 0) {
+        int kt, c;
+        if (set_chunk(u, kt, c)) {
 #pragma unroll
           for (int k = 0; k < PMAX; ++k)
             if (k == nst) {
-              load_patch(c, pv[k]);
+              load_patch(kt, c, pv[k]);
+              pks[k] = kt;
               pcs[k] = c;
             }
           ++nst;
@@ -386,31 +444,32 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
       wait_vm<0>();
 #pragma unroll
       for (int k = 0; k < PMAX; ++k)
-        if (k < nst) store_patch(pcs[k], pv[k]);
+        if (k < nst) store_patch(pks[k], pcs[k], pv[k]);
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the patches are in LDS
       __builtin_amdgcn_s_barrier();
       // Super-step s: store the patch loaded in super-step s-1, load the patch
       // and issue the weights of set s+D, wait until set s+2's weights (issued
       // in s-1) have landed, barrier.
-      int pend = -1;  // chunk staged in pv[0], loaded during the previous super-step
-      for (int s = 0; s < ns; ++s) {
-        if (pend >= 0) {
+      int pend_k = -1, pend_c = 0;  // chunk staged in pv[0], loaded during the previous super-step
+      for (int s = 0; s < NS; ++s) {
+        if (pend_k >= 0) {
           wait_vm<NWP>();  // that patch's loads (the weights issued after them may fly on)
-          store_patch(pend, pv[0]);
-          pend = -1;
+          store_patch(pend_k, pend_c, pv[0]);
+          pend_k = -1;
         }
         int nnew = 0;
-        if (s + D < ns) {
-          const int c = chunk_of(s + D);
-          if (c >= 0) {
-            load_patch(c, pv[0]);
-            pend = c;
+        if (s + D < NS) {
+          int kt, c;
+          if (set_chunk(s + D, kt, c)) {
+            load_patch(kt, c, pv[0]);
+            pend_k = kt;
+            pend_c = c;
             nnew = 2 * TI;
           }
           issue_weights(s + D);
           nnew += NWP;
         }
-        wait_vm_n(s + 1 < ns ? nnew : 0);
+        wait_vm_n(s + 1 < NS ? nnew : 0);
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): a patch stored this super-step is in LDS
         __builtin_amdgcn_s_barrier();
       }
@@ -434,12 +493,12 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
       for (int k = 0; k < NH; ++k) hist[k] = k < D - 3 ? cnt[D - 1 - k] : 0;
     }
     __builtin_amdgcn_s_barrier();
-    for (int s = 0; s < ns; ++s) {
-      const int nnew = s + D < ns ? issue_set(s + D, true) : 0;
+    for (int s = 0; s < NS; ++s) {
+      const int nnew = s + D < NS ? issue_set(s + D, true) : 0;
       int n = D >= 3 ? nnew : 0;  // in flight after set s+2: sets s+3 .. s+D
 #pragma unroll
       for (int k = 0; k < D - 3; ++k) n += hist[k];
-      wait_vm_n(s + 1 < ns ? n : 0);  // nothing may land after the last barrier
+      wait_vm_n(s + 1 < NS ? n : 0);  // nothing may land after the last barrier
       __builtin_amdgcn_s_barrier();  // set s+2 readable by every wave
 #pragma unroll
       for (int k = NH - 1; k > 0; --k) hist[k] = hist[k - 1];
@@ -459,14 +518,17 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
   // accx: the hi * (2048 lo) chain of the unscaled f16x3 form (not used by SC or one-product modes)
   constexpr int AXF = X3 && !SC ? MF : 1, AXS = X3 && !SC ? NSUB : 1;
   f32x16 acc[MF][NSUB], accx[AXF][AXS];
+  auto clear_acc = [&]() {
 #pragma unroll
-  for (int f = 0; f < MF; ++f)
+    for (int f = 0; f < MF; ++f)
 #pragma unroll
-    for (int sb = 0; sb < NSUB; ++sb) acc[f][sb] = f32x16{};
+      for (int sb = 0; sb < NSUB; ++sb) acc[f][sb] = f32x16{};
 #pragma unroll
-  for (int f = 0; f < AXF; ++f)
+    for (int f = 0; f < AXF; ++f)
 #pragma unroll
-    for (int sb = 0; sb < AXS; ++sb) accx[f][sb] = f32x16{};
+      for (int sb = 0; sb < AXS; ++sb) accx[f][sb] = f32x16{};
+  };
+  clear_acc();
   // Fragment reads run ahead of the MFMAs: the B fragments of K-step j+1 and
   // the A (activation) values of K-step j+2 are read while K-step j's MFMAs
   // run, and A of j+1 (read one K-step earlier) is split to f16 behind them,
@@ -588,12 +650,70 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
       }
     }
   };
+  // the fragments of a tile's first K-step (its K-step 0 is the next to read)
+  Frag F[2];
+  auto first_frags = [&]() {
+    if constexpr (LSPLIT) {
+      read_b(F[0]);
+      read_a_split(F[0]);
+    } else {
+      read_a();
+      read_b(F[0]);
+      split_a(F[0]);
+      read_a();
+    }
+  };
+  // the tile's outputs (register r of block f holds row m = (r&3) + 8(r>>2) + 4h of its 32 pixels)
+  auto epilogue = [&](const Tile& t) {
+    if constexpr (SC) {  // undo the column scale S_n (a power of two: exact)
+#pragma unroll
+      for (int sb = 0; sb < NSUB; ++sb) {
+        const float is = a.inv_scale[t.n0 + cb + sb * 32 + m];
+#pragma unroll
+        for (int f = 0; f < MF; ++f)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[f][sb][r] *= is;
+      }
+    } else if constexpr (X3) {
+#pragma unroll
+      for (int f = 0; f < MF; ++f)
+#pragma unroll
+        for (int sb = 0; sb < NSUB; ++sb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[f][sb][r] += accx[f][sb][r] * (1.0f / SPLIT_SCALE);
+    }
+    f32x4 stv[NSUB];  // ENC: the wave's InstanceNorm partials per column (its MF blocks combined)
+#pragma unroll
+    for (int f = 0; f < MF; ++f) {
+      int rows[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mm = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int y = t.y0 + 2 * (wm * MF + f) + (mm >> 4), x = t.x0 + (mm & 15);
+        rows[r] = (y < p.out_h && x < p.out_w) ? (t.b * p.out_h + y) * p.out_w + x : -1;
+      }
+#pragma unroll
+      for (int sb = 0; sb < NSUB; ++sb) tile_epilogue<false>(p, rows, t.n0 + cb + sb * 32 + m, acc[f][sb]);
+      if constexpr (ENC) {
+        if (p.stats_part) {  // InstanceNorm partials of the raw output, per wave (slot: spatial tile x 4 + wave)
+#pragma unroll
+          for (int sb = 0; sb < NSUB; ++sb) {
+            const int n = t.n0 + sb * 32 + m;
+            const f32x4 v = tile_stats_vals(rows, acc[f][sb], p.bias ? p.bias[n < p.n ? n : 0] : 0.f);
+            stv[sb] = f == 0 ? v : stats_combine(stv[sb], v);
+            if (f == MF - 1) stats_write(p, n, (long)t.st * 4 + w, stv[sb]);
+          }
+        }
+      }
+    }
+  };
 
   // ---- compute waves: pipeline ---------------------------------------------
   // Super-step s runs K-steps Us .. Us+U-1 (its reads reach K-step U(s+1)+1,
   // all in load sets s and s+1), then one barrier.  K-steps past nk (up to
-  // U*ns) run on zero weights and zero patches: they add exact zeros, and the
-  // loop body has no branches.
+  // nkp) run on zero weights and zero patches: they add exact zeros, and the
+  // loop body has no branches.  A tile's last super-step reads nothing ahead
+  // (the next tile's first fragments are read after its epilogue).
 #pragma unroll
   for (int u = 0; u < D; ++u) issue_weights(u);
   wait_vm<NWP * (D - 2)>();      // the weights of sets 0 and 1 (sets 2 .. D-1: before the first loop barrier)
@@ -601,28 +721,23 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
 #ifdef HALO_PRIO
   __builtin_amdgcn_s_setprio(HALO_PRIO);
 #endif
-  Frag F[2];
-  if constexpr (LSPLIT) {
-    read_b(F[0]);
-    read_a_split(F[0]);
-  } else {
-    read_a();
-    read_b(F[0]);
-    split_a(F[0]);
-    read_a();
-  }
+  first_frags();
 #ifdef STAMPS
-  unsigned long long t_cmp = 0, t_wait = 0, t_bar = 0, t0 = hstamp_now();
+  unsigned long long t_cmp = 0, t_wait = 0, t_bar = 0, t_epi = 0, t0 = hstamp_now();
   const unsigned long long c_loop = t0;
 #endif
-  for (int s = 0; s < ns; ++s) {
+  // one super-step's K-steps; LAST: the tile's last super-step, which reads nothing ahead
+  auto superstep = [&](auto last_tag) {
+    constexpr bool LAST = decltype(last_tag)::value;
 #pragma unroll
     for (int e = 0; e < U; ++e) {
 #ifdef HALO_ABL_MFMAONLY  // timing ablation (dev builds only): MFMAs on fragments read once
       mfma_step(F[e & 1]);
       asm volatile("" ::"v"(F[0].ah[0][0]), "v"(F[1].ah[0][0]));
 #else
-      if constexpr (LSPLIT) {
+      if (LAST && e == U - 1) {
+        mfma_step(F[e & 1]);
+      } else if constexpr (LSPLIT) {
         read_b(F[(e + 1) & 1]);
         read_a_split(F[(e + 1) & 1]);
         mfma_step(F[e & 1]);
@@ -634,12 +749,16 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
       }
 #endif
     }
+  };
+  bool first = true;
+  auto step_end = [&]() {
 #ifdef STAMPS
     unsigned long long t2 = hstamp_now();
     t_cmp += t2 - t0;
 #endif
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the next fragments are in registers
-    if (s == 0) wait_vm<0>();             // the prologue's weight sets 2 .. D-1 (this wave's only VMEM)
+    if (first) wait_vm<0>();              // the prologue's weight sets 2 .. D-1 (this wave's only DMAs)
+    first = false;
 #ifdef STAMPS
     unsigned long long t3 = hstamp_now();
     t_wait += t3 - t2;
@@ -649,52 +768,34 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
     t0 = hstamp_now();
     t_bar += t0 - t3;
 #endif
-  }
-
+  };
+  for (int kt = 0; kt < ntl; ++kt) {
+    for (int sl = 0; sl + 1 < ns_t; ++sl) {
+      superstep(std::false_type{});
+      step_end();
+    }
+    superstep(std::true_type{});
+    step_end();
+    // (non-LSPLIT: av already holds the next tile's K-step 0, read one K-step ahead)
+    __builtin_amdgcn_sched_barrier(0);
+    epilogue(tile_at(kt));
+    clear_acc();
+    __builtin_amdgcn_sched_barrier(0);
+    // the next tile's first fragments (after the last tile: reads of ring slots nobody uses,
+    // unconditional so that no path keeps the old fragments live through the epilogue)
+    if constexpr (LSPLIT) {
+      read_b(F[0]);
+      read_a_split(F[0]);
+    } else {
+      read_b(F[0]);
+      split_a(F[0]);
+      read_a();
+    }
 #ifdef STAMPS
-  const unsigned long long c_epi = hstamp_now();
+    const unsigned long long t4 = hstamp_now();
+    t_epi += t4 - t0;
+    t0 = t4;
 #endif
-  if constexpr (SC) {  // undo the column scale S_n (a power of two: exact)
-#pragma unroll
-    for (int sb = 0; sb < NSUB; ++sb) {
-      const float is = a.inv_scale[n0 + cb + sb * 32 + m];
-#pragma unroll
-      for (int f = 0; f < MF; ++f)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[f][sb][r] *= is;
-    }
-  } else if constexpr (X3) {
-#pragma unroll
-    for (int f = 0; f < MF; ++f)
-#pragma unroll
-      for (int sb = 0; sb < NSUB; ++sb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[f][sb][r] += accx[f][sb][r] * (1.0f / SPLIT_SCALE);
-  }
-  // ---- epilogue: register r of block f holds row m = (r&3) + 8(r>>2) + 4h of its 32 pixels
-  f32x4 stv[NSUB];  // ENC: the wave's InstanceNorm partials per column (its MF blocks combined)
-#pragma unroll
-  for (int f = 0; f < MF; ++f) {
-    int rows[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int mm = (r & 3) + 8 * (r >> 2) + 4 * h;
-      const int y = y0 + 2 * (wm * MF + f) + (mm >> 4), x = x0 + (mm & 15);
-      rows[r] = (y < p.out_h && x < p.out_w) ? (b * p.out_h + y) * p.out_w + x : -1;
-    }
-#pragma unroll
-    for (int sb = 0; sb < NSUB; ++sb) tile_epilogue<false>(p, rows, n0 + cb + sb * 32 + m, acc[f][sb]);
-    if constexpr (ENC) {
-      if (p.stats_part) {  // InstanceNorm partials of the raw output, per wave (slot: spatial tile x 4 + wave)
-#pragma unroll
-        for (int sb = 0; sb < NSUB; ++sb) {
-          const int n = n0 + sb * 32 + m;
-          const f32x4 v = tile_stats_vals(rows, acc[f][sb], p.bias ? p.bias[n < p.n ? n : 0] : 0.f);
-          stv[sb] = f == 0 ? v : stats_combine(stv[sb], v);
-          if (f == MF - 1) stats_write(p, n, (long)st * 4 + w, stv[sb]);
-        }
-      }
-    }
   }
 #ifdef STAMPS
   {
@@ -707,23 +808,28 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int q,
       g[2] = c_loop - c_entry;
       g[3] = t_cmp;
       g[4] = t_wait + t_bar;
-      g[5] = c_exit - c_epi;
+      g[5] = t_epi;
       g[6] = c_exit - c_entry;
     }
   }
 #endif
 }
 
-// One conv (or an independent pair, raft_conv2d_pair) per launch: one tile per work-group.
+// One conv (or an independent pair, raft_conv2d_pair) per launch: work-group g runs tiles
+// N-tile g % gn of spatial tiles (g / gn) * m .. + m-1 of its conv (the pair's first grid0
+// work-groups take a[0]'s tiles).
 template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH>
 __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
   using C = HaloCfg<KH, KW, BNT, PREC == RAFT_PREC_F16X3 ? 128 : 64, TH>;
-  constexpr int NORM_BYTES = (ENC && KH == 3 && KW == 3 && C::D == 3) ? 256 * 8 : 0;
+  constexpr int NORM_BYTES = halo_norm_bytes<KH, KW, BNT, PREC, ENC>(C::LDS_B, C::LDS_A, C::D);
   __shared__ __attribute__((aligned(1024))) char smem[C::LDS_B + C::LDS_A + NORM_BYTES];
-  int q = xcd_tile(blockIdx.x, gridDim.x);
-  const int prob = q >= hl.tiles0 ? 1 : 0;
-  q -= prob * hl.tiles0;
-  halo_body<KH, KW, BNT, PREC, ENC, TH>(hl.a, prob, q, smem);
+  int g = xcd_tile(blockIdx.x, gridDim.x);
+  const int prob = g >= hl.grid0 ? 1 : 0;
+  g -= prob * hl.grid0;
+  const int gn = hl.a[prob].gn;
+  const int st0 = (g / gn) * hl.m;
+  const int ntl = min(hl.m, (prob ? hl.sp1 : hl.sp0) - st0);
+  halo_body<KH, KW, BNT, PREC, ENC, TH>(hl.a, prob, g % gn, st0, ntl, smem);
 }
 
 template <int KH, int KW, int PREC>
@@ -879,9 +985,79 @@ void halo_set_th(const HaloOperands& o, HaloArgs& a, int th) {
   }
 }
 
-void launch_halo(const HaloLaunch& l, int bn, int th, long tiles, hipStream_t s) {
+// LDS left for the input-norm tables of a 3x3 ENC instantiation (halo_norm_bytes)
+template <int BNT, int WR, int TH>
+long halo_norm_cap_t() {
+  using C = HaloCfg<3, 3, BNT, WR, TH>;
+  return halo_norm_bytes<3, 3, BNT, RAFT_PREC_F16X3, true>(C::LDS_B, C::LDS_A, C::D);
+}
+long halo_norm_cap(int bn, int prec, int th) {
+  const bool x3 = prec == RAFT_PREC_F16X3;
+  if (th == HTH_BIG) return x3 ? halo_norm_cap_t<64, 128, HTH_BIG>() : halo_norm_cap_t<64, 64, HTH_BIG>();
+  if (bn == 64) return x3 ? halo_norm_cap_t<64, 128, HTH>() : halo_norm_cap_t<64, 64, HTH>();
+  return x3 ? halo_norm_cap_t<32, 128, HTH>() : halo_norm_cap_t<32, 64, HTH>();
+}
+
+// Tiles per work-group (halo_body): a launch with more tiles than CUs may run m spatial tiles per
+// work-group, the m of least cost in tile times (below), where padding every tile's K loop to
+// lcm(U, T) K-steps costs at most 1/8 and the input-norm tables of the images a work-group covers
+// fit its LDS; otherwise one tile per work-group.  RAFT_HALO_MT=0: always one.
+bool halo_mt_enabled() {
+  static const bool enabled = [] {
+    const char* e = getenv("RAFT_HALO_MT");
+    return !(e && e[0] == '0');
+  }();
+  return enabled;
+}
+double halo_mt_cost() {
+  static const double v = [] {
+    const char* e = getenv("RAFT_HALO_MT_COST");
+    return e ? atof(e) : 0.8;
+  }();
+  return v;
+}
+bool halo_mt_ok(const HaloArgs& a, int bn, int th, long m) {
+  const int T = a.p.kh * a.p.kw, U = (bn == 32 && T > 1) ? 4 : 2;
+  const int n1 = halo_nkp(a.nk, U, T, false), nm = halo_nkp(a.nk, U, T, true);
+  if ((long)(nm - n1) * 8 > n1) return false;
+  if (a.p.in_norm) {
+    const long per_img = (long)a.tx_n * a.ty_n;
+    const long imgs = cdiv_l(m, per_img) + 1;
+    if (imgs * a.p.in0_c * 8 > halo_norm_cap(bn, a.p.precision, th)) return false;
+  }
+  return true;
+}
+// sets l.m (spatial tiles per work-group) and l.grid0 for the launch of l.a[0] (and l.a[1] of a
+// pair, pair = true); returns the grid size
+long halo_plan_grid(HaloLaunch& l, int bn, int th, bool pair) {
+  const long cus = halo_cus();
+  const long s0 = halo_spatial(l.a[0]), s1 = pair ? halo_spatial(l.a[1]) : 0;
+  const long g0 = l.a[0].gn, g1 = pair ? l.a[1].gn : 0;
+  auto wgs = [&](long m) { return g0 * cdiv_l(s0, m) + g1 * cdiv_l(s1, m); };
+  // cost in tile times: rounds of work-groups x (the first tile + RAFT_HALO_MT_COST per later tile:
+  // the prologue and the output stores of the later tiles run under the K loops)
+  long m = 1;
+  if (halo_mt_enabled() && wgs(1) > cus) {
+    const double f = halo_mt_cost();
+    double best = (double)cdiv_l(wgs(1), cus);
+    for (long c = 2; c <= 64; ++c) {
+      const double cost = (double)cdiv_l(wgs(c), cus) * (1.0 + f * (double)(c - 1));
+      if (cost < best && halo_mt_ok(l.a[0], bn, th, c) && (!pair || halo_mt_ok(l.a[1], bn, th, c))) {
+        best = cost;
+        m = c;
+      }
+    }
+  }
+  l.m = (int)m;
+  l.sp0 = (int)s0;
+  l.sp1 = (int)s1;
+  l.grid0 = (int)(g0 * cdiv_l(s0, m));
+  return wgs(m);
+}
+
+void launch_halo(const HaloLaunch& l, int bn, int th, long wgs, hipStream_t s) {
   const raft_conv2d_params& p = l.a[0].p;
-  dim3 grid((unsigned)tiles);
+  dim3 grid((unsigned)wgs);
   if (p.kh == 1 && p.kw == 1)
     launch_halo_k<1, 1>(l, bn, th, grid, s);
   else if (p.kh == 3)
@@ -938,12 +1114,10 @@ int conv_halo_stats_slots(const HaloOperands& o) {
   return a.tx_n * cdiv(o.p.out_h, th) * 4;
 }
 
-// Launches the halo kernel when the conv is one it covers; returns 1 without launching
-// otherwise.  Arguments are already validated by raft_conv2d.
-
-int conv_halo_launch(const HaloOperands& o, hipStream_t s) {
-  HaloLaunch l;
-  if (!halo_enabled() || !halo_problem(o, l.a[0])) return 1;
+// the launch of one conv: operands, N-tile width, tile rows and grid size; false when the halo
+// kernel does not cover the conv
+static bool halo_plan(const HaloOperands& o, HaloLaunch& l, int& bn, int& th, long& wgs) {
+  if (!halo_enabled() || !halo_problem(o, l.a[0])) return false;
   const long spatial = halo_spatial(l.a[0]);
   const raft_conv2d_params& p = o.p;
   // one work-group per CU (LDS): 64 output channels per work-group unless
@@ -952,15 +1126,33 @@ int conv_halo_launch(const HaloOperands& o, hipStream_t s) {
   // leaves two rounds of work-groups (configs 3 - 5; RAFT_HALO_WIDE=0: never)
   const bool wide = p.precision != RAFT_PREC_F16X3 && !p.stats_part && !p.in_norm && o.n_pad % 128 == 0 &&
                     spatial * (o.n_pad / 128) >= 512 && halo_wide_enabled();
-  const int th = halo_pick_th(o, wide);
-  const int bn = th == HTH_BIG ? 64 : wide ? 128 : spatial * (o.n_pad / 64) > 128 ? 64 : 32;
+  th = halo_pick_th(o, wide);
+  bn = th == HTH_BIG ? 64 : wide ? 128 : spatial * (o.n_pad / 64) > 128 ? 64 : 32;
   halo_set_th(o, l.a[0], th);
   l.a[0].gn = o.n_pad / bn;
   const long tiles = halo_spatial(l.a[0]) * l.a[0].gn;
-  if (tiles >= (1L << 31)) return 1;
+  if (tiles >= (1L << 31)) return false;
   l.a[1] = l.a[0];
-  l.tiles0 = (int)tiles;
-  launch_halo(l, bn, th, tiles, s);
+  wgs = halo_plan_grid(l, bn, th, false);
+  return true;
+}
+
+// tiles per work-group of the conv's halo launch (halo_body), 0 when the halo kernel does not run it
+int conv_halo_tiles_per_wg(const HaloOperands& o) {
+  HaloLaunch l;
+  int bn, th;
+  long wgs;
+  return halo_plan(o, l, bn, th, wgs) ? l.m : 0;
+}
+
+// Launches the halo kernel when the conv is one it covers; returns 1 without launching
+// otherwise.  Arguments are already validated by raft_conv2d.
+int conv_halo_launch(const HaloOperands& o, hipStream_t s) {
+  HaloLaunch l;
+  int bn, th;
+  long wgs;
+  if (!halo_plan(o, l, bn, th, wgs)) return 1;
+  launch_halo(l, bn, th, wgs, s);
   return 0;
 }
 
@@ -986,8 +1178,7 @@ int conv_halo_launch_pair(const HaloOperands& o0, const HaloOperands& o1, hipStr
   l.a[1].gn = o1.n_pad / bn;
   const long t0 = s0 * l.a[0].gn, tiles = t0 + s1 * l.a[1].gn;
   if (tiles >= (1L << 31)) return 1;
-  l.tiles0 = (int)t0;
-  launch_halo(l, bn, th, tiles, s);
+  launch_halo(l, bn, th, halo_plan_grid(l, bn, th, true), s);
   return 0;
 }
 

@@ -405,6 +405,287 @@ __global__ __launch_bounds__(512, 2) void corr_build2_kernel(CorrBuildArgs a) {
   }
 }
 
+// K2 on 256 x 256 tiles from pre-split maps (raft_corr_build_ws, the forward's f16x3 build).
+// corr_build2 reads one LDS fragment per MFMA (its MFMA and LDS pipes both run at about half
+// rate) and moves 16 B of fmap rows from L2 per output; here a work-group computes C^T for 256
+// target pixels (a 16 x 16 block of (h2, w2)) x 256 query pixels: 0.5 fragment reads per MFMA
+// and 8 B per output.
+//   * Maps: corr_split4_kernel writes each fmap row as C/16 half-steps of 64 B (16 f16 hi | 16 f16
+//     lo = f16(x - hi)), the same 4 B per channel as fp32, so a half-step of a 256-pixel tile is a
+//     32 KiB LDS-DMA (buffer_load ... lds, lane-linear 16-B writes, the 16-B quads XOR-swizzled by
+//     (row >> 1) & 3 on the source side: conflict-free fragment reads).  4 stages of (targets |
+//     queries) = 128 KiB, issued 3 half-steps ahead by all 8 waves (4 DMAs each per half-step).
+//   * Waves: wm = w & 3 takes target rows 4wm .. 4wm+3 of the block (2 MFMA blocks of 4 x 8
+//     pixels), wn = w >> 2 takes 128 queries (4 blocks); per half-step 12 ds_read_b128, 24 MFMAs
+//     (hi*hi, lo*hi, hi*lo of every block in ONE fp32 chain; no block's MFMAs back to back).
+//   * Epilogue from registers: MFMA row m of a 4 x 8 block is target pixel (4wm + m/8, 8c + 4((m/4)&1)
+//     + m%4), so lane (query, h) holds a whole 4x4 level-0 tile, register r = tile element r: four
+//     16-B stores; the tile pools in registers to half a level-1 tile row pair, swapped with lane
+//     ^32 so each lane stores one 16-B level-1 tile row.
+//   * Persistent: work-group g runs units g, g + grid, ... (unit = image, query tile, target tile;
+//     target tiles fastest, so the running work-groups share a query tile in L2); the DMAs run on
+//     into the next unit while the last one's outputs are stored.
+constexpr int CB4_T = 256;                      // targets and queries per unit
+constexpr int CB4_ROW = 64;                     // bytes per (pixel, half-step) row
+constexpr int CB4_STAGE = 2 * CB4_T * CB4_ROW;  // one half-step of targets | queries: 32 KiB
+constexpr int CB4_NS = 4;                       // stages (3 half-steps in flight)
+
+struct CB4Args {
+  const char* s1;  // split query map  [B*P][C/16][64 B]
+  const char* s2;  // split target map
+  unsigned sbytes; // bytes of one split map
+  int H, W, P, nh;  // nh = C / 16 half-steps
+  float sqrt_c;
+  float* pyr;
+  Level l0, l1;
+  int nt;
+  int qt, ttx, tt;  // query tiles per image; target tiles along w2; target tiles per image
+  long units;       // B * qt * tt
+  f32x4* sink;      // 4 KiB the epilogue's lanes without an output store to (every store
+                    // instruction issues, so a wave's vmcnt after an epilogue is known)
+};
+
+__global__ __launch_bounds__(256) void corr_split4_kernel(const float* __restrict__ f, int ld, long npix, int C,
+                                                          char* __restrict__ out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;  // (pixel, group of 4 channels)
+  const int ng = C / 4;
+  if (i >= npix * ng) return;
+  const long px = i / ng;
+  const int g = (int)(i - px * ng);
+  const f32x4 v = *reinterpret_cast<const f32x4*>(f + px * ld + 4 * g);
+  h4 hi, lo;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const _Float16 h = (_Float16)v[e];
+    hi[e] = h;
+    lo[e] = (_Float16)(v[e] - (float)h);
+  }
+  char* r = out + px * (long)C * 4 + (g >> 2) * CB4_ROW + (g & 3) * 8;
+  *reinterpret_cast<h4*>(r) = hi;
+  *reinterpret_cast<h4*>(r + 32) = lo;
+}
+
+#ifdef CB4_STAMPS  // dev-only phase timing (tools/cb4_stamps.py with a -DCB4_STAMPS variant)
+__device__ unsigned long long g_cb4stamp[8 * 8 * 1024];
+__device__ __forceinline__ unsigned long long cb4_clock() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define CB4_ST(k)                       \
+  do {                                  \
+    const unsigned long long n_ = cb4_clock(); \
+    cb4_t[k] += n_ - cb4_prev;          \
+    cb4_prev = n_;                      \
+  } while (0)
+#else
+#define CB4_ST(k)
+#endif
+
+template <bool L1>
+__global__ __launch_bounds__(512) void corr_build4_kernel(CB4Args a) {
+#ifdef CB4_STAMPS
+  unsigned long long cb4_t[6] = {}, cb4_prev = cb4_clock();
+  const unsigned long long cb4_start = cb4_prev;
+  int cb4_units = 0;
+#endif
+  // store instructions of one epilogue per wave: 2 x 4 blocks x (4 level-0 + 1 level-1 row)
+  constexpr int NSTORE = 8 * (4 + (L1 ? 1 : 0));
+  __shared__ __attribute__((aligned(1024))) char smem[CB4_NS * CB4_STAGE];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = w & 3, wn = w >> 2;
+  const int m = lane & 31, h = lane >> 5;
+  const long grid = gridDim.x;
+  const unsigned rowb = (unsigned)a.nh * CB4_ROW;  // bytes per pixel row of a split map
+  const __amdgpu_buffer_rsrc_t rq = make_rsrc(a.s1, a.sbytes), rt = make_rsrc(a.s2, a.sbytes);
+  struct Unit {
+    int b, q0, ty0, tx0;  // image, first query, first target row / column
+  };
+  auto unit_at = [&](long u) {
+    Unit t;
+    const long per = (long)a.qt * a.tt;
+    t.b = (int)(u / per);
+    const long r = u - (long)t.b * per;
+    const int qi = (int)(r / a.tt), ti = (int)(r - (long)qi * a.tt);
+    t.q0 = qi * CB4_T;
+    t.ty0 = (ti / a.ttx) * 16;
+    t.tx0 = (ti % a.ttx) * 16;
+    return t;
+  };
+  // DMA k (0..3) of this wave per half-step: instruction i = w + 8k moves LDS rows 16i .. 16i+15
+  // (rows 0..255 targets, 256..511 queries); lane: row 16i + lane/4, physical quad lane & 3
+  unsigned voff[4];
+  auto set_offsets = [&](const Unit& t) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int row = 16 * (w + 8 * k) + (lane >> 2);
+      const unsigned lq = (unsigned)((lane & 3) ^ ((row >> 1) & 3));
+      bool ok;
+      long px;
+      if (k < 2) {  // target row R = 64 wm' + 32 c + m'
+        const int R = row, mm = R & 31, c = (R >> 5) & 1;
+        const int h2 = t.ty0 + 4 * (R >> 6) + (mm >> 3), w2 = t.tx0 + 8 * c + 4 * ((mm >> 2) & 1) + (mm & 3);
+        ok = h2 < a.H && w2 < a.W;
+        px = (long)t.b * a.P + (long)h2 * a.W + w2;
+      } else {
+        const int p1 = t.q0 + row - CB4_T;
+        ok = p1 < a.P;
+        px = (long)t.b * a.P + p1;
+      }
+      voff[k] = ok ? (unsigned)px * rowb + lq * 16u : OFF_INVALID;
+    }
+  };
+  const long total = a.units;
+  long u_is = blockIdx.x;  // unit of the next DMA
+  int s_is = 0;            // its half-step
+  long g_is = 0;           // global half-step counter of the next DMA (stage g % 4)
+  if (u_is >= total) return;
+  set_offsets(unit_at(u_is));
+  auto issue = [&]() {  // the next half-step's DMAs (zeros past the last unit)
+    const bool live = u_is < total;
+    char* st = smem + (g_is % CB4_NS) * CB4_STAGE;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      dma16(k < 2 ? rt : rq, st + (w + 8 * k) * 1024, live ? voff[k] : OFF_INVALID, (unsigned)s_is * CB4_ROW);
+    ++g_is;
+    if (++s_is == a.nh) {
+      s_is = 0;
+      u_is += grid;
+      if (u_is < total) set_offsets(unit_at(u_is));
+    }
+  };
+  issue();
+  issue();
+  issue();
+  const int arow0 = wm * 64 + m, brow0 = CB4_T + wn * 128 + m;
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[c][j] = f32x16{};
+  long g = 0;
+  int since = 3;  // half-steps since the last epilogue (3: none in flight)
+  for (long u = blockIdx.x; u < total; u += grid) {
+    for (int s = 0; s < a.nh; ++s, ++g, ++since) {
+      // this wave's DMAs of half-step g (those of the two younger half-steps may fly; in the three
+      // half-steps after an epilogue its NSTORE stores, younger than g's DMAs, may fly too)
+      CB4_ST(5);  // loop overhead
+      if (since <= 2)
+        wait_vm<8 + NSTORE>();
+      else
+        wait_vm<8>();
+      CB4_ST(0);  // DMA wait
+      // every wave's: stage g % 4 readable, stage (g - 1) % 4 free (the asm's memory clobber keeps
+      // the compiler from moving this step's LDS reads above the barrier)
+      asm volatile("s_barrier" ::: "memory");
+      CB4_ST(1);  // barrier
+      issue();  // half-step g + 3
+      CB4_ST(2);  // DMA issue
+      const char* st = smem + (g % CB4_NS) * CB4_STAGE;
+      h8 ah[2], al[2], bh[4], bl[4];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int row = arow0 + 32 * c, sw = (row >> 1) & 3;
+        ah[c] = *reinterpret_cast<const h8*>(st + row * CB4_ROW + ((h ^ sw) << 4));
+        al[c] = *reinterpret_cast<const h8*>(st + row * CB4_ROW + (((2 + h) ^ sw) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = brow0 + 32 * j, sw = (row >> 1) & 3;
+        bh[j] = *reinterpret_cast<const h8*>(st + row * CB4_ROW + ((h ^ sw) << 4));
+        bl[j] = *reinterpret_cast<const h8*>(st + row * CB4_ROW + (((2 + h) ^ sw) << 4));
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[c][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], bh[j], acc[c][j], 0, 0, 0);
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[c][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[c], bh[j], acc[c][j], 0, 0, 0);
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[c][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[c], bl[j], acc[c][j], 0, 0, 0);
+      CB4_ST(3);  // fragment reads + MFMAs
+    }
+    // ---- epilogue: level-0 tiles and level-1 rows of unit u from registers
+    const Unit t = unit_at(u);
+    const int ty = t.ty0 / 4 + wm;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p1 = t.q0 + wn * 128 + j * 32 + m;
+      const bool qok = p1 < a.P;
+      const long qb = (long)t.b * a.P + (qok ? p1 : 0);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int tx = t.tx0 / 4 + 2 * c + h;
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = acc[c][j][r] / a.sqrt_c;
+        {
+          const bool ok = qok && ty < a.l0.th && tx < a.l0.tw;
+          f32x4* dst = ok ? reinterpret_cast<f32x4*>(a.pyr + a.l0.off + qb * a.l0.mapsz + ((long)ty * a.l0.tw + tx) * 16)
+                          : a.sink + 4 * lane;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f32x4 x = {v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+            if (a.nt)
+              __builtin_nontemporal_store(x, dst + q);
+            else
+              dst[q] = x;
+          }
+        }
+        if constexpr (L1) {
+          // level-1 values (y1, x1) = (2 ty + ya, 2 tx + xb): avg_pool2d's window order, zeros past h1 x w1
+          float pv[2][2];
+#pragma unroll
+          for (int ya = 0; ya < 2; ++ya)
+#pragma unroll
+            for (int xb = 0; xb < 2; ++xb) {
+              const float s = ((v[8 * ya + 2 * xb] + v[8 * ya + 2 * xb + 1]) + v[8 * ya + 4 + 2 * xb]) + v[8 * ya + 4 + 2 * xb + 1];
+              const bool in = 2 * ty + ya < a.l1.h && 2 * tx + xb < a.l1.w;
+              pv[ya][xb] = in ? s / 4.0f : 0.f;
+            }
+          // lane h writes level-1 tile row 2 (ty & 1) + h: columns 0,1 from lane h = 0, 2,3 from h = 1
+          const float o0 = __shfl_xor(pv[1 - h][0], 32), o1 = __shfl_xor(pv[1 - h][1], 32);
+          const f32x4 row4 = h == 0 ? f32x4{pv[0][0], pv[0][1], o0, o1} : f32x4{o0, o1, pv[1][0], pv[1][1]};
+          const int ty1 = ty >> 1, tx1 = tx >> 1;
+          const bool ok = qok && ty1 < a.l1.th && tx1 < a.l1.tw;
+          f32x4* dst = ok ? reinterpret_cast<f32x4*>(a.pyr + a.l1.off + qb * a.l1.mapsz +
+                                                     ((long)ty1 * a.l1.tw + tx1) * 16 + (2 * (ty & 1) + h) * 4)
+                          : a.sink + 4 * lane;
+          if (a.nt)
+            __builtin_nontemporal_store(row4, dst);
+          else
+            *dst = row4;
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[c][j] = f32x16{};
+    since = 0;
+    CB4_ST(4);  // epilogue
+#ifdef CB4_STAMPS
+    ++cb4_units;
+#endif
+  }
+  wait_vm<0>();  // (the DMAs past the last unit load zeros; nothing may land after exit)
+#ifdef CB4_STAMPS
+  if (lane == 0 && blockIdx.x < 1024) {
+    unsigned long long* gs = g_cb4stamp + ((long)blockIdx.x * 8 + w) * 8;
+    for (int k = 0; k < 6; ++k) gs[k] = cb4_t[k];
+    gs[6] = cb4_clock() - cb4_start;
+    gs[7] = (unsigned long long)cb4_units;
+  }
+#endif
+}
+
 // Level l -> l+1 2x2 average pool (floor), tiled -> tiled, zeros in the padding.
 __global__ void pool2_tiled_kernel(const float* pyr, float* out_base, long n_maps, Level src,
                                    Level dst) {
@@ -1031,6 +1312,91 @@ extern "C" int raft_corr_build_prec(const float* fmap1, const float* fmap2, int 
     hipLaunchKernelGGL(pool2_tiled_kernel, dim3(grid_for(n)), dim3(256), 0, s, pyramid, pyramid, (long)B * P, lv[l - 1],
                        lv[l]);
     rc = check_launch("raft_corr_build(pool)");
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+#ifdef CB4_STAMPS
+extern "C" int raft_debug_cb4stamps(unsigned long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_cb4stamp), sizeof(unsigned long long) * (size_t)n);
+}
+#endif
+
+extern "C" size_t raft_corr_build_ws_bytes(int B, int H, int W, int C) {
+  if (B <= 0 || H <= 0 || W <= 0 || C <= 0) return 0;
+  return 2 * (size_t)B * H * W * C * 4 + 4096;  // the two split maps + the epilogue sink
+}
+
+extern "C" int raft_corr_build_ws(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C, int L,
+                                  float sqrt_c, int precision, float* pyramid, void* ws, size_t ws_bytes,
+                                  raft_stream_t stream) {
+  using namespace raft;
+  static const bool on = [] {
+    const char* e = getenv("RAFT_CORR_BUILD4");
+    return !(e && e[0] == '0');
+  }();
+  const long P = (long)H * W;
+  // the 256 x 256 kernel: f16x3, C a multiple of 16 with >= 4 half-steps, 32-bit map offsets
+  const bool fits = precision == RAFT_PREC_F16X3 && C % 16 == 0 && C >= 64 && C <= 1024 && ld % 4 == 0 &&
+                    ld >= C && (double)B * P * C * 4 < 2147483648.0;
+  if (!on || !fits) return raft_corr_build_prec(fmap1, fmap2, ld, B, H, W, C, L, sqrt_c, precision, pyramid, stream);
+  RAFT_REQUIRE(fmap1 && fmap2 && pyramid && ws, "raft_corr_build_ws: null pointer");
+  RAFT_REQUIRE(B > 0 && H > 0 && W > 0 && L >= 1 && L <= LK_MAXL, "raft_corr_build_ws: bad sizes");
+  RAFT_REQUIRE(ws_bytes >= raft_corr_build_ws_bytes(B, H, W, C), "raft_corr_build_ws: workspace too small "
+               "(raft_corr_build_ws_bytes)");
+  RAFT_REQUIRE((((uintptr_t)fmap1 | (uintptr_t)fmap2 | (uintptr_t)pyramid | (uintptr_t)ws) & 15) == 0,
+               "raft_corr_build_ws: fmaps, pyramid and workspace must be 16-byte aligned");
+  Level lv[LK_MAXL];
+  RAFT_REQUIRE(pyramid_levels(B, H, W, L, lv), "raft_corr_build_ws: a pyramid level is empty (%dx%d, %d levels)", H,
+               W, L);
+  hipStream_t s = as_stream(stream);
+  const size_t map_bytes = (size_t)B * P * C * 4;
+  char* s1 = static_cast<char*>(ws);
+  char* s2 = s1 + map_bytes;
+  const long nq = (long)B * P * (C / 4);
+  hipLaunchKernelGGL(corr_split4_kernel, dim3((unsigned)cdiv_l(nq, 256)), dim3(256), 0, s, fmap1, ld, (long)B * P, C, s1);
+  hipLaunchKernelGGL(corr_split4_kernel, dim3((unsigned)cdiv_l(nq, 256)), dim3(256), 0, s, fmap2, ld, (long)B * P, C, s2);
+  int rc = check_launch("raft_corr_build_ws(split)");
+  if (rc) return rc;
+  CB4Args a;
+  a.s1 = s1;
+  a.s2 = s2;
+  a.sbytes = (unsigned)map_bytes;
+  a.H = H;
+  a.W = W;
+  a.P = (int)P;
+  a.nh = C / 16;
+  a.sqrt_c = sqrt_c;
+  a.pyr = pyramid;
+  a.l0 = lv[0];
+  a.l1 = lv[L > 1 ? 1 : 0];
+  {
+    const char* e = getenv("RAFT_CORR_NT");
+    const double l0_bytes = 4.0 * B * (double)P * lv[0].mapsz;
+    a.nt = e && (e[0] == '0' || e[0] == '1') ? e[0] == '1' : l0_bytes > 512.0 * 1024 * 1024;
+  }
+  a.qt = (int)cdiv_l(P, CB4_T);
+  a.ttx = cdiv(W, 16);
+  a.tt = cdiv(H, 16) * a.ttx;
+  a.units = (long)B * a.qt * a.tt;
+  a.sink = reinterpret_cast<f32x4*>(s2 + map_bytes);
+  int cus = 256, dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    cus = 256;
+  const dim3 grid((unsigned)(a.units < cus ? a.units : cus));  // one work-group per CU (128 KiB LDS), persistent
+  if (L > 1)
+    hipLaunchKernelGGL(corr_build4_kernel<true>, grid, dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL(corr_build4_kernel<false>, grid, dim3(512), 0, s, a);
+  rc = check_launch("raft_corr_build_ws");
+  if (rc) return rc;
+  for (int l = 2; l < L; ++l) {
+    const long n = (long)B * P * lv[l].mapsz;
+    hipLaunchKernelGGL(pool2_tiled_kernel, dim3(grid_for(n)), dim3(256), 0, s, pyramid, pyramid, (long)B * P, lv[l - 1],
+                       lv[l]);
+    rc = check_launch("raft_corr_build_ws(pool)");
     if (rc) return rc;
   }
   return 0;

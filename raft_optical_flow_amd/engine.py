@@ -653,8 +653,11 @@ class RaftPlan:
             # the correlation GEMM follows the conv arithmetic: exact f32 MFMA in "fp32"
             # mode, the fp32-accurate f16 split otherwise (raft_hip.h)
             cprec = _lib.PREC_FP32 if pk.precision == _lib.PREC_FP32 else _lib.PREC_F16X3
-            L.append(Launch("raft_corr_build_prec", fmap1.data_ptr(), fmap2.data_ptr(), C, B, h, w, C, lv, div,
-                            cprec, self.pyramid.data_ptr()))
+            # (f16x3: fmaps split once into the workspace, the volume on 256 x 256 tiles: raft_hip.h)
+            wsb = int(_lib.load().raft_corr_build_ws_bytes(B, h, w, C))
+            self.corr_ws = A.flat((wsb + 3) // 4)
+            L.append(Launch("raft_corr_build_ws", fmap1.data_ptr(), fmap2.data_ptr(), C, B, h, w, C, lv, div,
+                            cprec, self.pyramid.data_ptr(), self.corr_ws.data_ptr(), wsb))
         else:
             # AlternateCorrBlock pools num_levels times (core/corr.py:157-161); the
             # last level is never used, but its existence is the reference's size check.

@@ -101,3 +101,34 @@ def test_halo_tile_rule_host_side():
     assert rows(256, 128, 3, 3, 1, 135, 240, "bf16") == 8  # config 5's conv (bf16): 2 vs 2 rounds
     assert rows(256, 128, 1, 5, 8, 55, 128) == 16         # q (1x5) at B = 8
     assert rows(64, 64, 3, 3, 1, 16, 16) == 8
+
+
+def test_halo_tiles_per_work_group_host_side():
+    """Spatial tiles per work-group of the halo launch (raft_conv2d_halo_tiles_per_wg: host logic
+    only): the m of least rounds x (1 + 0.8 (m - 1)) tile times over 256 CUs, where padding each
+    tile's K loop to lcm(U, T) K-steps costs at most 1/8."""
+    import ctypes
+    import torch
+    from raft_optical_flow_amd import _lib
+    from raft_optical_flow_amd import kernels as K
+    lib = _lib.load()
+    fake = 1 << 20
+
+    def mt(cin, cout, kh, kw, B, H, W, prec="f16x3"):
+        pc = K.pack_conv(torch.zeros(cout, cin, kh, kw), None, 1, ((kh - 1) // 2, (kw - 1) // 2))
+        p = _lib.ConvParams()
+        p.in0, p.in0_ld, p.in0_c = fake, cin, cin
+        p.batch, p.in_h, p.in_w, p.out_h, p.out_w = B, H, W, H, W
+        p.kh, p.kw, p.stride_h, p.stride_w, p.pad_h, p.pad_w = kh, kw, 1, 1, (kh - 1) // 2, (kw - 1) // 2
+        p.mode, p.weight, p.n, p.out, p.out_ld = pc.mode, fake, cout, fake, cout
+        p.precision = _lib.PRECISIONS[prec]
+        p.weight_s = fake if prec == "f16x3" else None
+        return lib.raft_conv2d_halo_tiles_per_wg(ctypes.byref(p))
+
+    assert mt(256, 192, 3, 3, 1, 55, 128) == 1        # a frame pair's convc2: one round
+    assert mt(64, 64, 3, 3, 2, 220, 512) == 7         # fnet layer1 at config 2: 1792 tiles
+    assert mt(96, 96, 3, 3, 2, 110, 256) == 1         # 3 chunks of 9 taps: 27 -> 36 K-steps, too much padding
+    assert mt(128, 128, 3, 3, 2, 55, 128) == 1        # fnet layer3 at config 2: 224 tiles, one round
+    assert mt(256, 192, 3, 3, 8, 55, 128) == 1        # convc2 at B = 8: 3 rounds of big tiles beat 4 per work-group
+    assert mt(256, 192, 3, 3, 1, 135, 240) == 3       # config 5's convc2: 255 spatial tiles x 3 N-tiles
+    assert mt(128, 256, 3, 3, 8, 68, 120) == 9        # config 4's fh1: 576 spatial tiles x 4 N-tiles

@@ -38,3 +38,72 @@ def test_corr_build_tile_order_bit_identical(monkeypatch, order):
     monkeypatch.setenv("RAFT_CB_ORDER", order)
     got = _build(f1, f2, C, B, H, W, C, L)
     assert torch.equal(got, ref)
+
+
+def _build_ws(f1, f2, ld, B, H, W, C, L, pad=None):
+    from raft_optical_flow_amd import _lib
+    from raft_optical_flow_amd import kernels as K
+    pyr = torch.full((K.pyramid_floats(B, H, W, L),), float("nan") if pad is None else pad, device=DEV)
+    wsb = int(_lib.load().raft_corr_build_ws_bytes(B, H, W, C))
+    ws = torch.full(((wsb + 3) // 4,), float("nan"), device=DEV)
+    _lib.call("raft_corr_build_ws", f1.data_ptr(), f2.data_ptr(), ld, B, H, W, C, L, K.sqrt_c(C), _lib.PREC_F16X3,
+              pyr.data_ptr(), ws.data_ptr(), wsb, K.stream_handle())
+    torch.cuda.synchronize()
+    return pyr
+
+
+@pytest.mark.parametrize("B,H,W,C,L,ld", [
+    (1, 55, 128, 256, 4, 256),   # config 2's map: 28 query tiles x 32 target tiles
+    (2, 37, 53, 256, 4, 256),    # ragged target blocks, odd sizes (level-1 padding rows / columns)
+    (1, 20, 36, 96, 2, 100),     # C = 96 (6 half-steps), ld > C, H = 20 (level-1 tile rows past H / 2)
+    (3, 9, 70, 64, 1, 64),       # one level only (no level-1 stores), 4 half-steps
+])
+def test_corr_build_ws_vs_fp64(B, H, W, C, L, ld):
+    """raft_corr_build_ws (split maps + corr_build4_kernel: 256 x 256 tiles, one accumulator chain,
+    stores from registers): every level within 1e-5 of its scale of fp64 (the oracle's algorithm,
+    core/corr.py:25-54, 96-127), padding zeros written (the buffer starts as NaN), level 1 the
+    exact avg_pool2d of the kernel's own level 0."""
+    import numpy as np
+    from oracle import raft_oracle as O
+    from raft_optical_flow_amd import _lib
+    from raft_optical_flow_amd import kernels as K
+    g = torch.Generator().manual_seed(B * H + W)
+    x1 = torch.randn(B, C, H, W, generator=g)
+    x2 = torch.randn(B, C, H, W, generator=g)
+    r1 = torch.zeros(B * H * W, ld)
+    r2 = torch.zeros(B * H * W, ld)
+    r1[:, :C] = x1.permute(0, 2, 3, 1).reshape(-1, C)
+    r2[:, :C] = x2.permute(0, 2, 3, 1).reshape(-1, C)
+    r1, r2 = r1.to(DEV), r2.to(DEV)
+    pyr = _build_ws(r1, r2, ld, B, H, W, C, L)
+    assert not bool(torch.isnan(pyr).any()), "a pyramid element was not written"
+    ref = O.corr_pyramid(x1.double().numpy(), x2.double().numpy(), L)
+    dims = K.pyramid_dims(H, W, L)
+    levels = []
+    for i, (lh, lw) in enumerate(dims):
+        out = torch.empty(B * H * W, lh, lw, device=DEV)
+        _lib.call("raft_corr_pyramid_level", pyr.data_ptr(), B, H, W, L, i, out.data_ptr(), K.stream_handle())
+        levels.append(out.cpu())
+        scale = max(1.0, float(np.abs(ref[i]).max()))
+        assert float(np.abs(out.cpu().double().numpy().reshape(ref[i].shape) - ref[i]).max()) < 1e-5 * scale, i
+    if L > 1:
+        l0 = levels[0]
+        h1, w1 = dims[1]
+        a = l0[:, 0:2 * h1:2, 0:2 * w1:2] + l0[:, 0:2 * h1:2, 1:2 * w1:2]
+        a = (a + l0[:, 1:2 * h1:2, 0:2 * w1:2]) + l0[:, 1:2 * h1:2, 1:2 * w1:2]
+        assert torch.equal(levels[1], a / 4.0)
+
+
+def test_corr_build_ws_matches_the_plain_build():
+    """The workspace build and raft_corr_build_prec(F16X3) agree to the split's accuracy (different
+    accumulation orders of the same products), and the workspace build is run to run bit-identical."""
+    from raft_optical_flow_amd import _lib
+    B, H, W, C, L = 1, 55, 128, 256, 4
+    g = torch.Generator(device=DEV).manual_seed(3)
+    f = torch.randn(2 * B * H * W, C, device=DEV, generator=g)
+    f1, f2 = f[: B * H * W], f[B * H * W:]
+    a = _build_ws(f1, f2, C, B, H, W, C, L)
+    b = _build(f1, f2, C, B, H, W, C, L)
+    assert float((a - b).abs().max()) < 1e-5 * max(1.0, float(b.abs().max()))
+    assert torch.equal(_build_ws(f1, f2, C, B, H, W, C, L, pad=0.0), a)
+    assert _lib.load().raft_corr_build_ws_bytes(B, H, W, C) == 2 * B * H * W * C * 4 + 4096

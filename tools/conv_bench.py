@@ -33,7 +33,7 @@ tot_t = 0
 for name, cin, cout, kh, kw, pad in SHAPES:
     if ONLY and name not in ONLY:
         continue
-    Bq, H, W = DIMS.get(name, (B, 55, 128))
+    Bq, H, W = DIMS.get(name, (B, int(__import__("os").environ.get("CB_H", 55)), int(__import__("os").environ.get("CB_W", 128))))
     x = torch.randn(Bq * H * W, cin, device=dev)
     w = torch.randn(cout, cin, kh, kw) * 0.05
     pc = K.pack_conv(w, torch.zeros(cout), 1, pad, device=dev)
