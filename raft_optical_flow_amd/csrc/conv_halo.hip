@@ -1018,6 +1018,11 @@ double halo_mt_cost() {
 }
 bool halo_mt_ok(const HaloArgs& a, int bn, int th, long m) {
   const int T = a.p.kh * a.p.kw, U = (bn == 32 && T > 1) ? 4 : 2;
+  // measured (profiles/r04mt3_experiments.txt, config 5's update convs at 135x240): the one-product
+  // modes' 3x3 convs with several N-tiles ran 18-30 % slower on multi-tile work-groups (their short
+  // K loops do not cover the next tile's loads beside the last one's stores); their 1x1 / 1x5 convs
+  // and every f16x3 conv gained
+  if (a.p.precision != RAFT_PREC_F16X3 && T == 9 && a.gn > 1) return false;
   const int n1 = halo_nkp(a.nk, U, T, false), nm = halo_nkp(a.nk, U, T, true);
   if ((long)(nm - n1) * 8 > n1) return false;
   if (a.p.in_norm) {

@@ -627,16 +627,30 @@ __global__ __launch_bounds__(512) void corr_build4_kernel(CB4Args a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] = acc[c][j][r] / a.sqrt_c;
         {
-          const bool ok = qok && ty < a.l0.th && tx < a.l0.tw;
-          f32x4* dst = ok ? reinterpret_cast<f32x4*>(a.pyr + a.l0.off + qb * a.l0.mapsz + ((long)ty * a.l0.tw + tx) * 16)
-                          : a.sink + 4 * lane;
+          // the quad's four queries' tiles transposed by 16-B rows (lane q of the quad gets row q of
+          // each): store i writes query 4k + i's tile, its rows from the quad's 4 lanes and the
+          // adjacent tile (tx + 1) from lanes + 32, so 8 lanes fill one 128-B run (scattered 16-B
+          // stores, one cache line per lane, ran the epilogue at a lane per clock)
+          float rt[4][4];  // rt[e][i]: element e of row (lane & 3) of query 4k + i's tile
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const f32x4 x = {v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+          for (int e = 0; e < 4; ++e) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) rt[e][i] = v[4 * i + e];
+            quad_transpose(rt[e]);
+          }
+          const int qr = lane & 3;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int pi = t.q0 + wn * 128 + j * 32 + (m & ~3) + i;
+            const bool ok = pi < a.P && ty < a.l0.th && tx < a.l0.tw;
+            f32x4* dst = ok ? reinterpret_cast<f32x4*>(a.pyr + a.l0.off + ((long)t.b * a.P + pi) * a.l0.mapsz +
+                                                       ((long)ty * a.l0.tw + tx) * 16) + qr
+                            : a.sink + 4 * lane + i;
+            const f32x4 x = {rt[0][i], rt[1][i], rt[2][i], rt[3][i]};
             if (a.nt)
-              __builtin_nontemporal_store(x, dst + q);
+              __builtin_nontemporal_store(x, dst);
             else
-              dst[q] = x;
+              *dst = x;
           }
         }
         if constexpr (L1) {

@@ -21,6 +21,8 @@ import sys
 base = sys.argv[1]
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RND = os.environ.get("PMC_ROUND", "r04")  # <out>/<round>_*_pmc.json
+OUTD = os.environ.get("PMC_OUT", os.path.join(ROOT, "profiles"))  # (on a GPU box: gpurun_out, then copy)
 
 
 def sha(name):
@@ -78,7 +80,7 @@ if lk_f:
 sfx = "" if B == 1 else f"_b{B}"
 # (the standalone lookup kernel only runs in the forward without the fused launch: RAFT_FUSE_CONVC1=0)
 if lk_f:
-    json.dump(res, open(os.path.join(ROOT, "profiles", f"r03_lookup_pmc{sfx}.json"), "w"), indent=1)
+    json.dump(res, open(os.path.join(OUTD, f"{RND}_lookup_pmc{sfx}.json"), "w"), indent=1)
 print(json.dumps(res, indent=1))
 
 halo = {"source_sha": sha("conv_halo.hip"),
@@ -93,7 +95,7 @@ for k, v in per.items():
     halo[k] = {"dispatches": len(v), "mfma_busy": round(statistics.mean(x[0] for x in v), 4),
                "mfma_busy_cycles_avg": round(statistics.mean(x[1] for x in v)),
                "gui_active_cycles_avg": round(statistics.mean(x[2] for x in v))}
-json.dump(halo, open(os.path.join(ROOT, "profiles", f"r03_halo_pmc{sfx}.json"), "w"), indent=1)
+json.dump(halo, open(os.path.join(OUTD, f"{RND}_halo_pmc{sfx}.json"), "w"), indent=1)
 print(json.dumps(halo, indent=1))
 
 # the forward's fused lookup launch (raft_corr_lookup_conv): window reads + coords + flow in,
@@ -112,5 +114,5 @@ if lc_f:
           "l2_hit_rate": round(sum(c["TCC_HIT_sum"] for c in lhit) / max(1.0, sum(c["TCC_HIT_sum"] + c["TCC_MISS_sum"] for c in lhit)), 4)}
     lc["hbm_bytes_per_launch"] = lc["hbm_read_bytes_per_launch"] + lc["hbm_write_bytes_per_launch"]
     lc["traffic_over_algorithmic"] = round(lc["hbm_bytes_per_launch"] / (a_r + a_w), 3)
-    json.dump(lc, open(os.path.join(ROOT, "profiles", f"r03_lookup_conv_pmc{sfx}.json"), "w"), indent=1)
+    json.dump(lc, open(os.path.join(OUTD, f"{RND}_lookup_conv_pmc{sfx}.json"), "w"), indent=1)
     print(json.dumps(lc, indent=1))
