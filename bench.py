@@ -112,6 +112,37 @@ def inforward_launch_us(plan, name):
     return sum(a.elapsed_time(b) for a, b in pairs) / len(pairs) * 1e3, len(pairs)
 
 
+def inforward_span_us(plan):
+    """Per-dispatch duration of the forward's fused lookup launches (raft_corr_lookup_conv) as they
+    run in the forward: the library's launch-span timing (raft_debug_launch_span: the device
+    realtime counter at each launch's first work-group start and last work-group end) over one
+    eager forward enqueued behind a GPU spin, so its kernels run back to back as in the graph
+    replay.  Returns (mean us, launches) or None."""
+    import ctypes
+    from raft_optical_flow_amd import _lib
+    from raft_optical_flow_amd import kernels as K
+    main = torch.cuda.current_stream()
+    side = plan.side_stream or torch.cuda.Stream(device=plan.device)
+    torch.cuda.synchronize()
+    _lib.call("raft_debug_launch_span", 1)
+    try:
+        torch.cuda._sleep(100_000_000)
+        for l in plan.launches:
+            if l is K.FORK:
+                side.wait_stream(main)
+            elif l is K.JOIN:
+                main.wait_stream(side)
+            else:
+                l(side.cuda_stream if l.side else main.cuda_stream)
+        torch.cuda.synchronize()
+        buf = (ctypes.c_ulonglong * 512)()
+        _lib.call("raft_debug_launch_span_read", buf, 512)
+    finally:
+        _lib.call("raft_debug_launch_span", 0)
+    spans = [(buf[2 * k + 1] - buf[2 * k]) * 0.01 for k in range(256) if buf[2 * k] != 2 ** 64 - 1 and buf[2 * k + 1]]
+    return (sum(spans) / len(spans), len(spans)) if spans else None
+
+
 def inforward_graph_us(plan, name, reps=5):
     """Per-dispatch duration of the launches called `name` INSIDE the graph-replayed forward: the
     plan's whole launch list captured as one hipGraph with timing events (external event-record
@@ -498,8 +529,14 @@ def main():
         # nodes around its 32 dispatches), as rocprofv3's in-forward mean reports it; without event
         # capture the iteration delta (also in-forward, and the larger figure)
         ig = inforward_graph_us(plan, "raft_corr_lookup_conv")
+        sp = inforward_span_us(plan)
+        if sp:
+            roof["inforward_span_us"] = round(sp[0], 2)
         us, how = ((ig[0], f"HIP event-record nodes around each of the {ig[1]} dispatches inside the captured forward "
                            f"graph, mean of the last replay") if ig else
+                   (sp[0], f"device realtime span (first work-group start to last work-group end, stores completed) "
+                           f"of each of the forward's {sp[1]} fused lookup launches, one eager forward enqueued behind a "
+                           f"GPU spin so its kernels run back to back (raft_debug_launch_span)") if sp else
                    (roof["iteration_delta_us"], "one iteration's graph with minus without the launch"))
         roof["launch_us"] = round(us, 2)
         roof["achieved"] = round(roof["algorithmic_bytes_per_launch"] / us / 1e3, 1)

@@ -58,6 +58,13 @@ const char* raft_hip_last_error(void);  /* message of the last failure on this t
  * SRC_HASH: the .hip files in SRCS order, the csrc .hpp headers and include/raft_hip.h); the loader
  * refuses a library whose hash differs from the sources beside it (a stale prebuilt .so) */
 const char* raft_hip_source_hash(void);
+/* Launch-span timing (bench / profiling): after raft_debug_launch_span(1) every
+ * raft_corr_lookup_conv launch takes the next of 256 slots and records the realtime counter
+ * (100 MHz) at its first work-group's start and at its last work-group's end, after that
+ * work-group's stores completed; raft_debug_launch_span_read copies n values (slot k: [2k] start,
+ * [2k+1] end).  raft_debug_launch_span(0) clears the slots and stops numbering. */
+int raft_debug_launch_span(int enable);
+int raft_debug_launch_span_read(unsigned long long* host, int n);
 /* Debug (tests only): fill the LDS of every CU with all-ones words (NaN as fp32, f16 and bf16) by
  * kernels that take a CU's whole 160 KiB each; no global memory is touched.  A kernel launched next
  * on the stream that reads LDS it did not write then sees NaN: the parity tests run every launch of

@@ -110,6 +110,8 @@ _PROTOS = {
     "raft_conv2d_stats_slots": (c_int, [ctypes.POINTER(ConvParams)]),
     "raft_conv2d_halo_tile_rows": (c_int, [ctypes.POINTER(ConvParams)]),
     "raft_conv2d_halo_tiles_per_wg": (c_int, [ctypes.POINTER(ConvParams)]),
+    "raft_debug_launch_span": (c_int, [c_int]),
+    "raft_debug_launch_span_read": (c_int, [P, c_int]),
     "raft_conv2d_in_norm_ok": (c_int, [ctypes.POINTER(ConvParams)]),
     "raft_instnorm_merge": (c_int, [P, c_int, c_int, c_int, c_int, c_float, P, P]),
     "raft_instnorm_merge_ws_floats": (c_size_t, [c_int, c_int, c_int]),

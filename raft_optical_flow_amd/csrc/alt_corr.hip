@@ -496,7 +496,8 @@ __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevel
   constexpr int WD = 2 * R + 2, NT = WD * WD, RD = 2 * R + 1;
   constexpr int TPT = (NT + 7) / 8;  // taps per thread (8 waves)
   constexpr int ABYTES = AT * AT * AM_KS * AM_ROW, BBYTES = AM_NB * AM_KS * AM_ROW;
-  static_assert(AM_NB * AM_SLD * 4 <= BBYTES && AT * AT * (NT + 1) * 4 <= BBYTES, "S and ts fit the band region");
+  static_assert(AM_NB * AM_SLD * 4 <= BBYTES && AT * AT * (NT + 1) * 4 + AT * AT * 16 <= BBYTES,
+                "S and ts (+ the query table) fit the band region");
   __shared__ __attribute__((aligned(16))) char smem[ABYTES + BBYTES];
   char* const As = smem;                // the F1 tile: resident over all levels
   char* const Bs = smem + ABYTES;       // band rows, then the band's S, then the tap sums
@@ -704,11 +705,15 @@ __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevel
     }
     // ---- tap sums -> LDS ts[q][t] (over the band region), then the bilinear binning
     float* ts = reinterpret_cast<float*>(Bs);
+    // (beside them: each query's bilinear fractions, pixel and validity for the binning below)
+    f32x4* qtab = reinterpret_cast<f32x4*>(ts + AT * AT * (NT + 1));
 #pragma unroll
     for (int j = 0; j < TPT; ++j) {
       const int t = g + 8 * j;
       if (t < NT) ts[lane * (NT + 1) + t] = tap[j];
     }
+    if (g == 0)
+      qtab[lane] = f32x4{cur.x - floorf(cur.x), cur.y - floorf(cur.y), __int_as_float(p), valid ? 1.f : 0.f};
     __syncthreads();
     ALT_ST(11);  // tap sums -> LDS + sync
     // the next level's box and first band go out before this level's binning
@@ -722,21 +727,18 @@ __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevel
     const float sdiv = a0.scale_div;
     int big = 0;
     if (a0.out_layout == 1) {
-      // wave g: queries q = g + 8i (uniform), lanes = output bins o, o + 64
-#pragma unroll 1
-      for (int i = 0; i < AT * AT / 8; ++i) {
-        const int q = g + 8 * i;
-        if (!__builtin_amdgcn_readlane((int)valid, q)) continue;
-        const float xq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cur.x), q));
-        const float yq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cur.y), q));
-        const int pq = __builtin_amdgcn_readlane(p, q);
-        const float dx = xq - floorf(xq), dy = yq - floorf(yq);
-        const float* tq = ts + q * (NT + 1);
-        float* orow = out + ((long)b * P1 + pq) * a0.out_ld;
-#pragma unroll
-        for (int o0 = 0; o0 < RD * RD; o0 += 64) {
-          const int o = o0 + lane;
-          if (o < RD * RD) {
+      // thread t: outputs i = t + 512k of the tile's 64 x RD^2 (query i / RD^2, bin i % RD^2), all
+      // independent (consecutive threads write consecutive bins of a query's row)
+      constexpr int NO = AT * AT * RD * RD, KO = (NO + 511) / 512;
+#pragma unroll 2
+      for (int k = 0; k < KO; ++k) {
+        const int i = tid + 512 * k;
+        if (i < NO) {
+          const int q = i / (RD * RD), o = i - q * (RD * RD);
+          const f32x4 qi = qtab[q];
+          if (qi[3] != 0.f) {
+            const float dx = qi[0], dy = qi[1];
+            const float* tq = ts + q * (NT + 1);
             const int ox = o / RD, oy = o - ox * RD;  // channel = oy + rd*ox
             float val = tq[oy * WD + ox] * ((1.f - dy) * (1.f - dx));
             val += tq[oy * WD + ox + 1] * ((1.f - dy) * dx);
@@ -744,7 +746,7 @@ __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevel
             val += tq[(oy + 1) * WD + ox + 1] * (dy * dx);
             val = val / sdiv;
             big |= fabsf(val) > RAFT_RANGE_LIMIT;
-            orow[o] = val;
+            out[((long)b * P1 + __float_as_int(qi[2])) * a0.out_ld + o] = val;
           }
         }
       }

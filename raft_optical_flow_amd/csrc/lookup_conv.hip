@@ -67,7 +67,14 @@ struct LookupConvArgs {
   int f1out_ld;
   int* f1flag;
   int tx_n, ty_n;       // pixel tiles per image row / column
+  int span_slot;        // raft_debug_launch_span: this launch's slot of g_lc_span, or -1
 };
+
+// raft_debug_launch_span: per timed launch, the realtime (100 MHz) of its first work-group's start
+// and of its last work-group's end (after its stores completed): the launch's span as it ran
+constexpr int LC_SPAN_SLOTS = 256;
+__device__ unsigned long long g_lc_span[2 * LC_SPAN_SLOTS];
+int g_lc_span_next = -1;  // host: the next slot, -1 = off
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -123,6 +130,8 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  if (g.span_slot >= 0 && threadIdx.x == 0)
+    atomicMin(&g_lc_span[2 * g.span_slot], (unsigned long long)__builtin_amdgcn_s_memrealtime());
   const int per = g.tx_n * g.ty_n;
   const int b = tile / per, sr = tile - b * per;
   const int y0 = (sr / g.tx_n) * LC_TH, x0 = (sr % g.tx_n) * LC_TW;
@@ -463,6 +472,12 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
   };
   store(acc, c1b, g.out, g.out_ld, 32 * wv + m, g.out_flag);
   if (wv < LC_F1N / 32) store(facc, f1b, g.f1out, g.f1out_ld, 32 * wv + m, g.f1flag);
+  if (g.span_slot >= 0) {  // (uniform) the work-group's end once its stores have completed
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0)
+      atomicMax(&g_lc_span[2 * g.span_slot + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  }
 #ifdef LC_END_FENCE  // dev experiment: agent-scope release of the outputs before the waves exit
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   __builtin_amdgcn_s_waitcnt(0);
@@ -554,6 +569,7 @@ extern "C" int raft_corr_lookup_conv(const float* pyramid, int B, int H, int W, 
   g.f1flag = f1_range_flag;
   g.tx_n = cdiv(W, LC_TW);
   g.ty_n = cdiv(H, LC_TH);
+  g.span_slot = g_lc_span_next >= 0 && g_lc_span_next < LC_SPAN_SLOTS ? g_lc_span_next++ : -1;
   const long nt = (long)B * g.tx_n * g.ty_n;
   RAFT_REQUIRE(nt < (1L << 31), "raft_corr_lookup_conv: grid too large");
   hipStream_t s = as_stream(stream);
@@ -565,4 +581,25 @@ extern "C" int raft_corr_lookup_conv(const float* pyramid, int B, int H, int W, 
   else
     hipLaunchKernelGGL(lookup_conv_kernel<RAFT_PREC_BF16>, grid, dim3(512), 0, s, g);
   return check_launch("raft_corr_lookup_conv");
+}
+
+// launch-span timing of raft_corr_lookup_conv (include/raft_hip.h)
+extern "C" int raft_debug_launch_span(int enable) {
+  using namespace raft;
+  unsigned long long init[2 * LC_SPAN_SLOTS];
+  for (int i = 0; i < LC_SPAN_SLOTS; ++i) {
+    init[2 * i] = ~0ull;
+    init[2 * i + 1] = 0ull;
+  }
+  const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_lc_span), init, sizeof(init));
+  if (e != hipSuccess) return set_error((int)e, "raft_debug_launch_span: %s", hipGetErrorString(e));
+  g_lc_span_next = enable ? 0 : -1;
+  return 0;
+}
+extern "C" int raft_debug_launch_span_read(unsigned long long* host, int n) {
+  using namespace raft;
+  RAFT_REQUIRE(host && n > 0 && n <= 2 * LC_SPAN_SLOTS, "raft_debug_launch_span_read: bad arguments");
+  const hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_lc_span), sizeof(unsigned long long) * (size_t)n);
+  if (e != hipSuccess) return set_error((int)e, "raft_debug_launch_span_read: %s", hipGetErrorString(e));
+  return 0;
 }
