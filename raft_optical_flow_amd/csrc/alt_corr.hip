@@ -716,12 +716,6 @@ __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevel
       qtab[lane] = f32x4{cur.x - floorf(cur.x), cur.y - floorf(cur.y), __int_as_float(p), valid ? 1.f : 0.f};
     __syncthreads();
     ALT_ST(11);  // tap sums -> LDS + sync
-    // the next level's box and first band go out before this level's binning
-    if (l + 1 < lvs.n) {
-      setup(l + 1, nxt);
-      if (nxt.fits) load_band(l + 1, nxt, 0);
-    }
-    ALT_ST(12);  // next level setup + first band issue
     // bin (core/corr.py + correlation_kernel.cu:95-116: the bilinear weights of frac(coords) over
     // each bin's four integer taps, then / scale), the arithmetic of alt_bin_store
     const float sdiv = a0.scale_div;
@@ -766,6 +760,13 @@ __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevel
       }
     }
     ALT_ST(13);  // binning + output stores
+    // the next level's box and first band go out behind this level's output stores (ahead of
+    // them they held the stores back in the memory pipeline: 0.3-2 % slower, r04h_experiments)
+    if (l + 1 < lvs.n) {
+      setup(l + 1, nxt);
+      if (nxt.fits) load_band(l + 1, nxt, 0);
+    }
+    ALT_ST(12);  // next level setup + first band issue
     if (a0.range_flag && big) *a0.range_flag = 1;
     if (valid && l == 0 && a0.flow && g == 0) {
       a0.flow[((long)b * P1 + p) * a0.flow_ld + 0] = cur.x * cdiv - (float)(p % a0.W1);

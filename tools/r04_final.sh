@@ -18,5 +18,9 @@ if [ "${PART:-a}" = a ]; then
 else
   PMC_OUT=gpurun_out PMC_ROUND=r04 timeout -k 10 600 bash tools/pmc_forward.sh 1 > gpurun_out/pmc_r04f.log 2>&1 || { tail -20 gpurun_out/pmc_r04f.log; exit 1; }
   tail -5 gpurun_out/pmc_r04f.log
+  # the bench's forward (the fused lookup launch): r04_lookup_conv_pmc.json and its conv counters
+  mkdir -p gpurun_out/pmc_unfused && cp gpurun_out/r04_halo_pmc.json gpurun_out/pmc_unfused/
+  RAFT_FUSE_CONVF1=1 PMC_OUT=gpurun_out PMC_ROUND=r04 timeout -k 10 600 bash tools/pmc_forward.sh 1 > gpurun_out/pmc2_r04f.log 2>&1 || { tail -20 gpurun_out/pmc2_r04f.log; exit 1; }
+  [ -n "$PMC_ONLY" ] && exit 0
   timeout -k 10 900 bash tools/config_sweep.sh r04f || exit 1
 fi
