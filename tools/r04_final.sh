@@ -15,6 +15,8 @@ if [ "${PART:-a}" = a ]; then
   cat gpurun_out/bench_r04f.json
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r04f -o run --output-format csv -- python bench.py > gpurun_out/bench_r04f_rocprof.json 2> gpurun_out/bench_r04f_rocprof.err || { tail -20 gpurun_out/bench_r04f_rocprof.err; exit 1; }
   ls gpurun_out/prof_r04f
+  python tools/roofline_rocprof.py gpurun_out/prof_r04f/run_kernel_trace.csv gpurun_out/bench_r04f_rocprof.json > gpurun_out/r04_final_roofline_rocprof.json
+  cat gpurun_out/r04_final_roofline_rocprof.json
 else
   PMC_OUT=gpurun_out PMC_ROUND=r04 timeout -k 10 600 bash tools/pmc_forward.sh 1 > gpurun_out/pmc_r04f.log 2>&1 || { tail -20 gpurun_out/pmc_r04f.log; exit 1; }
   tail -5 gpurun_out/pmc_r04f.log

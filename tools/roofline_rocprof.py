@@ -30,5 +30,7 @@ out = {
                            "median_us": round(statistics.median(rest), 3)},
 }
 out["live_vs_rocprof_back_to_back"] = round(live / out["rocprof_back_to_back"]["mean_us"] - 1, 4)
+# (round 4: the live figure is the in-forward launch span, so it is checked against the in-forward mean)
+out["live_vs_rocprof_in_forward"] = round(live / out["rocprof_in_forward"]["mean_us"] - 1, 4)
 out["in_forward_vs_back_to_back"] = round(out["rocprof_in_forward"]["mean_us"] / out["rocprof_back_to_back"]["mean_us"] - 1, 4)
 print(json.dumps(out, indent=1))
