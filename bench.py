@@ -17,9 +17,10 @@ The line also carries
                 the 324-channel correlation rows never leave the CU), HBM-bound:
                 algorithmic bytes per pair-iteration = P * (L*(2r+2)^2*4 window reads +
                 8 coords + 4*(256 + 128) convc1 / convf1 outputs + 8 flow) over its
-                per-dispatch duration (the forward's own launch, back to back in one
-                hipGraph; the rocprofv3 per-dispatch mean of the same kernel in the
-                forward is committed under profiles/); without the fused launch (fp32
+                per-dispatch duration in the forward (the library's device launch span,
+                raft_debug_launch_span, over one eager forward whose kernels run back to
+                back; the rocprofv3 per-dispatch mean of the same kernel in the forward is
+                committed under profiles/, tools/roofline_rocprof.py); without the fused launch (fp32
                 mode) the lookup-only kernel (HIP event pairs in an eager forward)
                 with SURVEY 8(d)'s P*2904 B; `traffic` = HBM bytes per launch from a
                 committed in-forward PMC summary taken on the current kernel source;
