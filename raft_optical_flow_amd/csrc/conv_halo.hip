@@ -1091,6 +1091,13 @@ bool conv_halo_norm_ok(const HaloOperands& o) {
   return p.kh == 3 && p.kw == 3 && p.in0_c <= 256 && HaloCfg<3, 3, 64>::D == 3 && HaloCfg<3, 3, 32>::D == 3;
 }
 
+long halo_wide_min() {  // the least 128-column tile count for the wide tiles (RAFT_HALO_WIDE_MIN, default 512)
+  static const long v = [] {
+    const char* e = getenv("RAFT_HALO_WIDE_MIN");
+    return e ? atol(e) : 512L;
+  }();
+  return v;
+}
 bool halo_wide_enabled() {
   static const bool enabled = [] {
     const char* e = getenv("RAFT_HALO_WIDE");
@@ -1105,7 +1112,7 @@ int conv_halo_tile_rows(const HaloOperands& o) {
   if (!halo_enabled() || !halo_problem(o, a)) return 0;
   const raft_conv2d_params& p = o.p;
   const bool wide = p.precision != RAFT_PREC_F16X3 && !p.stats_part && !p.in_norm && o.n_pad % 128 == 0 &&
-                    halo_spatial(a) * (o.n_pad / 128) >= 512 && halo_wide_enabled();
+                    halo_spatial(a) * (o.n_pad / 128) >= halo_wide_min() && halo_wide_enabled();
   return halo_pick_th(o, wide);
 }
 
@@ -1130,7 +1137,7 @@ static bool halo_plan(const HaloOperands& o, HaloLaunch& l, int& bn, int& th, lo
   // the one-product modes take 128-column tiles (2 x 2 waves of 64 x 64) where that still
   // leaves two rounds of work-groups (configs 3 - 5; RAFT_HALO_WIDE=0: never)
   const bool wide = p.precision != RAFT_PREC_F16X3 && !p.stats_part && !p.in_norm && o.n_pad % 128 == 0 &&
-                    spatial * (o.n_pad / 128) >= 512 && halo_wide_enabled();
+                    spatial * (o.n_pad / 128) >= halo_wide_min() && halo_wide_enabled();
   th = halo_pick_th(o, wide);
   bn = th == HTH_BIG ? 64 : wide ? 128 : spatial * (o.n_pad / 64) > 128 ? 64 : 32;
   halo_set_th(o, l.a[0], th);
