@@ -1022,7 +1022,7 @@ bool halo_mt_ok(const HaloArgs& a, int bn, int th, long m) {
   // modes' 3x3 convs with several N-tiles ran 18-30 % slower on multi-tile work-groups (their short
   // K loops do not cover the next tile's loads beside the last one's stores); their 1x1 / 1x5 convs
   // and every f16x3 conv gained
-  if (a.p.precision != RAFT_PREC_F16X3 && T == 9 && a.gn > 1) return false;
+  if (a.p.precision != RAFT_PREC_F16X3 && T == 9 && (a.gn > 1 || bn == 128)) return false;  // (wide: unmeasured)
   const int n1 = halo_nkp(a.nk, U, T, false), nm = halo_nkp(a.nk, U, T, true);
   if ((long)(nm - n1) * 8 > n1) return false;
   if (a.p.in_norm) {
@@ -1091,10 +1091,12 @@ bool conv_halo_norm_ok(const HaloOperands& o) {
   return p.kh == 3 && p.kw == 3 && p.in0_c <= 256 && HaloCfg<3, 3, 64>::D == 3 && HaloCfg<3, 3, 32>::D == 3;
 }
 
-long halo_wide_min() {  // the least 128-column tile count for the wide tiles (RAFT_HALO_WIDE_MIN, default 512)
+// the least 128-column tile count for the wide tiles (RAFT_HALO_WIDE_MIN): 256, one round (512 until
+// r04j: config 5's bf16 update convs 364 -> 351 us per iteration, 47.0 -> 47.8 pairs/s on one box)
+long halo_wide_min() {
   static const long v = [] {
     const char* e = getenv("RAFT_HALO_WIDE_MIN");
-    return e ? atol(e) : 512L;
+    return e ? atol(e) : 256L;
   }();
   return v;
 }
@@ -1135,7 +1137,7 @@ static bool halo_plan(const HaloOperands& o, HaloLaunch& l, int& bn, int& th, lo
   // one work-group per CU (LDS): 64 output channels per work-group unless
   // 32 still fits the grid in one round of 256 CUs with half of them idle at 64;
   // the one-product modes take 128-column tiles (2 x 2 waves of 64 x 64) where that still
-  // leaves two rounds of work-groups (configs 3 - 5; RAFT_HALO_WIDE=0: never)
+  // leaves a round of work-groups (RAFT_HALO_WIDE_MIN, configs 3 - 5; RAFT_HALO_WIDE=0: never)
   const bool wide = p.precision != RAFT_PREC_F16X3 && !p.stats_part && !p.in_norm && o.n_pad % 128 == 0 &&
                     spatial * (o.n_pad / 128) >= halo_wide_min() && halo_wide_enabled();
   th = halo_pick_th(o, wide);
