@@ -1108,14 +1108,26 @@ bool halo_wide_enabled() {
   return enabled;
 }
 
+// The tile of a conv: the one-product modes' 128-column tiles (wide) where at least two rounds of
+// them remain (512), else the big tiles where the rounds rule picks them, else the wide tiles from
+// RAFT_HALO_WIDE_MIN (256) of them, else the 128-pixel tiles.  Returns the tile rows; `wide` out.
+int halo_pick(const HaloOperands& o, const HaloArgs& a, bool& wide) {
+  const raft_conv2d_params& p = o.p;
+  const bool can = p.precision != RAFT_PREC_F16X3 && !p.stats_part && !p.in_norm && o.n_pad % 128 == 0 &&
+                   halo_wide_enabled();
+  const long n = halo_spatial(a) * (o.n_pad / 128);
+  wide = can && n >= 512;
+  const int th = halo_pick_th(o, wide);
+  if (!wide && th != HTH_BIG) wide = can && n >= halo_wide_min();
+  return th;
+}
+
 // tile rows conv_halo_launch picks for the conv (HTH or HTH_BIG), 0 when the halo kernel does not run it
 int conv_halo_tile_rows(const HaloOperands& o) {
   HaloArgs a;
   if (!halo_enabled() || !halo_problem(o, a)) return 0;
-  const raft_conv2d_params& p = o.p;
-  const bool wide = p.precision != RAFT_PREC_F16X3 && !p.stats_part && !p.in_norm && o.n_pad % 128 == 0 &&
-                    halo_spatial(a) * (o.n_pad / 128) >= halo_wide_min() && halo_wide_enabled();
-  return halo_pick_th(o, wide);
+  bool wide;
+  return halo_pick(o, a, wide);
 }
 
 int conv_halo_stats_slots(const HaloOperands& o) {
@@ -1133,14 +1145,12 @@ int conv_halo_stats_slots(const HaloOperands& o) {
 static bool halo_plan(const HaloOperands& o, HaloLaunch& l, int& bn, int& th, long& wgs) {
   if (!halo_enabled() || !halo_problem(o, l.a[0])) return false;
   const long spatial = halo_spatial(l.a[0]);
-  const raft_conv2d_params& p = o.p;
   // one work-group per CU (LDS): 64 output channels per work-group unless
   // 32 still fits the grid in one round of 256 CUs with half of them idle at 64;
-  // the one-product modes take 128-column tiles (2 x 2 waves of 64 x 64) where that still
-  // leaves a round of work-groups (RAFT_HALO_WIDE_MIN, configs 3 - 5; RAFT_HALO_WIDE=0: never)
-  const bool wide = p.precision != RAFT_PREC_F16X3 && !p.stats_part && !p.in_norm && o.n_pad % 128 == 0 &&
-                    spatial * (o.n_pad / 128) >= halo_wide_min() && halo_wide_enabled();
-  th = halo_pick_th(o, wide);
+  // the one-product modes take 128-column tiles (2 x 2 waves of 64 x 64) by halo_pick
+  // (RAFT_HALO_WIDE=0: never)
+  bool wide;
+  th = halo_pick(o, l.a[0], wide);
   bn = th == HTH_BIG ? 64 : wide ? 128 : spatial * (o.n_pad / 64) > 128 ? 64 : 32;
   halo_set_th(o, l.a[0], th);
   l.a[0].gn = o.n_pad / bn;
