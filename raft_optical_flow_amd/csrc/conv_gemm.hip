@@ -938,7 +938,11 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
         p.pad_w == 1 && p.out_h == p.in_h && p.out_w == p.in_w) {
       // 4x16 tiles while they fill the CUs; 2x16 (twice the work-groups) when not
       const long t4 = (long)p.batch * cdiv(p.out_h, 4) * cdiv(p.out_w, 16);
-      if (t4 >= SN_TH4_MIN_TILES) {
+      static const long th4_min = [] {
+        const char* e = getenv("RAFT_SN_TH4_MIN");
+        return e ? atol(e) : (long)SN_TH4_MIN_TILES;
+      }();
+      if (t4 >= th4_min) {
         hipLaunchKernelGGL((conv_smalln3x3_kernel<2, 4>), dim3((unsigned)t4), dim3(512), 0, s, a, p.weight);
       } else {
         const long t2 = (long)p.batch * cdiv(p.out_h, 2) * cdiv(p.out_w, 16);
