@@ -524,7 +524,7 @@ __global__ __launch_bounds__(256) void conv_smalln_kernel(ConvArgs a) {
 
 // Small-N 3x3 "same" convolution (the flow head's 256 -> 2 conv, core/update.py:6-16)
 // over TH x 16 output tiles (4x16, or 2x16 when 4x16 tiles would leave CUs
-// idle: config 2 at B = 1 has 110): one 512-thread work-group per tile; wave w owns the
+// idle: config 2 at B = 1 has 112): one 512-thread work-group per tile; wave w owns the
 // input channels 32w + 256k.  Lane (q, pb) = (lane & 7, lane >> 3) holds the
 // weights of channel quad q for all 9 taps in registers (loaded with the
 // patch: one memory round trip, no scalar-load chain) and accumulates the
@@ -533,7 +533,9 @@ __global__ __launch_bounds__(256) void conv_smalln_kernel(ConvArgs a) {
 // pixel] (row stride padded to 109 pixels).  Partial sums meet through lane
 // shuffles (the 8 quads) and LDS (the 8 waves) in a fixed order.
 #ifndef SN_TH4_MIN_TILES  // dev builds: 0 = always 4x16 tiles
-#define SN_TH4_MIN_TILES 512
+// 256 (one round; 512 until r04k: config 5's 510 4x16 tiles vs 1020 2x16 ones, 47.9 / 48.0 -> 48.3 / 48.4
+// pairs/s on one box); RAFT_SN_TH4_MIN overrides
+#define SN_TH4_MIN_TILES 256
 #endif
 // TH x 16 output tiles (TH = 4 or 2); SN_PXB = TH*16/8 pixels per lane block
 template <int TH>
