@@ -377,7 +377,9 @@ int raft_conv2d(const raft_conv2d_params* p, raft_stream_t stream);
  * raft_conv2d(p1).  When both are halo-kernel convs of one shape class and precision, their
  * tiles run side by side in ONE launch: the pair fills CUs that either alone leaves idle at
  * one frame pair, with no second stream (a cross-stream fork/join costs a graph ~7 us per
- * edge on ROCm).  Otherwise, or when one reads what the other writes, or both write a common
+ * edge on ROCm).  Each conv keeps the tile rows raft_conv2d would pick for it
+ * (raft_conv2d_halo_tile_rows), so the bits match also with weight_s set; convs that pick
+ * different rows are not co-launched.  Otherwise, or when one reads what the other writes, or both write a common
  * element (column ranges of their output rows meet), the two run in order. */
 int raft_conv2d_pair(const raft_conv2d_params* p0, const raft_conv2d_params* p1, raft_stream_t stream);
 /* fp32 packed weight [n_pad][k_pad] -> split form for RAFT_PREC_F16X3 / F16:

@@ -165,8 +165,14 @@ constexpr int halo_norm_bytes(int LDS_B, int LDS_A, int D) {
   return (ENC && KH == 3 && KW == 3 && D == 3) ? ((HALO_LDS - LDS_B - LDS_A) & ~1023) : 0;
 }
 
-template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH>
-__device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt, int st0, int ntl, char* smem) {
+//
+// MT: the multi-tile body (ntl >= 1 at run time).  !MT: exactly one tile per work-group, compiled
+// without the tile loop, so the single-round launches (config 2's whole update loop) carry none of
+// its cost: no per-load-set tile / chunk divisions, the tile's patch offsets fixed once per lane,
+// one K loop and one epilogue (round 4's shared body had made every 128-pixel update conv 7-16 %
+// slower in the forward).
+template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH, bool MT = false>
+__device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt, int st0, int ntl_arg, char* smem) {
   constexpr bool X3 = PREC == RAFT_PREC_F16X3;
   constexpr bool BF = PREC == RAFT_PREC_BF16;
   using C = HaloCfg<KH, KW, BNT, X3 ? 128 : 64, TH>;
@@ -222,7 +228,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
   struct Tile {
     int b, y0, x0, n0, st;
   };
-  auto tile_at = [&](int k) {
+  auto tile_calc = [&](int k) {
     Tile t;
     t.st = st0 + k;
     t.b = t.st / per;
@@ -232,11 +238,26 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
     t.n0 = nt * BNT;
     return t;
   };
+  const Tile tile0 = tile_calc(0);
+  auto tile_at = [&](int k) { return MT ? tile_calc(k) : tile0; };
+  const int ntl = MT ? ntl_arg : 1;
   const int nk = a.nk, nch = a.nch;
-  const int nkp = halo_nkp(nk, U, T, ntl > 1);  // K-steps per tile (multiple of U)
-  const int ns_t = nkp / U;                     // super-steps per tile
-  const int NS = ntl * ns_t;                    // super-steps of the work-group
-  const int nchp = nkp / T;                     // patch-ring chunks per tile (ntl > 1: exact)
+  const int nkp = halo_nkp(nk, U, T, MT && ntl > 1);  // K-steps per tile (multiple of U)
+  const int ns_t = nkp / U;                           // super-steps per tile
+  const int NS = MT ? ntl * ns_t : ns_t;              // super-steps of the work-group
+  const int nchp = nkp / T;                           // patch-ring chunks per tile (ntl > 1: exact)
+  // load set u -> (tile kt, set ul within the tile); !MT: (0, u)
+  auto set_tile = [&](int u, int& kt, int& ul) {
+    if constexpr (MT) {
+      kt = u / ns_t;
+      ul = u - kt * ns_t;
+    } else {
+      kt = 0;
+      ul = u;
+    }
+  };
+  // patch ring slot of chunk c of tile kt
+  auto pslot = [&](int kt, int c) { return MT ? (kt * nchp + c) % PA : c % PA; };
 
   // Weight pieces of wave lw (a loader, or in the prologue the MFMA wave of the
   // same index): NWP consecutive 8-row pieces of the block of K-step ew of
@@ -249,14 +270,16 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
   for (int k = 0; k < NWP; ++k) {
     const int r = RPP * (wpc0 + k) + lane / QPR;
     const int qd = X3 ? (lane & 7) ^ ((r >> 1) & 7) : (lane & 3) ^ ((r >> 2) & 3);
-    wvoff[k] = (unsigned)r * ((unsigned)a.K * 4u) + (unsigned)qd * 16u;
+    // (!MT: the N-tile's first row folded in here; MT: in soff, 0 for the zero sets past the last tile)
+    wvoff[k] = (unsigned)(r + (MT ? 0 : nt * BNT)) * ((unsigned)a.K * 4u) + (unsigned)qd * 16u;
   }
   auto issue_weights = [&](int u) {
-    const int kt = u / ns_t, ul = u - kt * ns_t;
+    int kt, ul;
+    set_tile(u, kt, ul);
     const int j = U * ul + ew;
-    const bool in = j < nk && kt < ntl;
+    const bool in = j < nk && (!MT || kt < ntl);
     const int c = j / T, t = j - c * T;
-    const int n0 = in ? nt * BNT : 0;
+    const int n0 = MT && in ? nt * BNT : 0;
     // packed K-step (tap, chunk) of the tile's N-tile rows
     const unsigned soff = in ? (unsigned)(t * nch + c) * 128u + (unsigned)n0 * ((unsigned)a.K * 4u) : 0u;
     char* dst = smem + (U * (u % (D + 1)) + ew) * (BNT * WROW) + wpc0 * 1024;
@@ -299,30 +322,37 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
     };
     // the chunk starting in load set u: its tile kt and chunk c within the tile (at most one: T >= U)
     auto set_chunk = [&](int u, int& kt, int& c) -> bool {
-      kt = u / ns_t;
-      const int ul = u - kt * ns_t;
+      int ul;
+      set_tile(u, kt, ul);
       c = (U * ul + T - 1) / T;
-      return kt < ntl && c * T < U * ul + U;
+      return (!MT || kt < ntl) && c * T < U * ul + U;
     };
     // Patch pieces of this loader: i = lw, lw+4, ... (< PI), pixels 8i .. 8i+7; per chunk the
     // tile's pixel offsets plus the channel offset
     constexpr int PK = (PI + 3) / 4;
     const int pcw = PI > lw ? (PI - 1 - lw) / 4 + 1 : 0;  // this wave's pieces per patch
-    // chunk c of tile kt into patch ring slot (kt * nchp + c) % PA (chunks past nch load zeros)
+    // per lane and piece: the channel quad within a chunk (swizzled source) x 4, and (!MT) the
+    // input pixel of the one tile, fixed for the work-group
+    unsigned pq4[PK], ppix0[PK];
+#pragma unroll
+    for (int k = 0; k < PK; ++k) {
+      const int pp = 8 * (lw + 4 * k) + (lane >> 3);
+      pq4[k] = 4u * (unsigned)((lane & 7) ^ (((pp % PW) >> 1) & 7));
+      ppix0[k] = MT ? 0u : patch_pix(tile0, pp);
+    }
+    // chunk c of tile kt into patch ring slot pslot(kt, c) (chunks past nch load zeros)
     auto issue_patch = [&](int kt, int c) {
       const Tile t = tile_at(kt);
       const bool s0 = 32 * c < in0_c;  // uniform: the chunk lies in one segment
       const unsigned cb = (unsigned)(s0 ? 32 * c : 32 * c - in0_c);
       const unsigned lim = (unsigned)(s0 ? in0_c : in1_c);
       const unsigned ld = s0 ? ld0 : ld1;
-      char* base = smem + C::LDS_B + ((kt * nchp + c) % PA) * (PI * 1024);
+      char* base = smem + C::LDS_B + pslot(kt, c) * (PI * 1024);
 #pragma unroll
       for (int k = 0; k < PK; ++k) {
         if (lw + 4 * k < PI) {
-          const int pp = 8 * (lw + 4 * k) + (lane >> 3);
-          const unsigned pix = patch_pix(t, pp);
-          const unsigned qd = (unsigned)((lane & 7) ^ (((pp % PW) >> 1) & 7));
-          const unsigned ch = cb + 4u * qd;
+          const unsigned pix = MT ? patch_pix(t, 8 * (lw + 4 * k) + (lane >> 3)) : ppix0[k];
+          const unsigned ch = cb + pq4[k];
           const unsigned voff = (pix != OFF_INVALID && ch < lim) ? (pix * ld + ch) * 4u : OFF_INVALID;
           dma16(s0 ? rs0 : rs1, base + (lw + 4 * k) * 1024, voff, 0);
         }
@@ -336,8 +366,9 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
         n = NWP;
       }
       if constexpr (T == 1) {
-        const int kt = u / ns_t, ul = u - kt * ns_t;
-        if (kt >= ntl) return n;
+        int kt, ul;
+        set_tile(u, kt, ul);
+        if (MT && kt >= ntl) return n;
 #pragma unroll
         for (int e = 0; e < U; ++e) issue_patch(kt, U * ul + e);
         return n + U * pcw;
@@ -357,14 +388,19 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
       // (still a super-step before its first read; its slot was free already).
       constexpr int NT = 4 * NPIX, TI = (NT + 255) / 256;
       const unsigned tg8 = 8u * (unsigned)(lane & 3);  // channel offset 8g within the chunk (g = t & 3 = lane & 3)
-      int tlds[TI];  // byte offset of the task's hi quad in a patch slot (lo: ^ 64), -1 past NT
+      int tlds[TI];        // byte offset of the task's hi quad in a patch slot (lo: ^ 64), -1 past NT
+      unsigned tpix0[TI];  // !MT: the task's input pixel in the one tile (patch_pix)
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         const int t = 64 * lw + lane + 256 * i;
         const int pp = t >> 2, g = t & 3;
         const int px = pp % PW;
         tlds[i] = t < NT ? pp * 128 + ((g ^ ((px >> 1) & 7)) << 4) : -1;
+        tpix0[i] = MT ? 0u : patch_pix(tile0, pp);
       }
+      auto task_pix = [&](const Tile& tt, int i) {
+        return MT ? patch_pix(tt, (64 * lw + lane + 256 * i) >> 2) : tpix0[i];
+      };
       using Staged = f32x4[TI][2];
       auto load_patch = [&](int kt, int c, Staged& dst) {  // chunks past the end load zeros
         const Tile tt = tile_at(kt);
@@ -374,7 +410,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
         const unsigned ld = s0 ? ld0 : ld1;
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
-          const unsigned pix = patch_pix(tt, (64 * lw + lane + 256 * i) >> 2);
+          const unsigned pix = task_pix(tt, i);
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
             const unsigned ch = cb + tg8 + 4u * q;
@@ -385,7 +421,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
       };
       const bool nrm = NORM_BYTES > 0 && p.in_norm != nullptr;
       auto store_patch = [&](int kt, int c, const Staged& src) {
-        char* base = smem + C::LDS_B + ((kt * nchp + c) % PA) * (PI * 1024);
+        char* base = smem + C::LDS_B + pslot(kt, c) * (PI * 1024);
         const bool s0 = 32 * c < in0_c;  // (the norm applies to segment 0)
         if (nrm && s0) {
           const Tile tt = tile_at(kt);
@@ -394,7 +430,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
           for (int i = 0; i < TI; ++i) {
             if (tlds[i] >= 0) {
               // channels 32c + 8g .. +7: (x - mean) * rstd, relu; padding (no pixel, or past in0_c) stays 0
-              const bool pix_ok = patch_pix(tt, (64 * lw + lane + 256 * i) >> 2) != OFF_INVALID;
+              const bool pix_ok = task_pix(tt, i) != OFF_INVALID;
               const int ch = 32 * c + (int)tg8;
               float e[8] = {src[i][0][0], src[i][0][1], src[i][0][2], src[i][0][3],
                             src[i][1][0], src[i][1][1], src[i][1][2], src[i][1][3]};
@@ -769,6 +805,19 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
     t_bar += t0 - t3;
 #endif
   };
+  if constexpr (!MT) {
+    // one tile: the last super-step's look-ahead reads land in ring slots nobody writes any more
+    for (int s = 0; s < NS; ++s) {
+      superstep(std::false_type{});
+      step_end();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    epilogue(tile0);
+#ifdef STAMPS
+    const unsigned long long t4 = hstamp_now();
+    t_epi += t4 - t0;
+#endif
+  } else {
   for (int kt = 0; kt < ntl; ++kt) {
     for (int sl = 0; sl + 1 < ns_t; ++sl) {
       superstep(std::false_type{});
@@ -797,6 +846,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
     t0 = t4;
 #endif
   }
+  }
 #ifdef STAMPS
   {
     const unsigned long long c_exit = hstamp_now(), r_exit = hstamp_real();
@@ -818,7 +868,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
 // One conv (or an independent pair, raft_conv2d_pair) per launch: work-group g runs tiles
 // N-tile g % gn of spatial tiles (g / gn) * m .. + m-1 of its conv (the pair's first grid0
 // work-groups take a[0]'s tiles).
-template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH>
+template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH, bool MT = false>
 __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
   using C = HaloCfg<KH, KW, BNT, PREC == RAFT_PREC_F16X3 ? 128 : 64, TH>;
   constexpr int NORM_BYTES = halo_norm_bytes<KH, KW, BNT, PREC, ENC>(C::LDS_B, C::LDS_A, C::D);
@@ -827,9 +877,25 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
   const int prob = g >= hl.grid0 ? 1 : 0;
   g -= prob * hl.grid0;
   const int gn = hl.a[prob].gn;
-  const int st0 = (g / gn) * hl.m;
-  const int ntl = min(hl.m, (prob ? hl.sp1 : hl.sp0) - st0);
-  halo_body<KH, KW, BNT, PREC, ENC, TH>(hl.a, prob, g % gn, st0, ntl, smem);
+  if constexpr (MT) {
+    const int st0 = (g / gn) * hl.m;
+    const int ntl = min(hl.m, (prob ? hl.sp1 : hl.sp0) - st0);
+    halo_body<KH, KW, BNT, PREC, ENC, TH, true>(hl.a, prob, g % gn, st0, ntl, smem);
+  } else {  // (hl.m == 1)
+    halo_body<KH, KW, BNT, PREC, ENC, TH, false>(hl.a, prob, g % gn, g / gn, 1, smem);
+  }
+}
+
+// the kernel of a launch: the multi-tile body where the plan runs several tiles per work-group
+// (l.m > 1), else the one-tile body.  (The one-product 3x3 wide tiles never run several:
+// halo_mt_ok.)
+template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH>
+void launch_halo_mt(const HaloLaunch& l, dim3 grid, hipStream_t s) {
+  constexpr bool NO_MT = PREC != RAFT_PREC_F16X3 && KH * KW == 9 && BNT == 128;
+  if (!NO_MT && l.m > 1)
+    hipLaunchKernelGGL((conv_halo_kernel<KH, KW, BNT, PREC, ENC, TH, !NO_MT>), grid, dim3(512), 0, s, l);
+  else
+    hipLaunchKernelGGL((conv_halo_kernel<KH, KW, BNT, PREC, ENC, TH, false>), grid, dim3(512), 0, s, l);
 }
 
 template <int KH, int KW, int PREC>
@@ -838,9 +904,9 @@ void launch_halo_p(const HaloLaunch& l, int bn, int th, dim3 grid, hipStream_t s
   if constexpr (KH == 3 && KW == 3) {
     if (th == HTH_BIG) {  // (halo_pick: N tile 64)
       if (p.stats_part || p.in_norm)
-        hipLaunchKernelGGL((conv_halo_kernel<3, 3, 64, PREC, true, HTH_BIG>), grid, dim3(512), 0, s, l);
+        launch_halo_mt<3, 3, 64, PREC, true, HTH_BIG>(l, grid, s);
       else
-        hipLaunchKernelGGL((conv_halo_kernel<3, 3, 64, PREC, false, HTH_BIG>), grid, dim3(512), 0, s, l);
+        launch_halo_mt<3, 3, 64, PREC, false, HTH_BIG>(l, grid, s);
       return;
     }
   } else if constexpr (KH * KW == 5) {
@@ -848,29 +914,29 @@ void launch_halo_p(const HaloLaunch& l, int bn, int th, dim3 grid, hipStream_t s
     // 16 x 20 patches the T = 5 ring needs (D = 3); f16x3's 128-B rows do not, so it runs D = 2 with
     // fp32 patches split by the compute waves (216 / 232 VGPRs)
     if (th == HTH_BIG) {
-      hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 64, PREC, false, HTH_BIG>), grid, dim3(512), 0, s, l);
+      launch_halo_mt<KH, KW, 64, PREC, false, HTH_BIG>(l, grid, s);
       return;
     }
   }
   if constexpr (PREC != RAFT_PREC_F16X3) {
     if (bn == 128) {  // (conv_halo_launch picks it only without stats_part / in_norm)
-      hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 128, PREC>), grid, dim3(512), 0, s, l);
+      launch_halo_mt<KH, KW, 128, PREC>(l, grid, s);
       return;
     }
   }
   if constexpr ((KH == 1 && KW == 1) || (KH == 3 && KW == 3)) {
     if (p.stats_part || p.in_norm) {  // (one conv per launch: raft_conv2d_pair takes neither)
       if (bn == 64)
-        hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 64, PREC, true>), grid, dim3(512), 0, s, l);
+        launch_halo_mt<KH, KW, 64, PREC, true>(l, grid, s);
       else
-        hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 32, PREC, true>), grid, dim3(512), 0, s, l);
+        launch_halo_mt<KH, KW, 32, PREC, true>(l, grid, s);
       return;
     }
   }
   if (bn == 64)
-    hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 64, PREC>), grid, dim3(512), 0, s, l);
+    launch_halo_mt<KH, KW, 64, PREC>(l, grid, s);
   else
-    hipLaunchKernelGGL((conv_halo_kernel<KH, KW, 32, PREC>), grid, dim3(512), 0, s, l);
+    launch_halo_mt<KH, KW, 32, PREC>(l, grid, s);
 }
 template <int KH, int KW>
 void launch_halo_k(const HaloLaunch& l, int bn, int th, dim3 grid, hipStream_t s) {
@@ -1188,11 +1254,11 @@ int conv_halo_launch_pair(const HaloOperands& o0, const HaloOperands& o1, hipStr
   if (!halo_enabled() || !halo_problem(o0, l.a[0]) || !halo_problem(o1, l.a[1])) return 1;
   const raft_conv2d_params &p0 = o0.p, &p1 = o1.p;
   if (p0.kh != p1.kh || p0.kw != p1.kw || p0.precision != p1.precision) return 1;
-  // the big tiles when both convs qualify and pay for the two together (the rounds rule)
-  const int th = halo_big_ok(o0) && halo_big_ok(o1) &&
-                         halo_big_pays(halo_big_tiles(o0) + halo_big_tiles(o1), halo_small_tiles(o0) + halo_small_tiles(o1))
-                     ? HTH_BIG
-                     : HTH;
+  // each conv's own tile rows (the rounds rule, as raft_conv2d would pick them): the big f16x3 tiles
+  // run the scaled one-chain arithmetic, so only convs that pick the same rows share a launch, which
+  // keeps the pair bit-identical to the two single launches (raft_hip.h); otherwise they run in order
+  const int th = halo_pick_th(o0, false);
+  if (halo_pick_th(o1, false) != th) return 1;
   halo_set_th(o0, l.a[0], th);
   halo_set_th(o1, l.a[1], th);
   const long s0 = halo_spatial(l.a[0]), s1 = halo_spatial(l.a[1]);

@@ -105,11 +105,16 @@ def test_multi_tile_encoder_features(H, W, B, prec):
     assert float(((got[..., 1] - r) / r).abs().max()) < 1e-5
 
 
-@pytest.mark.parametrize("prec,k,shapes", [("f16x3", 3, [(256, 192), (128, 64)]),
-                                           ("bf16", 1, [(256, 256), (128, 128)])])   # (1x1: no big tiles)
-def test_multi_tile_pair_launch_equals_two_convs(prec, k, shapes):
+@pytest.mark.parametrize("prec,k,shapes,scaled", [
+    ("f16x3", 3, [(256, 192), (128, 64)], False),
+    ("f16x3", 3, [(256, 192), (128, 64)], True),    # both convs pick the 16x16 tiles: one launch
+    ("f16x3", 3, [(256, 192), (128, 32)], True),    # 16x16 vs 128-pixel tiles: run in order
+    ("bf16", 1, [(256, 256), (128, 128)], False)])  # (1x1: no big tiles)
+def test_multi_tile_pair_launch_equals_two_convs(prec, k, shapes, scaled):
     """A multi-round raft_conv2d_pair (each conv's tiles on their own work-groups, several per
-    work-group) == the two convs launched alone (other tile counts per work-group), bit for bit."""
+    work-group) == the two convs launched alone (other tile counts per work-group), bit for bit,
+    also with the column-scaled split weight set (raft_hip.h: the pair's contract; a pair whose convs
+    pick different tile rows runs them in order)."""
     from raft_optical_flow_amd import _lib
     from raft_optical_flow_amd import kernels as K
     B, H, W = 8, 55, 128
@@ -124,14 +129,16 @@ def test_multi_tile_pair_launch_equals_two_convs(prec, k, shapes):
         pcs.append(pc)
         pair.append(K.Rows(torch.full((B * H * W, cout), 7.0, device=DEV)))
         seq.append(K.Rows(torch.full((B * H * W, cout), 7.0, device=DEV)))
-    # (f16x3 without the scaled weight: the pair and the single launches all take the 128-pixel
-    # tiles; with it the rounds rule may give them different tile sizes, i.e. different arithmetic)
     prm = [K.conv_params(pcs[i], xs[i], B, H, W, pair[i], epilogue=_lib.EPI_RELU) for i in range(2)]
     one = [K.conv_params(pcs[i], xs[i], B, H, W, seq[i], epilogue=_lib.EPI_RELU) for i in range(2)]
-    for q in prm + one:
-        q.weight_s = None
+    if not scaled:  # (f16x3: every launch on the 128-pixel tiles)
+        for q in prm + one:
+            q.weight_s = None
     lib = _lib.load()
     assert lib.raft_conv2d_halo_tiles_per_wg(ctypes.byref(one[0])) > 1
+    if scaled:
+        rows = [lib.raft_conv2d_halo_tile_rows(ctypes.byref(q)) for q in one]
+        assert rows[0] == 16 and rows[1] == (16 if shapes[1][1] % 64 == 0 else 8), rows
     K.conv_pair_launch(prm[0], prm[1])(K.stream_handle())
     for q in one:
         K.conv_launch(q)(K.stream_handle())

@@ -1,7 +1,7 @@
 """Phase stamps of the alternate lookup's MFMA tile kernel (a -DALT_STAMPS variant):
 
     make -C raft_optical_flow_amd/csrc variant NAME=altst DEFS=-DALT_STAMPS
-    RAFT_HIP_LIB=variants/altst/libraft_hip.so python tools/alt_stamps.py [B] [spread_px]
+    RAFT_HIP_LIB=ab/altst/libraft_hip.so python tools/alt_stamps.py [B] [spread_px]
 
 One raft_alt_corr_lookup_levels launch at the config-3 shape (tools/alt_bench.py's smooth
 synthetic flow); prints per-wave cycle means of each phase for an MFMA wave (0) and a

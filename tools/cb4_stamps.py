@@ -1,7 +1,7 @@
 """Phase stamps of corr_build4_kernel (a -DCB4_STAMPS variant):
 
     make -C raft_optical_flow_amd/csrc variant NAME=cb4st DEFS=-DCB4_STAMPS
-    RAFT_HIP_LIB=variants/cb4st/libraft_hip.so python tools/cb4_stamps.py [B H8 W8]
+    RAFT_HIP_LIB=ab/cb4st/libraft_hip.so python tools/cb4_stamps.py [B H8 W8]
 
 One raft_corr_build_ws launch; per-wave cycle means of each phase (waves 0 and 7) and units per
 work-group."""

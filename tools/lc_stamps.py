@@ -1,7 +1,7 @@
 """Phase stamps of the fused lookup + convc1 + convf1 kernel (a -DLC_STAMPS variant):
 
     make -C raft_optical_flow_amd/csrc variant NAME=lcst DEFS=-DLC_STAMPS
-    RAFT_HIP_LIB=variants/lcst/libraft_hip.so python tools/lc_stamps.py
+    RAFT_HIP_LIB=ab/lcst/libraft_hip.so python tools/lc_stamps.py
 
 Runs config 2 forwards eagerly, then replays the last iteration's fused launch alone once and
 prints per-wave cycle means of each phase and the launch's wall span (100 MHz realtime)."""
