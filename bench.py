@@ -35,6 +35,8 @@ The line also carries
   dominant_kernel  the step's dominant kernel, conv_halo_kernel<3,3,64> (convc2 and
                 the flow-head conv1), with the MFMA-busy PMC of the newest committed
                 profiles/rNN_halo_pmc.json taken on the current conv_halo.hip;
+  drop_in_forward  the same workload through RAFT.forward() itself (the unchanged caller's call, default
+                range guard: one host flag read per forward), beside `value`'s plan.replay() loop;
   fp32_exact    with the default f16x3 conv arithmetic: the same run with exact
                 f32 MFMA convs (value, ms_per_step), rank 0, N = 1;
   cpu_baseline  the reference's CPU path restated with the same torch CPU operators
@@ -593,6 +595,28 @@ def main():
                                      or hpmc.get("conv_halo_kernel<3, 3, 64, 1, false>") or {}).get("mfma_busy")
             dominant["mfma_busy_source"] = f"profiles/{hname}"
 
+    # the drop-in path itself: RAFT.forward() as demo.py / evaluate.py call it (core/raft.py:145-251;
+    # demo.py:58-67), on the same padded pool pairs, with the default range guard (one host-side flag
+    # read per forward) and the plan's hipGraph replay
+    drop_in = None
+    if world == 1:
+        def fwd(k):
+            with torch.no_grad():
+                return model(*pool[k % len(pool)], iters=args.iters, test_mode=True)
+        for k in range(max(1, args.warmup)):
+            fwd(k)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            fwd(k)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        drop_in = {"value": round(args.batch * args.steps / dt, 3), "ms_per_step": round(dt / args.steps * 1e3, 3),
+                   "range_guard": model.range_guard,
+                   "timing": f"{args.steps} RAFT.forward(image1, image2, iters={args.iters}, test_mode=True) calls "
+                             f"back to back (torch.no_grad), wall clock between two synchronizes; each forward "
+                             f"replays the plan's graph and reads its range-guard flag on the host"}
+
     exact = None
     if prec != "fp32" and world == 1 and not args.no_fp32_exact:
         model.conv_precision = "fp32"
@@ -623,6 +647,7 @@ def main():
             "iteration": iteration,
             "update_gemm": update_roof,
             "dominant_kernel": dominant,
+            "drop_in_forward": drop_in,
             "fp32_exact": exact,
             "cpu_baseline": cpu,
         }

@@ -137,6 +137,22 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
   const int y0 = (sr / g.tx_n) * LC_TH, x0 = (sr % g.tx_n) * LC_TW;
   const int H = a.H, W = a.W, P = H * W;
 
+  // The K stream of step 4, in registers: convc1's 11 K-steps (all waves) then convf1's 4 (waves
+  // 0-3), prefetched PF steps ahead.  LC_EARLY: the first PF steps are issued here, before the coords
+  // load, so that the weight bytes (the whole 360 KB split convc1 weight per work-group) stream in
+  // under the coords / window-tile round trips and the taps instead of after them.
+#ifndef LC_PF
+#define LC_PF 3
+#endif
+  constexpr int PF = LC_PF;
+  h8 wb[PF + 1][NT];
+  auto load_w = [&](int j, h8 (&dst)[NT]) {
+    const h8* wf = j < LC_KS ? g.wfrag + ((j * (LC_N / 32) + wv) * 4) * 64
+                             : g.f1frag + (((j - LC_KS) * (LC_F1N / 32) + wv) * 4) * 64;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) dst[t] = wf[t * 64 + lane];
+  };
+
   // ---- 1. the window tiles of this wave's four query pixels (the critical path) --------------
   const int ti = lane >> 4, tj = (lane >> 2) & 3, rr = lane & 3;
   const int lrow = ti * 4 + rr;
@@ -170,6 +186,12 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
 #pragma unroll
     for (int k = 1; k < LC_PX; ++k) gk = (lane & 3) == k ? px_gp[k] : gk;
     const float cx = a.coords[2L * gk], cy = a.coords[2L * gk + 1];
+#ifdef LC_EARLY  // (behind the coords load: its wait leaves the weight loads in flight)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < PF; ++j) load_w(j, wb[j]);
+    __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
     for (int k = 0; k < LC_PX; ++k) {
       px_x[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cx), k));
@@ -254,19 +276,12 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
   LC_STAMP(2);
 
   // ---- 3. the taps of each pixel -> split rows of convc1's A operand ------------------------
-  // The K stream of step 4, in registers: convc1's 11 K-steps (all waves) then convf1's 4 (waves
-  // 0-3), prefetched PF steps ahead; the first PF steps are issued here, behind the tiles, so they
-  // land during the taps.
-  constexpr int PF = 3;
-  h8 wb[PF + 1][NT];
-  auto load_w = [&](int j, h8 (&dst)[NT]) {
-    const h8* wf = j < LC_KS ? g.wfrag + ((j * (LC_N / 32) + wv) * 4) * 64
-                             : g.f1frag + (((j - LC_KS) * (LC_F1N / 32) + wv) * 4) * 64;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) dst[t] = wf[t * 64 + lane];
-  };
+  // (default: the first PF K-steps of the weight stream are issued here, behind the tiles, so they
+  // land during the taps)
+#ifndef LC_EARLY
 #pragma unroll
   for (int j = 0; j < PF; ++j) load_w(j, wb[j]);
+#endif
   char* Abase = smem;
   bool big = false;
   auto patch_of = [&](int k) {
