@@ -114,7 +114,16 @@ struct HaloCfg {
   static constexpr int D = halo_lds_bytes(T, U, 3, BNT, PI, WR) <= LB ? 3 : 2;
 #endif
   static constexpr int PA = patch_slots(T, U, D);
-  static constexpr int SB = U * (D + 1);  // weight-block ring (K-steps)
+  // DW: the weight DMAs' lead in super-steps (dev builds: HALO_WX more than the patches' D on the
+  // pre-split patch path where the longer weight ring fits)
+#ifndef HALO_WX
+#define HALO_WX 0
+#endif
+  static constexpr int DW = (T > 1 && D == 3 && HALO_WX > 0 &&
+                             U * (D + HALO_WX + 1) * BNT * WR + PA * PI * 1024 + 16 * 1024 <= LB)
+                                ? D + HALO_WX
+                                : D;
+  static constexpr int SB = U * (DW + 1);  // weight-block ring (K-steps)
   static constexpr int LDS_B = SB * BNT * WR, LDS_A = PA * PI * 1024;
 };
 
@@ -177,6 +186,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
   constexpr bool BF = PREC == RAFT_PREC_BF16;
   using C = HaloCfg<KH, KW, BNT, X3 ? 128 : 64, TH>;
   constexpr int T = C::T, U = C::U, D = C::D, PW = C::PW, NPIX = C::NPIX, PI = C::PI, PA = C::PA, SB = C::SB;
+  constexpr int DW = C::DW;  // weight lead (== D unless HALO_WX)
   // Weight rows in LDS: f16x3 the packed K-step row as it is (32 hi then 32 lo halves, 128 B);
   // the one-product modes (F16, BF16) read only hi, so only the 64-B hi half of each row
   // moves (half the weight bytes a CU ingests per K-step).  16-B quads XOR-swizzled by row
@@ -282,7 +292,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
     const int n0 = MT && in ? nt * BNT : 0;
     // packed K-step (tap, chunk) of the tile's N-tile rows
     const unsigned soff = in ? (unsigned)(t * nch + c) * 128u + (unsigned)n0 * ((unsigned)a.K * 4u) : 0u;
-    char* dst = smem + (U * (u % (D + 1)) + ew) * (BNT * WROW) + wpc0 * 1024;
+    char* dst = smem + (U * (u % (DW + 1)) + ew) * (BNT * WROW) + wpc0 * 1024;
 #pragma unroll
     for (int k = 0; k < NWP; ++k) dma16(rs_w, dst + k * 1024, in ? wvoff[k] : OFF_INVALID, soff);
   };
@@ -502,10 +512,13 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
             pend_c = c;
             nnew = 2 * TI;
           }
-          issue_weights(s + D);
+        }
+        if (s + DW < NS) {
+          issue_weights(s + DW);
           nnew += NWP;
         }
-        wait_vm_n(s + 1 < NS ? nnew : 0);
+        // set s+2 has landed: the weight sets issued in the last DW - D super-steps may fly on
+        wait_vm_n(s + 1 < NS ? nnew + (DW - D) * NWP : 0);
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): a patch stored this super-step is in LDS
         __builtin_amdgcn_s_barrier();
       }
@@ -751,8 +764,8 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
   // loop body has no branches.  A tile's last super-step reads nothing ahead
   // (the next tile's first fragments are read after its epilogue).
 #pragma unroll
-  for (int u = 0; u < D; ++u) issue_weights(u);
-  wait_vm<NWP * (D - 2)>();      // the weights of sets 0 and 1 (sets 2 .. D-1: before the first loop barrier)
+  for (int u = 0; u < DW; ++u) issue_weights(u);
+  wait_vm<NWP * (DW - 2)>();      // the weights of sets 0 and 1 (sets 2 .. D-1: before the first loop barrier)
   __builtin_amdgcn_s_barrier();  // load sets 0 and 1 have landed
 #ifdef HALO_PRIO
   __builtin_amdgcn_s_setprio(HALO_PRIO);
