@@ -131,6 +131,7 @@ struct HaloCfg {
 // per compute wave: realtime at entry / exit (100 MHz), then shader cycles of
 // the prologue, compute, wait + barrier, epilogue
 __device__ unsigned long long g_hstamp[8 * 16384];
+__device__ unsigned long long g_lstamp[8 * 16384];  // loader waves (pre-split patch path)
 __device__ __forceinline__ unsigned long long hstamp_real() {
   unsigned long long t;
   __builtin_amdgcn_sched_barrier(0);
@@ -497,12 +498,20 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
       // and issue the weights of set s+D, wait until set s+2's weights (issued
       // in s-1) have landed, barrier.
       int pend_k = -1, pend_c = 0;  // chunk staged in pv[0], loaded during the previous super-step
+#ifdef STAMPS
+      unsigned long long l_st = 0, l_ld = 0, l_w = 0, l_wait = 0, l_bar = 0, l0 = hstamp_now(), l1;
+      const unsigned long long l_loop = l0;
+#define LSTAMP(acc) (l1 = hstamp_now(), acc += l1 - l0, l0 = l1)
+#else
+#define LSTAMP(acc)
+#endif
       for (int s = 0; s < NS; ++s) {
         if (pend_k >= 0) {
           wait_vm<NWP>();  // that patch's loads (the weights issued after them may fly on)
           store_patch(pend_k, pend_c, pv[0]);
           pend_k = -1;
         }
+        LSTAMP(l_st);
         int nnew = 0;
         if (s + D < NS) {
           int kt, c;
@@ -513,15 +522,35 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
             nnew = 2 * TI;
           }
         }
+        LSTAMP(l_ld);
         if (s + DW < NS) {
           issue_weights(s + DW);
           nnew += NWP;
         }
+        LSTAMP(l_w);
         // set s+2 has landed: the weight sets issued in the last DW - D super-steps may fly on
         wait_vm_n(s + 1 < NS ? nnew + (DW - D) * NWP : 0);
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): a patch stored this super-step is in LDS
+        LSTAMP(l_wait);
         __builtin_amdgcn_s_barrier();
+        LSTAMP(l_bar);
       }
+#undef LSTAMP
+#ifdef STAMPS
+      {  // per loader wave: patch split + store, patch load issue, weight DMA issue, vmcnt wait, barrier, loop total
+        const unsigned lid = blockIdx.x * 4 + lw;
+        if (lane == 0 && lid < 16384) {
+          unsigned long long* g = g_lstamp + lid * 8;
+          g[0] = l_st;
+          g[1] = l_ld;
+          g[2] = l_w;
+          g[3] = l_wait;
+          g[4] = l_bar;
+          g[5] = hstamp_now() - l_loop;
+          g[6] = 1;
+        }
+      }
+#endif
       wait_vm<0>();
       return;
     }
@@ -1158,6 +1187,13 @@ void launch_halo(const HaloLaunch& l, int bn, int th, long wgs, hipStream_t s) {
 #ifdef STAMPS
 extern "C" int raft_debug_hstamps(unsigned long long* host, int n) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_hstamp), sizeof(unsigned long long) * (size_t)n);
+}
+extern "C" int raft_debug_lstamps(unsigned long long* host, int n, int clear) {
+  if (clear) {
+    static unsigned long long zero[8 * 16384];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_lstamp), zero, sizeof(zero));
+  }
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_lstamp), sizeof(unsigned long long) * (size_t)n);
 }
 #endif
 

@@ -41,6 +41,8 @@ for name, cin, cout, kh, kw, pad in SHAPES:
     out = torch.empty(Bq * H * W, cout, device=dev)
     prm = K.conv_params(pc, K.Rows(x), Bq, H, W, K.Rows(out), epilogue=_lib.EPI_RELU)
     L = [K.conv_launch(prm)]
+    if __import__("os").environ.get("HSTAMPS"):
+        _lib.load().raft_debug_lstamps(None, 0, 1)
     for _ in range(3):
         L[0](K.stream_handle())
     torch.cuda.synchronize()
@@ -74,6 +76,15 @@ for name, cin, cout, kh, kw, pad in SHAPES:
         print(f"   halo stamps, {len(st)} compute waves: span {span:.1f} us, entry skew {(st[:, 0].max() - st[:, 0].min()) * 0.01:.1f} us, "
               f"clock {clk:.0f} MHz; cycles/wave: prologue {mean[2]:.0f} compute {mean[3]:.0f} "
               f"wait+barrier {mean[4]:.0f} epilogue {mean[5]:.0f} total {mean[6]:.0f}")
+        lb = np.zeros(8 * 16384, dtype=np.uint64)
+        lib.raft_debug_lstamps(ctypes.c_void_p(lb.ctypes.data), lb.size, 0)
+        ls = lb.reshape(-1, 8).astype(np.float64)
+        ls = ls[ls[:, 6] > 0]
+        if len(ls):
+            lm = ls.mean(0)
+            print(f"   loader stamps, {len(ls)} waves (cycles in the last launch): "
+                  f"patch store {lm[0]:.0f} patch load {lm[1]:.0f} weight DMA issue {lm[2]:.0f} vm wait {lm[3]:.0f} "
+                  f"barrier {lm[4]:.0f} loop {lm[5]:.0f}")
     if __import__("os").environ.get("STAMPS"):
         import ctypes
         import numpy as np

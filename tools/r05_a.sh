@@ -19,3 +19,7 @@ for V in lcst lcst7; do
   RAFT_SKIP_SRC_CHECK=1 RAFT_HIP_LIB=ab/$V/libraft_hip.so timeout -k 10 200 python tools/lc_stamps.py 2>&1 | grep -v amdgpu.ids || exit 1
 done
 ./tools/variant_bench.sh "base hwx1" f16x3 1 || exit 1
+for V in hst hstwx; do
+  echo "== halo stamps $V"
+  HSTAMPS=1 RAFT_SKIP_SRC_CHECK=1 RAFT_HIP_LIB=ab/$V/libraft_hip.so timeout -k 10 200 python tools/conv_bench.py 1 convc2,conv,zr_split,q_split,fh1 2>&1 | grep -v amdgpu.ids || exit 1
+done
