@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define RAFT_HIP_ABI_VERSION 16
+#define RAFT_HIP_ABI_VERSION 17
 
 /* Negative return codes (argument errors, raised before any launch). */
 #define RAFT_E_INVALID (-1)   /* bad size / null pointer / unsupported shape */
@@ -62,7 +62,9 @@ const char* raft_hip_source_hash(void);
  * raft_corr_lookup_conv launch takes the next of 256 slots and records the realtime counter
  * (100 MHz) at its first work-group's start and at its last work-group's end, after that
  * work-group's stores completed; raft_debug_launch_span_read copies n values (slot k: [2k] start,
- * [2k+1] end).  raft_debug_launch_span(0) clears the slots and stops numbering. */
+ * [2k+1] end).  raft_debug_launch_span(0) clears the slots and stops numbering.  Valid for eager
+ * launches from one host thread on one device only: a launch enqueued while its stream is being
+ * captured takes no slot (a graph would replay the slot it baked in). */
 int raft_debug_launch_span(int enable);
 int raft_debug_launch_span_read(unsigned long long* host, int n);
 /* Debug (tests only): fill the LDS of every CU with all-ones words (NaN as fp32, f16 and bf16) by
@@ -99,7 +101,9 @@ int raft_corr_build_prec(const float* fmap1, const float* fmap2, int ld, int B, 
  * 64 <= C <= 1024, both fmaps are split once into f16 hi | lo maps in ws and the volume is built on
  * 256 x 256 tiles (one fp32 accumulator chain for hi*hi, lo*hi, hi*lo; same ~2^-22 relative
  * accuracy); otherwise it is raft_corr_build_prec.  ws: >= raft_corr_build_ws_bytes(B, H, W, C)
- * bytes, 16-byte aligned.  RAFT_CORR_BUILD4=0: always raft_corr_build_prec. */
+ * bytes, 16-byte aligned; ws == NULL, or fmaps / pyramid / ws off 16-B alignment, also take
+ * raft_corr_build_prec (ws_bytes may then be 0).  RAFT_CORR_BUILD4=0: always raft_corr_build_prec.
+ * (Argument order since ABI 15: ..., pyramid, ws, ws_bytes, stream.) */
 size_t raft_corr_build_ws_bytes(int B, int H, int W, int C);
 int raft_corr_build_ws(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C,
                        int num_levels, float sqrt_c, int precision, float* pyramid, void* ws, size_t ws_bytes,
@@ -368,6 +372,14 @@ int raft_instnorm_merge(const float* part, int slots_per_image, int B, int C, in
 size_t raft_instnorm_merge_ws_floats(int slots_per_image, int B, int C);
 int raft_instnorm_merge_ws(const float* part, int slots_per_image, int B, int C, int stats_ld, float eps, void* ws,
                            float* stats, raft_stream_t stream);
+/* raft_instnorm_merge_ws as ONE launch: the level-1 block of a (64-channel group, image) whose
+ * group sums land last (an agent-scope counter per group and image) runs level 2, in level 2's
+ * order: the same statistics bit for bit, one kernel boundary fewer.  counters:
+ * raft_instnorm_merge_counters(B, C) ints, zero before the first call; every call leaves them zero
+ * (so a captured graph replays).  ws as raft_instnorm_merge_ws. */
+size_t raft_instnorm_merge_counters(int B, int C);
+int raft_instnorm_merge_fused(const float* part, int slots_per_image, int B, int C, int stats_ld, float eps, void* ws,
+                              int* counters, float* stats, raft_stream_t stream);
 
 /* Packed weight geometry for a conv (n_pad, k_pad in floats per row). */
 int raft_conv2d_packed_shape(int mode, int n, int kh, int kw, int cin, int* n_pad, int* k_pad);

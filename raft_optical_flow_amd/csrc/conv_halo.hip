@@ -40,6 +40,7 @@
 // three independent accumulator chains.  F16 (mixed precision) runs hi*hi;
 // BF16 rounds activations and weights to bf16 and runs one
 // v_mfma_f32_32x32x16_bf16 product (bf16 mixed precision).
+#include <atomic>
 #include <type_traits>
 
 #include "conv_common.hpp"
@@ -1048,15 +1049,21 @@ double halo_big_cost() {
   }();
   return v;
 }
+// the CU count of the device the launch runs on (the current device), cached per device: the tile
+// choice (rounds rule, tiles per work-group) follows it when one process drives several GPUs
 long halo_cus() {
-  static const long v = [] {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      return 256L;
-    return (long)cus;
-  }();
-  return v;
+  constexpr int MAXDEV = 64;
+  static std::atomic<int> cache[MAXDEV];  // 0 = not queried yet
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256L;
+  if (dev >= 0 && dev < MAXDEV) {
+    const int c = cache[dev].load(std::memory_order_relaxed);
+    if (c > 0) return (long)c;
+  }
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  if (dev >= 0 && dev < MAXDEV) cache[dev].store(cus, std::memory_order_relaxed);
+  return (long)cus;
 }
 bool halo_big_ok(const HaloOperands& o) {
   const raft_conv2d_params& p = o.p;

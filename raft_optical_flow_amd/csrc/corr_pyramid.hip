@@ -1352,10 +1352,12 @@ extern "C" int raft_corr_build_ws(const float* fmap1, const float* fmap2, int ld
   }();
   const long P = (long)H * W;
   // the 256 x 256 kernel: f16x3, C a multiple of 16 with >= 4 half-steps, 32-bit map offsets
+  // (no workspace, or an operand off 16-B alignment: the shape does not fit either, as in ABI 14)
   const bool fits = precision == RAFT_PREC_F16X3 && C % 16 == 0 && C >= 64 && C <= 1024 && ld % 4 == 0 &&
-                    ld >= C && (double)B * P * C * 4 < 2147483648.0;
+                    ld >= C && (double)B * P * C * 4 < 2147483648.0 && ws != nullptr &&
+                    (((uintptr_t)fmap1 | (uintptr_t)fmap2 | (uintptr_t)pyramid | (uintptr_t)ws) & 15) == 0;
   if (!on || !fits) return raft_corr_build_prec(fmap1, fmap2, ld, B, H, W, C, L, sqrt_c, precision, pyramid, stream);
-  RAFT_REQUIRE(fmap1 && fmap2 && pyramid && ws, "raft_corr_build_ws: null pointer");
+  RAFT_REQUIRE(fmap1 && fmap2 && pyramid, "raft_corr_build_ws: null pointer");
   RAFT_REQUIRE(B > 0 && H > 0 && W > 0 && L >= 1 && L <= LK_MAXL, "raft_corr_build_ws: bad sizes");
   RAFT_REQUIRE(ws_bytes >= raft_corr_build_ws_bytes(B, H, W, C), "raft_corr_build_ws: workspace too small "
                "(raft_corr_build_ws_bytes)");

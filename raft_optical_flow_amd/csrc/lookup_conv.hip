@@ -584,7 +584,11 @@ extern "C" int raft_corr_lookup_conv(const float* pyramid, int B, int H, int W, 
   g.f1flag = f1_range_flag;
   g.tx_n = cdiv(W, LC_TW);
   g.ty_n = cdiv(H, LC_TH);
-  g.span_slot = g_lc_span_next >= 0 && g_lc_span_next < LC_SPAN_SLOTS ? g_lc_span_next++ : -1;
+  // (span timing: eager launches only, one thread, one device: a captured launch would bake its slot into
+  // the graph; raft_debug_launch_span)
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  const bool capturing = hipStreamIsCapturing(as_stream(stream), &cap) == hipSuccess && cap != hipStreamCaptureStatusNone;
+  g.span_slot = !capturing && g_lc_span_next >= 0 && g_lc_span_next < LC_SPAN_SLOTS ? g_lc_span_next++ : -1;
   const long nt = (long)B * g.tx_n * g.ty_n;
   RAFT_REQUIRE(nt < (1L << 31), "raft_corr_lookup_conv: grid too large");
   hipStream_t s = as_stream(stream);

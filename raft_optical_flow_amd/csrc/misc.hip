@@ -470,6 +470,102 @@ __global__ __launch_bounds__(64 * MERGE2_WAVES) void instnorm_merge2_kernel(cons
   stats[2 * ((long)b * C + c) + 1] = (float)(1.0 / sqrt(var + (double)eps));
 }
 
+// raft_instnorm_merge_fused: level 1 and level 2 in ONE launch.  Each level-1 block stores its
+// group's sums write-through (sc1) and adds to the (channel group, image) counter; the block whose add
+// comes last runs level 2 over the G group sums (sc1 loads, after its add returned / a block barrier:
+// MI355X_MICROARCH.md's last-arriver hand-off) in exactly merge2's order, so the statistics equal
+// raft_instnorm_merge_ws's bit for bit; it then clears the counter for the next launch.
+__global__ __launch_bounds__(256) void instnorm_merge_fused_kernel(const float* part, int slots, int C, int ld,
+                                                                   double* ws, int G, float eps, float* stats,
+                                                                   int* counters) {
+  __shared__ double red[MERGE2_WAVES][3][64];  // (level 1 uses rows 0-3)
+  __shared__ int is_last;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane, b = blockIdx.y, g = blockIdx.z;
+  const bool cok = c < C;
+  const float* pb = part + ((long)b * slots * ld + (cok ? c : 0)) * 4;
+  const float K = cok ? pb[1] : 0.f;  // slot 0's mean (slot 0 always holds pixels)
+  {
+    f32x4 v[MERGE_SPG / 4];
+#pragma unroll
+    for (int i = 0; i < MERGE_SPG / 4; ++i) {
+      const int k = g * MERGE_SPG + w + 4 * i;
+      v[i] = (cok && k < slots) ? *reinterpret_cast<const f32x4*>(pb + (long)k * ld * 4) : f32x4{};
+    }
+    double n = 0.0, s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < MERGE_SPG / 4; ++i) {
+      const double cnt = v[i][0], d = (double)v[i][1] - (double)K;
+      n += cnt;
+      s1 += cnt * d;
+      s2 += (double)v[i][2] + cnt * d * d;
+    }
+    red[w][0][lane] = n;
+    red[w][1][lane] = s1;
+    red[w][2][lane] = s2;
+  }
+  __syncthreads();
+  int* cnt = counters + (long)b * gridDim.x + blockIdx.x;
+  if (w == 0) {
+    if (cok) {
+      unsigned long long* o = reinterpret_cast<unsigned long long*>(ws + (((long)b * G + g) * C + c) * 3);
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        __hip_atomic_store(o + q,
+                           __double_as_longlong(((red[0][q][lane] + red[1][q][lane]) + red[2][q][lane]) + red[3][q][lane]),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sums have left for memory (sc1)
+    if (lane == 0) is_last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
+  }
+  __syncthreads();
+  if (!is_last) return;
+  // level 2 (merge2's order: its wave k sums groups k, k + 16, ... in batches of 8; wave w here runs
+  // merge2's waves w, w + 4, w + 8, w + 12)
+  const unsigned long long* p = reinterpret_cast<const unsigned long long*>(ws + ((long)b * G * C + (cok ? c : 0)) * 3);
+  for (int kk = w; kk < MERGE2_WAVES; kk += 4) {
+    double n = 0.0, s1 = 0.0, s2 = 0.0;
+    for (int g0 = kk; g0 < G; g0 += 8 * MERGE2_WAVES) {
+      double t[8][3];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int gg = g0 + MERGE2_WAVES * i;
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          t[i][q] = (cok && gg < G) ? __longlong_as_double(__hip_atomic_load(p + (long)gg * C * 3 + q, __ATOMIC_RELAXED,
+                                                                              __HIP_MEMORY_SCOPE_AGENT))
+                                    : 0.0;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        n += t[i][0];
+        s1 += t[i][1];
+        s2 += t[i][2];
+      }
+    }
+    red[kk][0][lane] = n;
+    red[kk][1][lane] = s1;
+    red[kk][2][lane] = s2;
+  }
+  __syncthreads();
+  if (w != 0) return;
+  if (lane == 0) *cnt = 0;  // (the next launch starts from zero; kernel boundary orders it)
+  if (!cok) return;
+  double n = 0.0, s1 = 0.0, s2 = 0.0;
+#pragma unroll
+  for (int k = 0; k < MERGE2_WAVES; ++k) {
+    n += red[k][0][lane];
+    s1 += red[k][1][lane];
+    s2 += red[k][2][lane];
+  }
+  const double Kd = K;
+  const double mean = n > 0.0 ? Kd + s1 / n : 0.0;
+  const double m2 = n > 0.0 ? fmax(s2 - s1 * s1 / n, 0.0) : 0.0;
+  const double var = n > 0.0 ? m2 / n : 0.0;
+  stats[2 * ((long)b * C + c)] = (float)mean;
+  stats[2 * ((long)b * C + c) + 1] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
 // nn.GroupNorm statistics (core/extractor.py:23-25, the blocks' norm_fn='group'): one block per
 // (group, image); mean, then the variance around it, over the group's C/G channels x HW pixels in
 // double with a fixed-order tree (deterministic); written per (image, channel) as the {mean, rstd}
@@ -682,6 +778,24 @@ extern "C" int raft_instnorm_merge_ws(const float* part, int slots_per_image, in
   hipLaunchKernelGGL(instnorm_merge2_kernel, dim3(cdiv(C, 64), B), dim3(64 * MERGE2_WAVES), 0, s, part, slots_per_image, C, stats_ld,
                      reinterpret_cast<const double*>(ws), G, eps, stats);
   return check_launch("raft_instnorm_merge_ws");
+}
+
+extern "C" size_t raft_instnorm_merge_counters(int B, int C) {
+  if (B <= 0 || C <= 0) return 0;
+  return (size_t)B * cdiv(C, 64);
+}
+
+extern "C" int raft_instnorm_merge_fused(const float* part, int slots_per_image, int B, int C, int stats_ld, float eps,
+                                         void* ws, int* counters, float* stats, raft_stream_t stream) {
+  RAFT_REQUIRE(part && ws && counters && stats && slots_per_image > 0 && B > 0 && C > 0 && stats_ld >= C && B < 65536,
+               "raft_instnorm_merge_fused: bad arguments");
+  RAFT_REQUIRE(aligned16(part) && ((uintptr_t)ws & 7) == 0 && ((uintptr_t)counters & 3) == 0,
+               "raft_instnorm_merge_fused: part 16-B, ws 8-B, counters 4-B aligned");
+  const int G = cdiv(slots_per_image, MERGE_SPG);
+  RAFT_REQUIRE(G < 65536, "raft_instnorm_merge_fused: too many slots");
+  hipLaunchKernelGGL(instnorm_merge_fused_kernel, dim3(cdiv(C, 64), B, G), dim3(256), 0, as_stream(stream), part,
+                     slots_per_image, C, stats_ld, reinterpret_cast<double*>(ws), G, eps, stats, counters);
+  return check_launch("raft_instnorm_merge_fused");
 }
 
 extern "C" int raft_instnorm_apply(const float* x, int ld, const float* stats, const float* resid, int resid_ld,

@@ -221,8 +221,17 @@ def _conv_in(L, A: Arena, pc: PackedConv, src: Rows, n_img, h, w, out: Rows, src
         L.append(conv_launch(p))
         st = A.flat(2 * n_img * out.c)
         ws = A.flat(_lib.load().raft_instnorm_merge_ws_floats(slots, n_img, out.c))
-        L.append(Launch("raft_instnorm_merge_ws", part.data_ptr(), slots, n_img, out.c, out.c, 1e-5, ws.data_ptr(),
-                        st.data_ptr()))
+        if os.environ.get("RAFT_MERGE_FUSED", "1") != "0":
+            # one launch (the last level-1 block per channel group and image runs level 2); its
+            # counters start at zero and every launch leaves them zero
+            cnt = torch.zeros(int(_lib.load().raft_instnorm_merge_counters(n_img, out.c)), dtype=torch.int32,
+                              device=A.device)
+            A.bufs.append(cnt)
+            L.append(Launch("raft_instnorm_merge_fused", part.data_ptr(), slots, n_img, out.c, out.c, 1e-5,
+                            ws.data_ptr(), cnt.data_ptr(), st.data_ptr()))
+        else:
+            L.append(Launch("raft_instnorm_merge_ws", part.data_ptr(), slots, n_img, out.c, out.c, 1e-5,
+                            ws.data_ptr(), st.data_ptr()))
         return st
     L.append(conv_launch(p))
     return _in_stats(L, A, out, n_img, ho * wo)
@@ -654,10 +663,13 @@ class RaftPlan:
             # mode, the fp32-accurate f16 split otherwise (raft_hip.h)
             cprec = _lib.PREC_FP32 if pk.precision == _lib.PREC_FP32 else _lib.PREC_F16X3
             # (f16x3: fmaps split once into the workspace, the volume on 256 x 256 tiles: raft_hip.h)
-            wsb = int(_lib.load().raft_corr_build_ws_bytes(B, h, w, C))
-            self.corr_ws = A.flat((wsb + 3) // 4)
+            # (the workspace only where the library takes that path: raft_corr_build_ws)
+            fits4 = (cprec == _lib.PREC_F16X3 and C % 16 == 0 and 64 <= C <= 1024 and B * h * w * C * 4 < 2 ** 31
+                     and os.environ.get("RAFT_CORR_BUILD4", "1") != "0")
+            wsb = int(_lib.load().raft_corr_build_ws_bytes(B, h, w, C)) if fits4 else 0
+            self.corr_ws = A.flat((wsb + 3) // 4) if fits4 else None
             L.append(Launch("raft_corr_build_ws", fmap1.data_ptr(), fmap2.data_ptr(), C, B, h, w, C, lv, div,
-                            cprec, self.pyramid.data_ptr(), self.corr_ws.data_ptr(), wsb))
+                            cprec, self.pyramid.data_ptr(), self.corr_ws.data_ptr() if fits4 else None, wsb))
         else:
             # AlternateCorrBlock pools num_levels times (core/corr.py:157-161); the
             # last level is never used, but its existence is the reference's size check.

@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_queries_without_gpu():
     lib = _lib.load()
-    assert lib.raft_hip_abi_version() == _lib.ABI_VERSION == 16
+    assert lib.raft_hip_abi_version() == _lib.ABI_VERSION == 17
     # the library was built from the sources beside it (csrc/Makefile SRC_HASH)
     assert lib.raft_hip_source_hash().decode() == _lib.source_hash()
     assert lib.raft_hip_arch() == b"gfx950"
@@ -57,6 +57,9 @@ def test_argument_errors_are_reported_without_launch():
     assert b"null" in lib.raft_hip_last_error()
     rc = lib.raft_corr_build(16, 16, 256, 1, 8, 8, 102, 4, 10.0, 16, None)  # C % 4 != 0
     assert rc == -1 and b"multiple of 4" in lib.raft_hip_last_error()
+    rc = lib.raft_instnorm_merge_fused(None, 4, 1, 64, 64, 1e-5, None, None, None, None)
+    assert rc == -1 and b"bad arguments" in lib.raft_hip_last_error()
+    assert lib.raft_instnorm_merge_counters(2, 96) == 4 and lib.raft_instnorm_merge_counters(0, 64) == 0
     rc = lib.raft_conv2d_pair(None, None, None)
     assert rc == -1 and b"null params" in lib.raft_hip_last_error()
     # the fused lookup + convf1 checks its convf1 arguments before any launch

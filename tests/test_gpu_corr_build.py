@@ -107,3 +107,32 @@ def test_corr_build_ws_matches_the_plain_build():
     assert float((a - b).abs().max()) < 1e-5 * max(1.0, float(b.abs().max()))
     assert torch.equal(_build_ws(f1, f2, C, B, H, W, C, L, pad=0.0), a)
     assert _lib.load().raft_corr_build_ws_bytes(B, H, W, C) == 2 * B * H * W * C * 4 + 4096
+
+
+def test_corr_build_ws_without_workspace_falls_back():
+    """raft_corr_build_ws with ws == NULL (ws_bytes 0), or with an operand off 16-B alignment, takes
+    raft_corr_build_prec: the same pyramid bit for bit (argument order: ..., pyramid, ws, ws_bytes,
+    stream)."""
+    from raft_optical_flow_amd import _lib
+    from raft_optical_flow_amd import kernels as K
+    B, H, W, C, L = 1, 24, 40, 128, 4
+    g = torch.Generator(device=DEV).manual_seed(4)
+    f = torch.randn(2 * B * H * W, C, device=DEV, generator=g)
+    f1, f2 = f[: B * H * W], f[B * H * W:]
+    n = int(_lib.load().raft_corr_pyramid_floats(B, H, W, L))
+    ref = torch.zeros(n, device=DEV)  # (tile padding the builds may leave unwritten: zeros in all three)
+    _lib.call("raft_corr_build_prec", f1.data_ptr(), f2.data_ptr(), C, B, H, W, C, L, K.sqrt_c(C), _lib.PREC_F16X3,
+              ref.data_ptr(), K.stream_handle())
+    out = torch.zeros(n, device=DEV)
+    _lib.call("raft_corr_build_ws", f1.data_ptr(), f2.data_ptr(), C, B, H, W, C, L, K.sqrt_c(C), _lib.PREC_F16X3,
+              out.data_ptr(), None, 0, K.stream_handle())
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    # a workspace off 16-B alignment: the same fallback
+    wsb = int(_lib.load().raft_corr_build_ws_bytes(B, H, W, C))
+    ws = torch.empty(wsb // 4 + 8, device=DEV)
+    out2 = torch.zeros(n, device=DEV)
+    _lib.call("raft_corr_build_ws", f1.data_ptr(), f2.data_ptr(), C, B, H, W, C, L, K.sqrt_c(C), _lib.PREC_F16X3,
+              out2.data_ptr(), ws.data_ptr() + 4, wsb, K.stream_handle())
+    torch.cuda.synchronize()
+    assert torch.equal(out2, ref)

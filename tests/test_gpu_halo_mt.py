@@ -98,6 +98,15 @@ def test_multi_tile_encoder_features(H, W, B, prec):
     stats = torch.empty(2 * B * cout, device=DEV)
     _lib.call("raft_instnorm_merge_ws", part.data_ptr(), slots, B, cout, cout, 1e-5, ws.data_ptr(), stats.data_ptr(),
               K.stream_handle())
+    # the one-launch merge: the same statistics bit for bit, counters left zero (twice: a replay)
+    cnt = torch.zeros(int(lib.raft_instnorm_merge_counters(B, cout)), dtype=torch.int32, device=DEV)
+    for _ in range(2):
+        stats1 = torch.full_like(stats, float("nan"))
+        _lib.call("raft_instnorm_merge_fused", part.data_ptr(), slots, B, cout, cout, 1e-5, ws.data_ptr(),
+                  cnt.data_ptr(), stats1.data_ptr(), K.stream_handle())
+        torch.cuda.synchronize()
+        assert torch.equal(stats1, stats)
+        assert int(cnt.abs().sum()) == 0
     got = stats.view(B, cout, 2).cpu().double()
     yd = out.t.view(B, H * W, cout).cpu().double()
     assert float((got[..., 0] - yd.mean(1)).abs().max()) < 1e-5 * max(1.0, float(yd.mean(1).abs().max()))
@@ -106,10 +115,10 @@ def test_multi_tile_encoder_features(H, W, B, prec):
 
 
 @pytest.mark.parametrize("prec,k,shapes,scaled", [
-    ("f16x3", 3, [(256, 192), (128, 64)], False),
-    ("f16x3", 3, [(256, 192), (128, 64)], True),    # both convs pick the 16x16 tiles: one launch
-    ("f16x3", 3, [(256, 192), (128, 32)], True),    # 16x16 vs 128-pixel tiles: run in order
-    ("bf16", 1, [(256, 256), (128, 128)], False)])  # (1x1: no big tiles)
+    ("f16x3", 3, [(256, 192, 8), (128, 64, 8)], False),
+    ("f16x3", 3, [(256, 192, 8), (128, 64, 8)], True),    # both convs pick the 16x16 tiles: one launch
+    ("f16x3", 3, [(256, 192, 8), (128, 64, 2)], True),    # 16x16 vs 128-pixel tiles: run in order
+    ("bf16", 1, [(256, 256, 8), (128, 128, 8)], False)])  # (1x1: no big tiles)
 def test_multi_tile_pair_launch_equals_two_convs(prec, k, shapes, scaled):
     """A multi-round raft_conv2d_pair (each conv's tiles on their own work-groups, several per
     work-group) == the two convs launched alone (other tile counts per work-group), bit for bit,
@@ -117,10 +126,10 @@ def test_multi_tile_pair_launch_equals_two_convs(prec, k, shapes, scaled):
     pick different tile rows runs them in order)."""
     from raft_optical_flow_amd import _lib
     from raft_optical_flow_amd import kernels as K
-    B, H, W = 8, 55, 128
+    H, W = 55, 128
     g = torch.Generator().manual_seed(5)
     xs, pcs, pair, seq = [], [], [], []
-    for cin, cout in shapes:
+    for cin, cout, B in shapes:
         x = torch.randn(B, cin, H, W, generator=g)
         w = torch.randn(cout, cin, k, k, generator=g) / np.sqrt(cin * k * k)
         pc = K.pack_conv(w, torch.randn(cout, generator=g), 1, (k // 2, k // 2), device=DEV)
@@ -129,16 +138,18 @@ def test_multi_tile_pair_launch_equals_two_convs(prec, k, shapes, scaled):
         pcs.append(pc)
         pair.append(K.Rows(torch.full((B * H * W, cout), 7.0, device=DEV)))
         seq.append(K.Rows(torch.full((B * H * W, cout), 7.0, device=DEV)))
-    prm = [K.conv_params(pcs[i], xs[i], B, H, W, pair[i], epilogue=_lib.EPI_RELU) for i in range(2)]
-    one = [K.conv_params(pcs[i], xs[i], B, H, W, seq[i], epilogue=_lib.EPI_RELU) for i in range(2)]
+    bs = [sh[2] for sh in shapes]
+    prm = [K.conv_params(pcs[i], xs[i], bs[i], H, W, pair[i], epilogue=_lib.EPI_RELU) for i in range(2)]
+    one = [K.conv_params(pcs[i], xs[i], bs[i], H, W, seq[i], epilogue=_lib.EPI_RELU) for i in range(2)]
     if not scaled:  # (f16x3: every launch on the 128-pixel tiles)
         for q in prm + one:
             q.weight_s = None
     lib = _lib.load()
-    assert lib.raft_conv2d_halo_tiles_per_wg(ctypes.byref(one[0])) > 1
-    if scaled:
+    if not scaled:  # (on the 16x16 tiles the cost rule keeps one tile per work-group here)
+        assert lib.raft_conv2d_halo_tiles_per_wg(ctypes.byref(one[0])) > 1
+    else:
         rows = [lib.raft_conv2d_halo_tile_rows(ctypes.byref(q)) for q in one]
-        assert rows[0] == 16 and rows[1] == (16 if shapes[1][1] % 64 == 0 else 8), rows
+        assert rows == ([16, 16] if bs[1] == 8 else [16, 8]), rows
     K.conv_pair_launch(prm[0], prm[1])(K.stream_handle())
     for q in one:
         K.conv_launch(q)(K.stream_handle())
