@@ -144,6 +144,9 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
 #ifndef LC_PF
 #define LC_PF 3
 #endif
+#ifndef LC_TAPS2
+#define LC_TAPS2 0
+#endif
   constexpr int PF = LC_PF;
   h8 wb[PF + 1][NT];
   auto load_w = [&](int j, h8 (&dst)[NT]) {
@@ -303,9 +306,17 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
         auto at = [](const char* bp, int byte) { return *reinterpret_cast<const float*>(bp + byte); };
 #pragma unroll
         for (int iy = 0; iy < RD; ++iy) {
+#if LC_TAPS2
+          // (8 of the entry's 16 bytes: one ds_read_b64, 2 LDS cycles, instead of a b96 read's 8; 1 - ty
+          // is the same fp32 subtraction axis_entry stored)
+          const int2 ye = *reinterpret_cast<const int2*>(&yt[l * RD + iy]);
+          const int ro = ye.x;
+          const float ty = __int_as_float(ye.y), sS = 1.0f - ty;
+#else
           const int4 ye = yt[l * RD + iy];
           const int ro = ye.x;
           const float ty = __int_as_float(ye.y), sS = __int_as_float(ye.z);
+#endif
           const f32x2 c0 = {at(p0, ro), at(p0, ro + 4 * RS)}, c1 = {at(p1, ro), at(p1, ro + 4 * RS)};
           const f32x2 hh = __builtin_elementwise_fma(c0, (f32x2){ex, ex}, c1 * (f32x2){xt[k], xt[k]});
           val[iy] = fmaf(sS, hh.x, ty * hh.y);
@@ -352,6 +363,41 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
   auto write_row = [&](int k, const float (&val)[RD]) {
     const int mk = LC_PX * wv + k;
     const int sw = (mk >> 1) & 7;
+#if LC_TAPS2
+    // the lane's nine consecutive channels as four 4-B writes of channel pairs (c even, c + 1: one
+    // f16 pair of one quad) and one 2-B write, per half: 10 LDS writes instead of 18
+    if (col) {
+      const int par = cbase & 1;
+      float vv[RD];
+#pragma unroll
+      for (int iy = 0; iy < RD; ++iy) {
+        vv[iy] = px_ok[k] ? val[iy] : 0.f;
+        big |= fabsf(vv[iy]) > RAFT_RANGE_LIMIT;
+      }
+      auto at_c = [&](int c, int half) {  // byte address of channel c's f16 in half 0 (hi) / 1 (lo)
+        const int j = c >> 5, kk = c & 31;
+        return Abase + j * (LC_M * 128) + mk * 128 + (((4 * half + (kk >> 3)) ^ sw) << 4) + 2 * (kk & 7);
+      };
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float a0 = par ? vv[2 * q + 1] : vv[2 * q], a1 = par ? vv[2 * q + 2] : vv[2 * q + 1];
+        _Float16 h0, l0, h1, l1;
+        split1<X3, BF>(a0, h0, l0);
+        split1<X3, BF>(a1, h1, l1);
+        const int c = cbase + 2 * q + par;  // even
+        *reinterpret_cast<h2*>(at_c(c, 0)) = h2{h0, h1};
+        if constexpr (X3) *reinterpret_cast<h2*>(at_c(c, 1)) = h2{l0, l1};
+      }
+      {
+        const float a = par ? vv[0] : vv[RD - 1];
+        _Float16 hs, ls;
+        split1<X3, BF>(a, hs, ls);
+        const int c = cbase + (par ? 0 : RD - 1);
+        *reinterpret_cast<_Float16*>(at_c(c, 0)) = hs;
+        if constexpr (X3) *reinterpret_cast<_Float16*>(at_c(c, 1)) = ls;
+      }
+    } else if (lane - LC_L * RD < 32 * LC_KS - LC_NTAP) {
+#else
     if (col) {
 #pragma unroll
       for (int iy = 0; iy < RD; ++iy) {
@@ -366,6 +412,7 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
         if constexpr (X3) *reinterpret_cast<_Float16*>(rb + (((4 + (kk >> 3)) ^ sw) << 4) + 2 * (kk & 7)) = lo;
       }
     } else if (lane - LC_L * RD < 32 * LC_KS - LC_NTAP) {
+#endif
       const int c = LC_NTAP + lane - LC_L * RD;
       const int j = c >> 5, kk = c & 31;
       char* rb = Abase + j * (LC_M * 128) + mk * 128;

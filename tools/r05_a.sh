@@ -13,8 +13,8 @@ for V in cur r3; do
   python tools/phase_summary.py gpurun_out/fp_$V/run_kernel_trace.csv > gpurun_out/phase_r05a_$V.txt 2>&1
   grep -E "forward span|encoder phase span|loop span" gpurun_out/phase_r05a_$V.txt
 done
-./tools/ab_variants.sh "base lce3 lce6 lce7 hwx1" || exit 1
-for V in lcst lcst7; do
+./tools/ab_variants.sh "base lce7 lct2 lct2e7 hwx1" || exit 1
+for V in lcst lcst7 lcst2; do
   echo "== stamps $V"
   RAFT_SKIP_SRC_CHECK=1 RAFT_HIP_LIB=ab/$V/libraft_hip.so timeout -k 10 200 python tools/lc_stamps.py 2>&1 | grep -v amdgpu.ids || exit 1
 done
