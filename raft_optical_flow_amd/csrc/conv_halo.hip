@@ -446,12 +446,27 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
               const int ch = 32 * c + (int)tg8;
               float e[8] = {src[i][0][0], src[i][0][1], src[i][0][2], src[i][0][3],
                             src[i][1][0], src[i][1][1], src[i][1][2], src[i][1][3]};
+              if ((in0_c & 7) == 0) {
+                // (uniform) the 8 channels' {mean, rstd} as four 16-B reads; a group lies wholly inside
+                // or past in0_c
+                const bool ok = pix_ok && ch < in0_c;
+                const f32x4* t4 = reinterpret_cast<const f32x4*>(tab + (ch < in0_c ? ch : 0));
+                const f32x4 q0 = t4[0], q1 = t4[1], q2 = t4[2], q3 = t4[3];
+                const float mn[8] = {q0[0], q0[2], q1[0], q1[2], q2[0], q2[2], q3[0], q3[2]};
+                const float rs[8] = {q0[1], q0[3], q1[1], q1[3], q2[1], q2[3], q3[1], q3[3]};
 #pragma unroll
-              for (int j = 0; j < 8; ++j) {
-                const bool ok = pix_ok && ch + j < in0_c;
-                const float2 mr = tab[ok ? ch + j : 0];
-                const float v = (e[j] - mr.x) * mr.y;
-                e[j] = ok ? (p.in_norm_relu ? fmaxf(v, 0.f) : v) : 0.f;
+                for (int j = 0; j < 8; ++j) {
+                  const float v = (e[j] - mn[j]) * rs[j];
+                  e[j] = ok ? (p.in_norm_relu ? fmaxf(v, 0.f) : v) : 0.f;
+                }
+              } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                  const bool ok = pix_ok && ch + j < in0_c;
+                  const float2 mr = tab[ok ? ch + j : 0];
+                  const float v = (e[j] - mr.x) * mr.y;
+                  e[j] = ok ? (p.in_norm_relu ? fmaxf(v, 0.f) : v) : 0.f;
+                }
               }
               h8 hi, lo;
               split8<X3, BF>(f32x4{e[0], e[1], e[2], e[3]}, f32x4{e[4], e[5], e[6], e[7]}, hi, lo);
