@@ -537,11 +537,19 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
             pend_c = c;
             nnew = 2 * TI;
           }
+          LSTAMP(l_ld);
+          // (in the same branch as the patch loads: on every path the compiler sees NWP DMAs behind
+          // them, so its own waits for the staged registers stay at vmcnt(NWP), not vmcnt(0))
+          if constexpr (DW == D) {
+            issue_weights(s + D);
+            nnew += NWP;
+          }
         }
-        LSTAMP(l_ld);
-        if (s + DW < NS) {
-          issue_weights(s + DW);
-          nnew += NWP;
+        if constexpr (DW > D) {
+          if (s + DW < NS) {
+            issue_weights(s + DW);
+            nnew += NWP;
+          }
         }
         LSTAMP(l_w);
         // set s+2 has landed: the weight sets issued in the last DW - D super-steps may fly on

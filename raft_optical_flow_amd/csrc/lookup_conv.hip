@@ -145,7 +145,7 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
 #define LC_PF 3
 #endif
 #ifndef LC_TAPS2
-#define LC_TAPS2 0
+#define LC_TAPS2 1
 #endif
   constexpr int PF = LC_PF;
   h8 wb[PF + 1][NT];
