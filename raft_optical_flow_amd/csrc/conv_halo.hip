@@ -785,6 +785,10 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
           for (int r = 0; r < 16; ++r) acc[f][sb][r] += accx[f][sb][r] * (1.0f / SPLIT_SCALE);
     }
     f32x4 stv[NSUB];  // ENC: the wave's InstanceNorm partials per column (its MF blocks combined)
+    // the output geometry read once (the kernel argument sits at a run-time offset, prob: read inside
+    // the row loop it was a scalar load and wait per row), rows by selects, not branches
+    const int oh = __builtin_amdgcn_readfirstlane(p.out_h), ow = __builtin_amdgcn_readfirstlane(p.out_w);
+    const int rowb = t.b * oh;
 #pragma unroll
     for (int f = 0; f < MF; ++f) {
       int rows[16];
@@ -792,7 +796,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
       for (int r = 0; r < 16; ++r) {
         const int mm = (r & 3) + 8 * (r >> 2) + 4 * h;
         const int y = t.y0 + 2 * (wm * MF + f) + (mm >> 4), x = t.x0 + (mm & 15);
-        rows[r] = (y < p.out_h && x < p.out_w) ? (t.b * p.out_h + y) * p.out_w + x : -1;
+        rows[r] = ((y < oh) & (x < ow)) ? (rowb + y) * ow + x : -1;
       }
 #pragma unroll
       for (int sb = 0; sb < NSUB; ++sb) tile_epilogue<false>(p, rows, t.n0 + cb + sb * 32 + m, acc[f][sb]);
