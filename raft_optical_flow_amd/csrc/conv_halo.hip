@@ -1113,10 +1113,28 @@ bool halo_big_pays(long big_tiles, long small_tiles) {
   if (mn <= 0 || big_tiles < mn) return false;
   return (double)cdiv_l(big_tiles, cus) * halo_big_cost() < (double)cdiv_l(small_tiles, cus);
 }
+// the least multi-tile plan cost of the conv on tiles of th rows (halo_plan_grid's cost, in tile times
+// of that size), below
+double halo_mt_plan_cost(const HaloOperands& o, int th);
+// RAFT_HALO_BIG_MT=1: where the rounds rule keeps the 128-pixel tiles, also compare the two tile sizes'
+// multi-tile plans (a launch with rounds to spare runs several tiles per work-group, so whole rounds are
+// not the unit there): big tiles when cost(big) * RAFT_HALO_BIG_COST < cost(128-pixel)
+bool halo_big_mt() {
+  static const bool v = [] {
+    const char* e = getenv("RAFT_HALO_BIG_MT");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
 // Tile rows of a conv's launch: HTH_BIG where the big tiles qualify and pay, and (the one-product
 // modes without encoder features) the 128-column tiles do not apply
 int halo_pick_th(const HaloOperands& o, bool wide) {
-  return !wide && halo_big_ok(o) && halo_big_pays(halo_big_tiles(o), halo_small_tiles(o)) ? HTH_BIG : HTH;
+  if (wide || !halo_big_ok(o)) return HTH;
+  if (halo_big_pays(halo_big_tiles(o), halo_small_tiles(o))) return HTH_BIG;
+  if (halo_big_mt() && halo_big_min() > 0 && halo_big_tiles(o) >= halo_big_min() &&
+      halo_mt_plan_cost(o, HTH_BIG) * halo_big_cost() < halo_mt_plan_cost(o, HTH))
+    return HTH_BIG;
+  return HTH;
 }
 // the big tiles' operands: spatial tiles of TH_BIG rows; f16x3 reads the scaled weight
 void halo_set_th(const HaloOperands& o, HaloArgs& a, int th) {
@@ -1175,8 +1193,8 @@ bool halo_mt_ok(const HaloArgs& a, int bn, int th, long m) {
   return true;
 }
 // sets l.m (spatial tiles per work-group) and l.grid0 for the launch of l.a[0] (and l.a[1] of a
-// pair, pair = true); returns the grid size
-long halo_plan_grid(HaloLaunch& l, int bn, int th, bool pair) {
+// pair, pair = true); returns the grid size (cost_out: the plan's cost in tile times)
+long halo_plan_grid(HaloLaunch& l, int bn, int th, bool pair, double* cost_out = nullptr) {
   const long cus = halo_cus();
   const long s0 = halo_spatial(l.a[0]), s1 = pair ? halo_spatial(l.a[1]) : 0;
   const long g0 = l.a[0].gn, g1 = pair ? l.a[1].gn : 0;
@@ -1184,9 +1202,9 @@ long halo_plan_grid(HaloLaunch& l, int bn, int th, bool pair) {
   // cost in tile times: rounds of work-groups x (the first tile + RAFT_HALO_MT_COST per later tile:
   // the prologue and the output stores of the later tiles run under the K loops)
   long m = 1;
+  double best = (double)cdiv_l(wgs(1), cus);
   if (halo_mt_enabled() && wgs(1) > cus) {
     const double f = halo_mt_cost();
-    double best = (double)cdiv_l(wgs(1), cus);
     for (long c = 2; c <= 64; ++c) {
       const double cost = (double)cdiv_l(wgs(c), cus) * (1.0 + f * (double)(c - 1));
       if (cost < best && halo_mt_ok(l.a[0], bn, th, c) && (!pair || halo_mt_ok(l.a[1], bn, th, c))) {
@@ -1199,7 +1217,20 @@ long halo_plan_grid(HaloLaunch& l, int bn, int th, bool pair) {
   l.sp0 = (int)s0;
   l.sp1 = (int)s1;
   l.grid0 = (int)(g0 * cdiv_l(s0, m));
+  if (cost_out) *cost_out = best;
   return wgs(m);
+}
+
+double halo_mt_plan_cost(const HaloOperands& o, int th) {
+  HaloLaunch l;
+  if (!halo_problem(o, l.a[0])) return 1e30;
+  halo_set_th(o, l.a[0], th);
+  const int bn = th == HTH_BIG ? 64 : halo_spatial(l.a[0]) * (o.n_pad / 64) > 128 ? 64 : 32;
+  l.a[0].gn = o.n_pad / bn;
+  l.a[1] = l.a[0];
+  double cost = 1e30;
+  halo_plan_grid(l, bn, th, false, &cost);
+  return cost;
 }
 
 void launch_halo(const HaloLaunch& l, int bn, int th, long wgs, hipStream_t s) {
