@@ -117,6 +117,7 @@ _PROTOS = {
     "raft_instnorm_merge_ws_floats": (c_size_t, [c_int, c_int, c_int]),
     "raft_instnorm_merge_ws": (c_int, [P, c_int, c_int, c_int, c_int, c_float, P, P, P]),
     "raft_instnorm_merge_counters": (c_size_t, [c_int, c_int]),
+    "raft_conv2d_set_halo_loaders": (c_int, [c_int]),
     "raft_instnorm_merge_fused": (c_int, [P, c_int, c_int, c_int, c_int, c_float, P, P, P, P]),
     "raft_conv2d_split_weight": (c_int, [P, P, c_int, c_int, P]),
     "raft_conv2d_split_weight_prec": (c_int, [P, P, c_int, c_int, c_int, P]),

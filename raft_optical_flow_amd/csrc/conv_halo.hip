@@ -182,7 +182,9 @@ constexpr int halo_norm_bytes(int LDS_B, int LDS_A, int D) {
 // its cost: no per-load-set tile / chunk divisions, the tile's patch offsets fixed once per lane,
 // one K loop and one epilogue (round 4's shared body had made every 128-pixel update conv 7-16 %
 // slower in the forward).
-template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH, bool MT = false>
+// NL: loader waves (4, or 8 for the one-tile f16x3 update convs: RAFT_HALO_NL8, a 768-thread
+// work-group whose loaders each issue half the weight DMAs and stage half of each patch)
+template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH, bool MT = false, int NL = 4>
 __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt, int st0, int ntl_arg, char* smem) {
   constexpr bool X3 = PREC == RAFT_PREC_F16X3;
   constexpr bool BF = PREC == RAFT_PREC_BF16;
@@ -198,7 +200,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
   constexpr int QPR = WROW / 16;               // 16-B quads per row
   constexpr int RPP = 1024 / WROW;             // rows per 1-KiB DMA piece
   constexpr int NBI = BNT / RPP;    // 1-KiB DMA pieces per weight block (one K-step)
-  constexpr int NWP = U * NBI / 4;  // weight pieces per loader wave per load set
+  constexpr int NWP = U * NBI / NL;  // weight pieces per loader wave per load set
   // Compute waves (32-pixel MFMA row blocks = two tile rows): TH = 8, BNT <= 64: 4 waves along M,
   // each one block (tile rows 2w, 2w+1) x all BNT columns; TH = 8, BNT = 128 (the one-product
   // modes' wide tiles): 2 x 2 waves, each 2 blocks (64 pixels) x 64 columns; TH = 16, BNT = 64:
@@ -229,8 +231,8 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
 #endif
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool loader = w >= 4;  // the last 4 waves move the operands, the others compute
-  const int lw = w & 3;
+  const bool loader = w >= 4;  // the last NL waves move the operands, the first 4 compute
+  const int lw = loader ? w - 4 : w;  // loader index (compute waves: their block index)
   const int wc = w & 3;  // compute waves: block index
 
   const HaloArgs& a = args[prob];
@@ -276,28 +278,38 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
   // every load set.  Load set u (counted over the work-group's tiles) is set u % ns_t of
   // tile u / ns_t; sets past the last tile load zeros.
   const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(p.weight, a.w_bytes);
-  const int ew = (lw * NWP) / NBI, wpc0 = (lw * NWP) % NBI;
-  unsigned wvoff[NWP];
+  struct WPieces {
+    int ew, wpc0;
+    unsigned off[NWP];
+  };
+  auto wpieces = [&](int li) {
+    WPieces q;
+    q.ew = (li * NWP) / NBI;
+    q.wpc0 = (li * NWP) % NBI;
 #pragma unroll
-  for (int k = 0; k < NWP; ++k) {
-    const int r = RPP * (wpc0 + k) + lane / QPR;
-    const int qd = X3 ? (lane & 7) ^ ((r >> 1) & 7) : (lane & 3) ^ ((r >> 2) & 3);
-    // (!MT: the N-tile's first row folded in here; MT: in soff, 0 for the zero sets past the last tile)
-    wvoff[k] = (unsigned)(r + (MT ? 0 : nt * BNT)) * ((unsigned)a.K * 4u) + (unsigned)qd * 16u;
-  }
-  auto issue_weights = [&](int u) {
+    for (int k = 0; k < NWP; ++k) {
+      const int r = RPP * (q.wpc0 + k) + lane / QPR;
+      const int qd = X3 ? (lane & 7) ^ ((r >> 1) & 7) : (lane & 3) ^ ((r >> 2) & 3);
+      // (!MT: the N-tile's first row folded in here; MT: in soff, 0 for the zero sets past the last tile)
+      q.off[k] = (unsigned)(r + (MT ? 0 : nt * BNT)) * ((unsigned)a.K * 4u) + (unsigned)qd * 16u;
+    }
+    return q;
+  };
+  const WPieces wp0 = wpieces(lw);
+  auto issue_weights_q = [&](int u, const WPieces& q) {
     int kt, ul;
     set_tile(u, kt, ul);
-    const int j = U * ul + ew;
+    const int j = U * ul + q.ew;
     const bool in = j < nk && (!MT || kt < ntl);
     const int c = j / T, t = j - c * T;
     const int n0 = MT && in ? nt * BNT : 0;
     // packed K-step (tap, chunk) of the tile's N-tile rows
     const unsigned soff = in ? (unsigned)(t * nch + c) * 128u + (unsigned)n0 * ((unsigned)a.K * 4u) : 0u;
-    char* dst = smem + (U * (u % (DW + 1)) + ew) * (BNT * WROW) + wpc0 * 1024;
+    char* dst = smem + (U * (u % (DW + 1)) + q.ew) * (BNT * WROW) + q.wpc0 * 1024;
 #pragma unroll
-    for (int k = 0; k < NWP; ++k) dma16(rs_w, dst + k * 1024, in ? wvoff[k] : OFF_INVALID, soff);
+    for (int k = 0; k < NWP; ++k) dma16(rs_w, dst + k * 1024, in ? q.off[k] : OFF_INVALID, soff);
   };
+  auto issue_weights = [&](int u) { issue_weights_q(u, wp0); };
 
   // the input's InstanceNorm (raft_conv2d_params.in_norm: relu((x - mean) / std) applied as the
   // loaders split the patch): the tables of the images of this work-group's tiles into LDS (the
@@ -309,7 +321,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
       b_first = tile_at(0).b;
       const int nb = tile_at(ntl - 1).b - b_first + 1;
       if (loader)
-        for (int i = 64 * lw + lane; i < nb * 2 * p.in0_c; i += 256)
+        for (int i = 64 * lw + lane; i < nb * 2 * p.in0_c; i += 64 * NL)
           norm_tab[i] = p.in_norm[(long)b_first * 2 * p.in0_c + i];
       __syncthreads();
     }
@@ -341,14 +353,14 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
     };
     // Patch pieces of this loader: i = lw, lw+4, ... (< PI), pixels 8i .. 8i+7; per chunk the
     // tile's pixel offsets plus the channel offset
-    constexpr int PK = (PI + 3) / 4;
-    const int pcw = PI > lw ? (PI - 1 - lw) / 4 + 1 : 0;  // this wave's pieces per patch
+    constexpr int PK = (PI + NL - 1) / NL;
+    const int pcw = PI > lw ? (PI - 1 - lw) / NL + 1 : 0;  // this wave's pieces per patch
     // per lane and piece: the channel quad within a chunk (swizzled source) x 4, and (!MT) the
     // input pixel of the one tile, fixed for the work-group
     unsigned pq4[PK], ppix0[PK];
 #pragma unroll
     for (int k = 0; k < PK; ++k) {
-      const int pp = 8 * (lw + 4 * k) + (lane >> 3);
+      const int pp = 8 * (lw + NL * k) + (lane >> 3);
       pq4[k] = 4u * (unsigned)((lane & 7) ^ (((pp % PW) >> 1) & 7));
       ppix0[k] = MT ? 0u : patch_pix(tile0, pp);
     }
@@ -362,11 +374,11 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
       char* base = smem + C::LDS_B + pslot(kt, c) * (PI * 1024);
 #pragma unroll
       for (int k = 0; k < PK; ++k) {
-        if (lw + 4 * k < PI) {
-          const unsigned pix = MT ? patch_pix(t, 8 * (lw + 4 * k) + (lane >> 3)) : ppix0[k];
+        if (lw + NL * k < PI) {
+          const unsigned pix = MT ? patch_pix(t, 8 * (lw + NL * k) + (lane >> 3)) : ppix0[k];
           const unsigned ch = cb + pq4[k];
           const unsigned voff = (pix != OFF_INVALID && ch < lim) ? (pix * ld + ch) * 4u : OFF_INVALID;
-          dma16(s0 ? rs0 : rs1, base + (lw + 4 * k) * 1024, voff, 0);
+          dma16(s0 ? rs0 : rs1, base + (lw + NL * k) * 1024, voff, 0);
         }
       }
     };
@@ -395,23 +407,23 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
     };
     if constexpr (LSPLIT) {
       // 8-channel patch task t = (patch pixel t/4, channel group t%4), NT = 4*NPIX;
-      // this wave's tasks t = 64*lw + lane + 256*i.  A chunk's patch is loaded in
+      // this wave's tasks t = 64*lw + lane + 64*NL*i.  A chunk's patch is loaded in
       // the super-step that issues its load set and split + stored in the next one
       // (still a super-step before its first read; its slot was free already).
-      constexpr int NT = 4 * NPIX, TI = (NT + 255) / 256;
+      constexpr int NT = 4 * NPIX, TI = (NT + 64 * NL - 1) / (64 * NL);
       const unsigned tg8 = 8u * (unsigned)(lane & 3);  // channel offset 8g within the chunk (g = t & 3 = lane & 3)
       int tlds[TI];        // byte offset of the task's hi quad in a patch slot (lo: ^ 64), -1 past NT
       unsigned tpix0[TI];  // !MT: the task's input pixel in the one tile (patch_pix)
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
-        const int t = 64 * lw + lane + 256 * i;
+        const int t = 64 * lw + lane + 64 * NL * i;
         const int pp = t >> 2, g = t & 3;
         const int px = pp % PW;
         tlds[i] = t < NT ? pp * 128 + ((g ^ ((px >> 1) & 7)) << 4) : -1;
         tpix0[i] = MT ? 0u : patch_pix(tile0, pp);
       }
       auto task_pix = [&](const Tile& tt, int i) {
-        return MT ? patch_pix(tt, (64 * lw + lane + 256 * i) >> 2) : tpix0[i];
+        return MT ? patch_pix(tt, (64 * lw + lane + 64 * NL * i) >> 2) : tpix0[i];
       };
       using Staged = f32x4[TI][2];
       auto load_patch = [&](int kt, int c, Staged& dst) {  // chunks past the end load zeros
@@ -562,7 +574,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
 #undef LSTAMP
 #ifdef STAMPS
       {  // per loader wave: patch split + store, patch load issue, weight DMA issue, vmcnt wait, barrier, loop total
-        const unsigned lid = blockIdx.x * 4 + lw;
+        const unsigned lid = blockIdx.x * NL + lw;
         if (lane == 0 && lid < 16384) {
           unsigned long long* g = g_lstamp + lid * 8;
           g[0] = l_st;
@@ -820,9 +832,19 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
   // nkp) run on zero weights and zero patches: they add exact zeros, and the
   // loop body has no branches.  A tile's last super-step reads nothing ahead
   // (the next tile's first fragments are read after its epilogue).
+  if constexpr (NL == 8) {  // (each compute wave also issues the prologue pieces of loader lw + 4)
+    const WPieces wp1 = wpieces(lw + 4);
 #pragma unroll
-  for (int u = 0; u < DW; ++u) issue_weights(u);
-  wait_vm<NWP * (DW - 2)>();      // the weights of sets 0 and 1 (sets 2 .. D-1: before the first loop barrier)
+    for (int u = 0; u < DW; ++u) {
+      issue_weights(u);
+      issue_weights_q(u, wp1);
+    }
+    wait_vm<2 * NWP * (DW - 2)>();  // the weights of sets 0 and 1
+  } else {
+#pragma unroll
+    for (int u = 0; u < DW; ++u) issue_weights(u);
+    wait_vm<NWP * (DW - 2)>();
+  }      // the weights of sets 0 and 1 (sets 2 .. D-1: before the first loop barrier)
   __builtin_amdgcn_s_barrier();  // load sets 0 and 1 have landed
 #ifdef HALO_PRIO
   __builtin_amdgcn_s_setprio(HALO_PRIO);
@@ -938,8 +960,8 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
 // One conv (or an independent pair, raft_conv2d_pair) per launch: work-group g runs tiles
 // N-tile g % gn of spatial tiles (g / gn) * m .. + m-1 of its conv (the pair's first grid0
 // work-groups take a[0]'s tiles).
-template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH, bool MT = false>
-__global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
+template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH, bool MT = false, int NL = 4>
+__global__ __launch_bounds__(64 * (4 + NL)) void conv_halo_kernel(HaloLaunch hl) {
   using C = HaloCfg<KH, KW, BNT, PREC == RAFT_PREC_F16X3 ? 128 : 64, TH>;
   constexpr int NORM_BYTES = halo_norm_bytes<KH, KW, BNT, PREC, ENC>(C::LDS_B, C::LDS_A, C::D);
   __shared__ __attribute__((aligned(1024))) char smem[C::LDS_B + C::LDS_A + NORM_BYTES];
@@ -952,20 +974,40 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(HaloLaunch hl) {
     const int ntl = min(hl.m, (prob ? hl.sp1 : hl.sp0) - st0);
     halo_body<KH, KW, BNT, PREC, ENC, TH, true>(hl.a, prob, g % gn, st0, ntl, smem);
   } else {  // (hl.m == 1)
-    halo_body<KH, KW, BNT, PREC, ENC, TH, false>(hl.a, prob, g % gn, g / gn, 1, smem);
+    halo_body<KH, KW, BNT, PREC, ENC, TH, false, NL>(hl.a, prob, g % gn, g / gn, 1, smem);
   }
 }
 
 // the kernel of a launch: the multi-tile body where the plan runs several tiles per work-group
 // (l.m > 1), else the one-tile body.  (The one-product 3x3 wide tiles never run several:
 // halo_mt_ok.)
+// the one-tile f16x3 update convs' loader waves: 4 or 8 (RAFT_HALO_NL8=1; raft_conv2d_set_halo_loaders)
+std::atomic<int> g_halo_nl{0};  // 0: from the environment
+bool halo_nl8() {
+  int v = g_halo_nl.load(std::memory_order_relaxed);
+  if (v == 0) {
+    const char* e = getenv("RAFT_HALO_NL8");
+    v = e && e[0] == '1' ? 8 : 4;
+    g_halo_nl.store(v, std::memory_order_relaxed);
+  }
+  return v == 8;
+}
 template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH>
 void launch_halo_mt(const HaloLaunch& l, dim3 grid, hipStream_t s) {
   constexpr bool NO_MT = PREC != RAFT_PREC_F16X3 && KH * KW == 9 && BNT == 128;
-  if (!NO_MT && l.m > 1)
+  // the 8-loader form: one-tile f16x3 update-block convs (RAFT_HALO_NL8=1)
+  constexpr bool CAN_NL8 = PREC == RAFT_PREC_F16X3 && !ENC && TH == HTH && BNT <= 64 && KH * KW > 1;
+  if (!NO_MT && l.m > 1) {
     hipLaunchKernelGGL((conv_halo_kernel<KH, KW, BNT, PREC, ENC, TH, !NO_MT>), grid, dim3(512), 0, s, l);
-  else
+  } else {
+    if constexpr (CAN_NL8) {
+      if (halo_nl8()) {
+        hipLaunchKernelGGL((conv_halo_kernel<KH, KW, BNT, PREC, ENC, TH, false, 8>), grid, dim3(768), 0, s, l);
+        return;
+      }
+    }
     hipLaunchKernelGGL((conv_halo_kernel<KH, KW, BNT, PREC, ENC, TH, false>), grid, dim3(512), 0, s, l);
+  }
 }
 
 template <int KH, int KW, int PREC>
@@ -1261,6 +1303,13 @@ extern "C" int raft_debug_lstamps(unsigned long long* host, int n, int clear) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_lstamp), sizeof(unsigned long long) * (size_t)n);
 }
 #endif
+
+// the loader-wave count of the one-tile f16x3 update-block convs (4 or 8); returns the previous
+extern "C" int raft_conv2d_set_halo_loaders(int nl) {
+  const int prev = halo_nl8() ? 8 : 4;
+  if (nl == 4 || nl == 8) g_halo_nl.store(nl, std::memory_order_relaxed);
+  return prev;
+}
 
 // whether the conv takes its input InstanceNorm in the loaders (raft_conv2d_params.in_norm): the
 // 3x3 convs' split-patch path (D = 3 for both N-tile widths), <= 256 input channels

@@ -475,7 +475,7 @@ __global__ __launch_bounds__(64 * MERGE2_WAVES) void instnorm_merge2_kernel(cons
 // comes last runs level 2 over the G group sums (sc1 loads, after its add returned / a block barrier:
 // MI355X_MICROARCH.md's last-arriver hand-off) in exactly merge2's order, so the statistics equal
 // raft_instnorm_merge_ws's bit for bit; it then clears the counter for the next launch.
-__global__ __launch_bounds__(256) void instnorm_merge_fused_kernel(const float* part, int slots, int C, int ld,
+__global__ __launch_bounds__(64 * MERGE2_WAVES) void instnorm_merge_fused_kernel(const float* part, int slots, int C, int ld,
                                                                    double* ws, int G, float eps, float* stats,
                                                                    int* counters) {
   __shared__ double red[MERGE2_WAVES][3][64];  // (level 1 uses rows 0-3)
@@ -485,7 +485,9 @@ __global__ __launch_bounds__(256) void instnorm_merge_fused_kernel(const float* 
   const bool cok = c < C;
   const float* pb = part + ((long)b * slots * ld + (cok ? c : 0)) * 4;
   const float K = cok ? pb[1] : 0.f;  // slot 0's mean (slot 0 always holds pixels)
-  {
+  // (1024 threads: waves 0-3 run level 1 exactly as instnorm_merge1_kernel, all 16 waves level 2
+  // exactly as instnorm_merge2_kernel, so the last block's tail is as parallel as that launch)
+  if (w < 4) {
     f32x4 v[MERGE_SPG / 4];
 #pragma unroll
     for (int i = 0; i < MERGE_SPG / 4; ++i) {
@@ -520,10 +522,10 @@ __global__ __launch_bounds__(256) void instnorm_merge_fused_kernel(const float* 
   }
   __syncthreads();
   if (!is_last) return;
-  // level 2 (merge2's order: its wave k sums groups k, k + 16, ... in batches of 8; wave w here runs
-  // merge2's waves w, w + 4, w + 8, w + 12)
+  // level 2 (merge2's order: wave k sums groups k, k + 16, ... in batches of 8)
   const unsigned long long* p = reinterpret_cast<const unsigned long long*>(ws + ((long)b * G * C + (cok ? c : 0)) * 3);
-  for (int kk = w; kk < MERGE2_WAVES; kk += 4) {
+  {
+    const int kk = w;
     double n = 0.0, s1 = 0.0, s2 = 0.0;
     for (int g0 = kk; g0 < G; g0 += 8 * MERGE2_WAVES) {
       double t[8][3];
@@ -793,7 +795,7 @@ extern "C" int raft_instnorm_merge_fused(const float* part, int slots_per_image,
                "raft_instnorm_merge_fused: part 16-B, ws 8-B, counters 4-B aligned");
   const int G = cdiv(slots_per_image, MERGE_SPG);
   RAFT_REQUIRE(G < 65536, "raft_instnorm_merge_fused: too many slots");
-  hipLaunchKernelGGL(instnorm_merge_fused_kernel, dim3(cdiv(C, 64), B, G), dim3(256), 0, as_stream(stream), part,
+  hipLaunchKernelGGL(instnorm_merge_fused_kernel, dim3(cdiv(C, 64), B, G), dim3(64 * MERGE2_WAVES), 0, as_stream(stream), part,
                      slots_per_image, C, stats_ld, reinterpret_cast<double*>(ws), G, eps, stats, counters);
   return check_launch("raft_instnorm_merge_fused");
 }
