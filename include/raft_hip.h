@@ -396,7 +396,7 @@ int raft_conv2d(const raft_conv2d_params* p, raft_stream_t stream);
 int raft_conv2d_pair(const raft_conv2d_params* p0, const raft_conv2d_params* p1, raft_stream_t stream);
 /* Loader waves of the halo kernel's one-tile f16x3 3x3 / 1x5 / 5x1 convs (the update block at one frame
  * pair): 4 (a 512-thread work-group) or 8 (768 threads: each loader issues half the weight DMAs
- * and stages half of each patch); the same results bit for bit.  Default from RAFT_HALO_NL8 (=1: 8).
+ * and stages half of each patch); the same results bit for bit.  Default 8 (RAFT_HALO_NL8=0: 4).
  * Returns the previous count; other values only query.  Process-wide; plans capture launches, so
  * set it before building / capturing a plan. */
 int raft_conv2d_set_halo_loaders(int nl);

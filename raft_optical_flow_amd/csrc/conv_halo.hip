@@ -981,13 +981,14 @@ __global__ __launch_bounds__(64 * (4 + NL)) void conv_halo_kernel(HaloLaunch hl)
 // the kernel of a launch: the multi-tile body where the plan runs several tiles per work-group
 // (l.m > 1), else the one-tile body.  (The one-product 3x3 wide tiles never run several:
 // halo_mt_ok.)
-// the one-tile f16x3 update convs' loader waves: 4 or 8 (RAFT_HALO_NL8=1; raft_conv2d_set_halo_loaders)
+// the one-tile f16x3 update convs' loader waves: 8, or 4 (RAFT_HALO_NL8=0; raft_conv2d_set_halo_loaders)
 std::atomic<int> g_halo_nl{0};  // 0: from the environment
 bool halo_nl8() {
   int v = g_halo_nl.load(std::memory_order_relaxed);
   if (v == 0) {
+    // (default 8: config 2 +1.0-1.4 % in three interleaved pairs on one box, profiles/r05e_experiments.txt)
     const char* e = getenv("RAFT_HALO_NL8");
-    v = e && e[0] == '1' ? 8 : 4;
+    v = e && e[0] == '0' ? 4 : 8;
     g_halo_nl.store(v, std::memory_order_relaxed);
   }
   return v == 8;
@@ -995,7 +996,7 @@ bool halo_nl8() {
 template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH>
 void launch_halo_mt(const HaloLaunch& l, dim3 grid, hipStream_t s) {
   constexpr bool NO_MT = PREC != RAFT_PREC_F16X3 && KH * KW == 9 && BNT == 128;
-  // the 8-loader form: one-tile f16x3 update-block convs (RAFT_HALO_NL8=1)
+  // the 8-loader form: one-tile f16x3 update-block convs (default; RAFT_HALO_NL8=0: 4 loaders)
   constexpr bool CAN_NL8 = PREC == RAFT_PREC_F16X3 && !ENC && TH == HTH && BNT <= 64 && KH * KW > 1;
   if (!NO_MT && l.m > 1) {
     hipLaunchKernelGGL((conv_halo_kernel<KH, KW, BNT, PREC, ENC, TH, !NO_MT>), grid, dim3(512), 0, s, l);
