@@ -147,6 +147,9 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
 #ifndef LC_TAPS2
 #define LC_TAPS2 1
 #endif
+#ifndef LC_A1EARLY
+#define LC_A1EARLY 1
+#endif
   constexpr int PF = LC_PF;
   h8 wb[PF + 1][NT];
   auto load_w = [&](int j, h8 (&dst)[NT]) {
@@ -277,6 +280,29 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
     fl[fi] = fv;
   }
   LC_STAMP(2);
+#if LC_A1EARLY
+  // convf1's A operand before the taps, while the window tiles are still in flight
+  __syncthreads();  // the flow patch is visible
+  // convf1's im2col A operand: row mm, K = 2 (dy*7 + dx) + ci (the GATHER packing), 8 K per thread
+  {
+    const int mm = threadIdx.x >> 4, q = threadIdx.x & 15;
+    const int py = mm >> 4, px = mm & 15;
+    float e[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int k = 8 * q + i, t = k >> 1;
+      const int dy = t / LC_F1K, dx = t - dy * LC_F1K;
+      const float2 fv = fl[(py + (k < 2 * LC_F1KK ? dy : 0)) * LC_FPW + px + (k < 2 * LC_F1KK ? dx : 0)];
+      e[i] = k < 2 * LC_F1KK ? ((k & 1) ? fv.y : fv.x) : 0.f;
+    }
+    h8 hi, lo;
+    split8<X3, BF>(f32x4{e[0], e[1], e[2], e[3]}, f32x4{e[4], e[5], e[6], e[7]}, hi, lo);
+    const int j = q >> 2, qd = q & 3, sw = (mm >> 1) & 7;
+    char* row = smem + LC_OFF_A1 + j * (LC_M * 128) + mm * 128;
+    *reinterpret_cast<h8*>(row + ((qd ^ sw) << 4)) = hi;
+    if constexpr (X3) *reinterpret_cast<h8*>(row + (((4 + qd) ^ sw) << 4)) = lo;
+  }
+#endif
 
   // ---- 3. the taps of each pixel -> split rows of convc1's A operand ------------------------
   // (default: the first PF K-steps of the weight stream are issued here, behind the tiles, so they
@@ -443,6 +469,9 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
   }
   if (a.range_flag && big) *a.range_flag = 1;
   LC_STAMP(3);
+#if LC_A1EARLY
+  __syncthreads();  // every A row is in LDS
+#else
   __syncthreads();  // the flow patch is visible
   // convf1's im2col A operand: row mm, K = 2 (dy*7 + dx) + ci (the GATHER packing), 8 K per thread
   {
@@ -464,6 +493,7 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
     if constexpr (X3) *reinterpret_cast<h8*>(row + (((4 + qd) ^ sw) << 4)) = lo;
   }
   __syncthreads();  // every A row is in LDS
+#endif
   LC_STAMP(4);
 
   // ---- 4. convc1 (all waves, 32 outputs each) then convf1 (waves 0-3) on MFMA: one K stream ----
