@@ -972,7 +972,7 @@ __global__ __launch_bounds__(64 * (4 + NL)) void conv_halo_kernel(HaloLaunch hl)
   if constexpr (MT) {
     const int st0 = (g / gn) * hl.m;
     const int ntl = min(hl.m, (prob ? hl.sp1 : hl.sp0) - st0);
-    halo_body<KH, KW, BNT, PREC, ENC, TH, true>(hl.a, prob, g % gn, st0, ntl, smem);
+    halo_body<KH, KW, BNT, PREC, ENC, TH, true, NL>(hl.a, prob, g % gn, st0, ntl, smem);
   } else {  // (hl.m == 1)
     halo_body<KH, KW, BNT, PREC, ENC, TH, false, NL>(hl.a, prob, g % gn, g / gn, 1, smem);
   }
@@ -993,11 +993,30 @@ bool halo_nl8() {
   }
   return v == 8;
 }
+bool halo_nl8_enc() {
+  static const bool v = [] {
+    const char* e = getenv("RAFT_HALO_NL8_ENC");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
 template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH>
 void launch_halo_mt(const HaloLaunch& l, dim3 grid, hipStream_t s) {
   constexpr bool NO_MT = PREC != RAFT_PREC_F16X3 && KH * KW == 9 && BNT == 128;
   // the 8-loader form: one-tile f16x3 update-block convs (default; RAFT_HALO_NL8=0: 4 loaders)
   constexpr bool CAN_NL8 = PREC == RAFT_PREC_F16X3 && !ENC && TH == HTH && BNT <= 64 && KH * KW > 1;
+  // and for the encoders' f16x3 3x3 convs on 128-pixel tiles (RAFT_HALO_NL8_ENC=1): their loaders also
+  // apply the input InstanceNorm
+  constexpr bool CAN_NL8E = PREC == RAFT_PREC_F16X3 && ENC && TH == HTH && BNT <= 64 && KH * KW == 9;
+  if constexpr (CAN_NL8E) {
+    if (halo_nl8_enc()) {
+      if (l.m > 1)
+        hipLaunchKernelGGL((conv_halo_kernel<KH, KW, BNT, PREC, ENC, TH, true, 8>), grid, dim3(768), 0, s, l);
+      else
+        hipLaunchKernelGGL((conv_halo_kernel<KH, KW, BNT, PREC, ENC, TH, false, 8>), grid, dim3(768), 0, s, l);
+      return;
+    }
+  }
   if (!NO_MT && l.m > 1) {
     hipLaunchKernelGGL((conv_halo_kernel<KH, KW, BNT, PREC, ENC, TH, !NO_MT>), grid, dim3(512), 0, s, l);
   } else {
