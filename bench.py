@@ -591,8 +591,12 @@ def main():
                     "timing": "HIP events around a hipGraph of 50 replays of those launches"}
         hpmc, hname = load_pmc("halo_pmc.json", "conv_halo.hip")
         if hpmc:
-            dominant["mfma_busy"] = (hpmc.get("conv_halo_kernel<3, 3, 64, 1, false, 8>")
-                                     or hpmc.get("conv_halo_kernel<3, 3, 64, 1, false>") or {}).get("mfma_busy")
+            # the one-tile f16x3 3x3 N-64 instantiation, whatever its trailing template arguments (tile
+            # rows, multi-tile flag, loader waves): the entry with the most dispatches
+            keys = [k for k in hpmc if k.startswith("conv_halo_kernel<3, 3, 64, 1, false, 8")
+                    or k == "conv_halo_kernel<3, 3, 64, 1, false>"]
+            ent = max((hpmc[k] for k in keys), key=lambda e: e.get("dispatches", 0), default={})
+            dominant["mfma_busy"] = ent.get("mfma_busy")
             dominant["mfma_busy_source"] = f"profiles/{hname}"
 
     # the drop-in path itself: RAFT.forward() as demo.py / evaluate.py call it (core/raft.py:145-251;

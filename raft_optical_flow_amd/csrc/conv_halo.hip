@@ -995,8 +995,9 @@ bool halo_nl8() {
 }
 bool halo_nl8_enc() {
   static const bool v = [] {
+    // (default on: config 2 +0.1 / +0.3 % in two interleaved pairs on one box, profiles/r05f_experiments.txt)
     const char* e = getenv("RAFT_HALO_NL8_ENC");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return v;
 }
@@ -1005,7 +1006,7 @@ void launch_halo_mt(const HaloLaunch& l, dim3 grid, hipStream_t s) {
   constexpr bool NO_MT = PREC != RAFT_PREC_F16X3 && KH * KW == 9 && BNT == 128;
   // the 8-loader form: one-tile f16x3 update-block convs (default; RAFT_HALO_NL8=0: 4 loaders)
   constexpr bool CAN_NL8 = PREC == RAFT_PREC_F16X3 && !ENC && TH == HTH && BNT <= 64 && KH * KW > 1;
-  // and for the encoders' f16x3 3x3 convs on 128-pixel tiles (RAFT_HALO_NL8_ENC=1): their loaders also
+  // and for the encoders' f16x3 3x3 convs on 128-pixel tiles (default; RAFT_HALO_NL8_ENC=0: 4): their loaders also
   // apply the input InstanceNorm
   constexpr bool CAN_NL8E = PREC == RAFT_PREC_F16X3 && ENC && TH == HTH && BNT <= 64 && KH * KW == 9;
   if constexpr (CAN_NL8E) {

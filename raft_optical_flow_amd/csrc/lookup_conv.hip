@@ -148,7 +148,7 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
 #define LC_TAPS2 1
 #endif
 #ifndef LC_A1EARLY
-#define LC_A1EARLY 1
+#define LC_A1EARLY 0
 #endif
   constexpr int PF = LC_PF;
   h8 wb[PF + 1][NT];
@@ -204,6 +204,10 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
       px_y[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cy), k));
     }
   }
+#ifdef LC_STAMPS
+  asm volatile("" ::"v"(px_x[0]), "v"(px_y[LC_PX - 1]));
+  LC_STAMP(7);  // the coords have arrived
+#endif
   // the small loads the waits below need before the tiles (loads return in order):
   // this lane's level constants, the coords of convf1's 8x22 flow patch (threads 0 .. 175), the biases
   const bool col = lane < LC_L * RD;
@@ -584,6 +588,7 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
     gs[0] = lc_r0;
     gs[1] = lc_r1;
     for (int k = 0; k < 7; ++k) gs[2 + k] = lc_t[k];
+    gs[9] = lc_t[7];
   }
 #endif
 }

@@ -46,5 +46,8 @@ d = np.diff(t, axis=1)
 for k, n in enumerate(names):
     print(f"  {n:26s} mean {d[:, k].mean():8.0f} cyc  max {d[:, k].max():8.0f}")
 print(f"  total per wave mean {(t[:, 6] - t[:, 0]).mean():.0f} cycles")
+c7 = s[:, 9]
+if (c7 > 0).all():
+    print(f"  (issue loads = coords round trip {(c7 - t[:, 0]).mean():.0f} + tile issue {(t[:, 1] - c7).mean():.0f} cyc)")
 print(f"  launch span (realtime 100 MHz): {(r1.max() - r0.min()) / 100:.2f} us; wave mean {(r1 - r0).mean() / 100:.2f} us;"
       f" start spread {(r0.max() - r0.min()) / 100:.2f} us")

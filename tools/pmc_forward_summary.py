@@ -21,7 +21,7 @@ import sys
 base = sys.argv[1]
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-RND = os.environ.get("PMC_ROUND", "r04")  # <out>/<round>_*_pmc.json
+RND = os.environ.get("PMC_ROUND", "r05")  # <out>/<round>_*_pmc.json
 OUTD = os.environ.get("PMC_OUT", os.path.join(ROOT, "profiles"))  # (on a GPU box: gpurun_out, then copy)
 
 
