@@ -228,6 +228,50 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
 
   __builtin_amdgcn_sched_barrier(0);
   f32x4 v[LC_PX][LC_L];
+  // Every level's maps within 2^31 bytes (uniform): one buffer resource per level and 32-bit byte
+  // offsets, the window test per lane on the VALU.  Per (pixel, level) the scalar unit then computes
+  // only the window origin and one product (~12 SALU instead of ~46 with a 64-bit base and a resource
+  // per window: the scalar unit, shared by the CU's 8 waves, was the tile-issue phase's limit).
+#ifndef LC_OFF32
+#define LC_OFF32 1
+#endif
+  bool off32 = LC_OFF32 != 0;
+  const unsigned nmaps = (unsigned)(a.B * P);
+#pragma unroll
+  for (int l = 0; l < LC_L; ++l) off32 &= (unsigned long long)nmaps * lmsz[l] * 4ull < 0x7FFFFFF0ull;
+  if (off32) {
+    __amdgpu_buffer_rsrc_t rsl[LC_L];
+    unsigned lano[LC_L], lmsz4[LC_L];  // the lane's byte offset in a window at its origin; map bytes
+#pragma unroll
+    for (int l = 0; l < LC_L; ++l) {
+      rsl[l] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(lbs[l]), (short)0, (int)(nmaps * lmsz[l] * 4u),
+                                                 0x00020000);
+      lano[l] = __umul24((unsigned)ti, (unsigned)(64 * ltw[l])) + 16u * (unsigned)(lane & 15);
+      lmsz4[l] = lmsz[l] * 4u;
+    }
+#pragma unroll
+    for (int k = 0; k < LC_PX; ++k) {
+      const unsigned gp = (unsigned)px_gp[k];
+      const int xf = __builtin_amdgcn_readfirstlane((int)floorf(px_x[k]));
+      const int yf = __builtin_amdgcn_readfirstlane((int)floorf(px_y[k]));
+#pragma unroll
+      for (int l = 0; l < LC_L; ++l) {
+        const int wx0 = (xf >> l) - R, wy0 = (yf >> l) - R;
+        const int tyo = wy0 >> 2, txo = wx0 >> 2;
+        const int ntx = ((wx0 + WD - 1) >> 2) - txo + 1;
+        // map row / tile column this lane reads; inside the window and the map, or no access (tests
+        // combined bitwise and the offset selected: no branch around the load)
+        const int rowm = 4 * tyo + lrow, colt = txo + tj;
+        const bool tok = px_ok[k] & ((unsigned)(rowm - wy0) < (unsigned)WD) & ((unsigned)rowm < (unsigned)(4 * lth[l])) &
+                         ((unsigned)tj < (unsigned)ntx) & ((unsigned)colt < (unsigned)ltw[l]);
+        const unsigned sb = gp * lmsz4[l] + (unsigned)(tyo * ltw[l] + txo) * 64u;
+        unsigned offv = sb + lano[l];
+        asm volatile("" : "+v"(offv));  // (computed for every lane: a select, not a branch around it)
+        const unsigned off = tok ? offv : 0x80000000u;
+        v[k][l] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsl[l], off, 0, 0));
+      }
+    }
+  } else {
 #pragma unroll
   for (int k = 0; k < LC_PX; ++k) {
     const bool ok = px_ok[k];
@@ -252,6 +296,7 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
                                : 0x80000000u;
       v[k][l] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
     }
+  }
   }
   LC_STAMP(1);
   // ---- 2. while the tiles fly: the per-axis sampling entries of the four pixels ------------
