@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define RAFT_HIP_ABI_VERSION 18
+#define RAFT_HIP_ABI_VERSION 17
 
 /* Negative return codes (argument errors, raised before any launch). */
 #define RAFT_E_INVALID (-1)   /* bad size / null pointer / unsupported shape */
@@ -167,12 +167,6 @@ int raft_corr_lookup_conv(const float* pyramid, int B, int H, int W, int num_lev
                           const void* c1_weight, const float* c1_bias, int c1_n, float* c1_out, int c1_out_ld,
                           int* c1_range_flag, const void* f1_weight, const float* f1_bias, int f1_n, int f1_k,
                           float* f1_out, int f1_out_ld, int* f1_range_flag, raft_stream_t stream);
-/* Launches with more 2x16-pixel tiles than the device has CUs run persistent work-groups (one per
- * CU, each walking tiles with the next tile's coords and window loads in flight under the current
- * tile's taps and convs); on = 1 (default; RAFT_LC_PERSIST=0 starts it off) or 0 (one tile per
- * work-group): the same results bit for bit.  Returns the previous setting; other values only
- * query.  Process-wide; set it before building / capturing a plan. */
-int raft_corr_lookup_conv_set_persistent(int on);
 /* convc1's split weight [n_pad][k_pad] (k_pad % 32 == 0) -> raft_corr_lookup_conv's fragment order:
  * [k_pad/32][n/32][4][64] x 16 B, element (j, s, t, lane) = 8 halves of split row 32s + lane%32,
  * K-step j, quad (t/2)*4 + 2*(lane/32) + t%2; out holds raft_lookup_conv_weight_floats(n, k_pad)

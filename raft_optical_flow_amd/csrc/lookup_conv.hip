@@ -27,9 +27,6 @@
 // Arithmetic: the taps are the lookup kernel's; convc1 and convf1 run in the conv precision
 // (f16x3: hi*hi + lo*hi + hi*(2048 lo)/2048, fp32 accumulation, the halo kernel's split;
 // f16 / bf16: one product), as every other conv of the update block.
-#include <atomic>
-#include <cstdlib>
-
 #include "lookup_common.hpp"
 
 namespace raft {
@@ -70,7 +67,6 @@ struct LookupConvArgs {
   int f1out_ld;
   int* f1flag;
   int tx_n, ty_n;       // pixel tiles per image row / column
-  int ntiles;           // B * tx_n * ty_n
   int span_slot;        // raft_debug_launch_span: this launch's slot of g_lc_span, or -1
 };
 
@@ -118,10 +114,7 @@ __device__ __forceinline__ unsigned long long lc_real() {
 #define LC_STAMP(k)
 #endif
 
-// PERS (several rounds of tiles): one work-group per CU walks tiles blockIdx.x, + gridDim.x, ...; the
-// next tile's coords are loaded under this tile's taps and its window tiles issued before this tile's
-// convs, so both round trips land under the GEMMs and the epilogue instead of at a work-group's start.
-template <int PREC, bool PERS>
+template <int PREC>
 __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
 #ifdef LC_STAMPS
   unsigned long long lc_t[10];
@@ -136,28 +129,26 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
   const LookupArgs& a = g.a;
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int tile = PERS ? (int)blockIdx.x : xcd_tile(blockIdx.x, gridDim.x);
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
   if (g.span_slot >= 0 && threadIdx.x == 0)
     atomicMin(&g_lc_span[2 * g.span_slot], (unsigned long long)__builtin_amdgcn_s_memrealtime());
   const int per = g.tx_n * g.ty_n;
+  const int b = tile / per, sr = tile - b * per;
+  const int y0 = (sr / g.tx_n) * LC_TH, x0 = (sr % g.tx_n) * LC_TW;
   const int H = a.H, W = a.W, P = H * W;
-  auto geom = [&](int t, int& bb, int& yy0, int& xx0) {
-    bb = t / per;
-    const int sr = t - bb * per;
-    yy0 = (sr / g.tx_n) * LC_TH;
-    xx0 = (sr % g.tx_n) * LC_TW;
-  };
-  int b, y0, x0;
-  geom(tile, b, y0, x0);
 
   // The K stream of step 4, in registers: convc1's 11 K-steps (all waves) then convf1's 4 (waves
-  // 0-3), prefetched PF steps ahead; the first PF steps are issued behind the window tiles, so that
-  // they land during the taps.
+  // 0-3), prefetched PF steps ahead.  LC_EARLY: the first PF steps are issued here, before the coords
+  // load, so that the weight bytes (the whole 360 KB split convc1 weight per work-group) stream in
+  // under the coords / window-tile round trips and the taps instead of after them.
 #ifndef LC_PF
 #define LC_PF 3
 #endif
 #ifndef LC_TAPS2
 #define LC_TAPS2 1
+#endif
+#ifndef LC_A1EARLY
+#define LC_A1EARLY 0
 #endif
   constexpr int PF = LC_PF;
   h8 wb[PF + 1][NT];
@@ -169,7 +160,8 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
   };
 
   // ---- 1. the window tiles of this wave's four query pixels (the critical path) --------------
-  const int ti = lane >> 4, tj = (lane >> 2) & 3, lrow = ti * 4 + (lane & 3);
+  const int ti = lane >> 4, tj = (lane >> 2) & 3, rr = lane & 3;
+  const int lrow = ti * 4 + rr;
   // per-level map geometry in registers up front (re-read from the kernel arguments inside the
   // pixel loop, each read is a scalar-cache round trip)
   int lth[LC_L], ltw[LC_L];
@@ -185,66 +177,62 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
   float px_x[LC_PX], px_y[LC_PX];
   int px_gp[LC_PX];
   bool px_ok[LC_PX];
-  auto set_px = [&](int bb, int yy0, int xx0) {
+  // the four pixels' coords, every load issued before the first is used (uniform: scalar loads)
 #pragma unroll
-    for (int k = 0; k < LC_PX; ++k) {
-      const int mk = LC_PX * wv + k;
-      const int yy = yy0 + (mk >> 4), xx = xx0 + (mk & 15);
-      const bool ok = yy < H && xx < W;
-      px_ok[k] = ok;
-      px_gp[k] = ok ? bb * P + yy * W + xx : bb * P;
-    }
-  };
-  // a tile's coords loads, issued ahead of their use: lane k < 4 of each quad loads pixel k's x and y
-  // (two 4-B loads), threads 0 .. 175 the coords of convf1's 8x22 flow patch (out-of-image threads
-  // pass an out-of-range offset: zeros, no access, no branch around the load)
-  const int fi = threadIdx.x;
-  const __amdgpu_buffer_rsrc_t crs =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.coords), (short)0, (int)((unsigned)(a.B * P) * 8u), 0x00020000);
-  float cx, cy;
-  f32x2 fc;
-  int fyy, fxx;
-  bool fin;
-  auto issue_coords = [&](int bb, int yy0, int xx0) {
-    const int mk = LC_PX * wv + (lane & 3);
-    const int yy = yy0 + (mk >> 4), xx = xx0 + (mk & 15);
-    const int gk = (yy < H && xx < W) ? bb * P + yy * W + xx : bb * P;
-    cx = a.coords[2L * gk];
-    cy = a.coords[2L * gk + 1];
-    fyy = yy0 - 3 + fi / LC_FPW;
-    fxx = xx0 - 3 + fi % LC_FPW;
-    fin = fi < LC_FPH * LC_FPW && (unsigned)fyy < (unsigned)H && (unsigned)fxx < (unsigned)W;
-    const unsigned fo = fin ? (unsigned)(bb * P + fyy * W + fxx) * 8u : 0x80000000u;
-    fc = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(crs, fo, 0, 0));
-  };
-  auto resolve_coords = [&]() {
+  for (int k = 0; k < LC_PX; ++k) {
+    const int mk = LC_PX * wv + k;
+    const int yy = y0 + (mk >> 4), xx = x0 + (mk & 15);
+    const bool ok = yy < H && xx < W;
+    px_ok[k] = ok;
+    px_gp[k] = ok ? b * P + yy * W + xx : b * P;
+  }
+  {
+    // one round trip: lane k < 4 loads pixel k's x and y (two 4-B loads), then lane reads
+    int gk = px_gp[0];
+#pragma unroll
+    for (int k = 1; k < LC_PX; ++k) gk = (lane & 3) == k ? px_gp[k] : gk;
+    const float cx = a.coords[2L * gk], cy = a.coords[2L * gk + 1];
+#ifdef LC_EARLY  // (behind the coords load: its wait leaves the weight loads in flight)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < PF; ++j) load_w(j, wb[j]);
+    __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
     for (int k = 0; k < LC_PX; ++k) {
       px_x[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cx), k));
       px_y[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cy), k));
     }
-  };
-  issue_coords(b, y0, x0);
-  // the small loads the waits below need before the tiles (loads return in order):
-  // this lane's level constants, the biases
-  f32x4 prm;
-  {
-    int lq = 0;
-#pragma unroll
-    for (int k = 1; k < LC_L; ++k) lq += lane >= k * RD ? 1 : 0;
-    prm = a.prm[lane < LC_L * RD ? lq : 0];  // this lane's level constants
   }
-  const float c1b = g.bias ? g.bias[32 * wv + (lane & 31)] : 0.f;
-  const float f1b = (wv < 4 && g.f1bias) ? g.f1bias[32 * wv + (lane & 31)] : 0.f;
-  set_px(b, y0, x0);
-  resolve_coords();
-  // (their waits here, with the coords': behind the window loads the compiler would wait for all)
-  asm volatile("" ::"v"(prm), "v"(c1b), "v"(f1b));
 #ifdef LC_STAMPS
   asm volatile("" ::"v"(px_x[0]), "v"(px_y[LC_PX - 1]));
   LC_STAMP(7);  // the coords have arrived
 #endif
+  // the small loads the waits below need before the tiles (loads return in order):
+  // this lane's level constants, the coords of convf1's 8x22 flow patch (threads 0 .. 175), the biases
+  const bool col = lane < LC_L * RD;
+  int lq = 0;
+#pragma unroll
+  for (int k = 1; k < LC_L; ++k) lq += lane >= k * RD ? 1 : 0;
+  const int l = col ? lq : 0;
+  const int ix = lane - l * RD;
+  const f32x4 prm = a.prm[l];
+  const int fi = threadIdx.x;
+  const int fyy = y0 - 3 + fi / LC_FPW, fxx = x0 - 3 + fi % LC_FPW;
+  const bool fin = fi < LC_FPH * LC_FPW && (unsigned)fyy < (unsigned)H && (unsigned)fxx < (unsigned)W;
+  f32x2 fc = {0.f, 0.f};
+  if (fin) fc = *reinterpret_cast<const f32x2*>(a.coords + 2L * ((long)b * P + fyy * W + fxx));
+  const int m = lane & 31, h = lane >> 5;
+  const float c1b = g.bias ? g.bias[32 * wv + m] : 0.f;
+  const float f1b = (wv < 4 && g.f1bias) ? g.f1bias[32 * wv + m] : 0.f;
+  // (their waits here, behind the coords' round trip: after the window loads the compiler, which
+  // cannot count the loads of the two window paths below as equal, would wait for all of them)
+#ifndef LC_EARLYWAIT
+#define LC_EARLYWAIT 1
+#endif
+  if constexpr (LC_EARLYWAIT != 0) asm volatile("" ::"v"(prm), "v"(c1b), "v"(f1b), "v"(fc));
 
+  __builtin_amdgcn_sched_barrier(0);
   f32x4 v[LC_PX][LC_L];
   // Every level's maps within 2^31 bytes (uniform): one buffer resource per level and 32-bit byte
   // offsets, the window test per lane on the VALU.  Per (pixel, level) the scalar unit then computes
@@ -257,412 +245,390 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
   const unsigned nmaps = (unsigned)(a.B * P);
 #pragma unroll
   for (int l = 0; l < LC_L; ++l) off32 &= (unsigned long long)nmaps * lmsz[l] * 4ull < 0x7FFFFFF0ull;
-  __amdgpu_buffer_rsrc_t rsl[LC_L];
-  unsigned lano[LC_L], lmsz4[LC_L];  // the lane's byte offset in a window at its origin; map bytes
+  if (off32) {
+    __amdgpu_buffer_rsrc_t rsl[LC_L];
+    unsigned lano[LC_L], lmsz4[LC_L];  // the lane's byte offset in a window at its origin; map bytes
 #pragma unroll
-  for (int l = 0; l < LC_L; ++l) {
-    rsl[l] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(lbs[l]), (short)0, (int)(nmaps * lmsz[l] * 4u),
-                                               0x00020000);
-    lano[l] = __umul24((unsigned)ti, (unsigned)(64 * ltw[l])) + 16u * (unsigned)(lane & 15);
-    lmsz4[l] = lmsz[l] * 4u;
+    for (int l = 0; l < LC_L; ++l) {
+      rsl[l] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(lbs[l]), (short)0, (int)(nmaps * lmsz[l] * 4u),
+                                                 0x00020000);
+      lano[l] = __umul24((unsigned)ti, (unsigned)(64 * ltw[l])) + 16u * (unsigned)(lane & 15);
+      lmsz4[l] = lmsz[l] * 4u;
+    }
+#pragma unroll
+    for (int k = 0; k < LC_PX; ++k) {
+      const unsigned gp = (unsigned)px_gp[k];
+      const int xf = __builtin_amdgcn_readfirstlane((int)floorf(px_x[k]));
+      const int yf = __builtin_amdgcn_readfirstlane((int)floorf(px_y[k]));
+#pragma unroll
+      for (int l = 0; l < LC_L; ++l) {
+        const int wx0 = (xf >> l) - R, wy0 = (yf >> l) - R;
+        const int tyo = wy0 >> 2, txo = wx0 >> 2;
+        const int ntx = ((wx0 + WD - 1) >> 2) - txo + 1;
+        // map row / tile column this lane reads; inside the window and the map, or no access (tests
+        // combined bitwise and the offset selected: no branch around the load)
+        const int rowm = 4 * tyo + lrow, colt = txo + tj;
+        const bool tok = px_ok[k] & ((unsigned)(rowm - wy0) < (unsigned)WD) & ((unsigned)rowm < (unsigned)(4 * lth[l])) &
+                         ((unsigned)tj < (unsigned)ntx) & ((unsigned)colt < (unsigned)ltw[l]);
+        const unsigned sb = gp * lmsz4[l] + (unsigned)(tyo * ltw[l] + txo) * 64u;
+        unsigned offv = sb + lano[l];
+        asm volatile("" : "+v"(offv));  // (computed for every lane: a select, not a branch around it)
+        const unsigned off = tok ? offv : 0x80000000u;
+        v[k][l] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsl[l], off, 0, 0));
+      }
+    }
+  } else {
+#pragma unroll
+  for (int k = 0; k < LC_PX; ++k) {
+    const bool ok = px_ok[k];
+    const int gp = px_gp[k];
+    const int xf = __builtin_amdgcn_readfirstlane((int)floorf(px_x[k]));
+    const int yf = __builtin_amdgcn_readfirstlane((int)floorf(px_y[k]));
+#pragma unroll
+    for (int l = 0; l < LC_L; ++l) {
+      const int wx0 = (xf >> l) - R, wy0 = (yf >> l) - R;
+      const int tyo = wy0 >> 2, txo = wx0 >> 2;
+      const int ntx = ((wx0 + WD - 1) >> 2) - txo + 1;
+      // (the scalar-interval window test of corr_lookup_kernel<..., SCAL>)
+      const int rlo = max(wy0, 0), rhi = min(wy0 + WD, 4 * lth[l]);
+      const int clo = max(txo, 0), chi = min(txo + ntx, ltw[l]);
+      const int rb = __builtin_amdgcn_readfirstlane(rlo - 4 * tyo), cb = __builtin_amdgcn_readfirstlane(clo - txo);
+      const bool tok = ok && ((unsigned)(lrow - rb) < (unsigned)max(rhi - rlo, 0)) &&
+                       ((unsigned)(tj - cb) < (unsigned)max(chi - clo, 0));
+      const float* wbase = lbs[l] + (long)((unsigned long long)(unsigned)gp * lmsz[l]) + ((long)tyo * ltw[l] + txo) * 16;
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wbase), (short)0, 0x7FFFFFFF, 0x00020000);
+      const unsigned off = tok ? __umul24((unsigned)ti, (unsigned)(64 * ltw[l])) + 16u * (unsigned)(lane & 15)
+                               : 0x80000000u;
+      v[k][l] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    }
   }
-  auto issue_windows = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    if (off32) {
+  }
+  LC_STAMP(1);
+  // ---- 2. while the tiles fly: the per-axis sampling entries of the four pixels ------------
+  // lane (l, ix) = (lane / 9, lane % 9), lanes 0 .. 35: x-entry ix kept in registers, y-entry
+  // ix through LDS (the reference's arithmetic, see axis_entry)
+  int4* ytab = reinterpret_cast<int4*>(smem + LC_OFF_YT) + wv * LC_PX * LC_L * RD;
+  int xw[LC_PX], xi[LC_PX];
+  float xt[LC_PX];
+  bool onp[LC_PX];  // this lane's x- and y-entry lie on the staged patch
 #pragma unroll
-      for (int k = 0; k < LC_PX; ++k) {
-        const unsigned gp = (unsigned)px_gp[k];
-        const int xf = __builtin_amdgcn_readfirstlane((int)floorf(px_x[k]));
-        const int yf = __builtin_amdgcn_readfirstlane((int)floorf(px_y[k]));
+  for (int k = 0; k < LC_PX; ++k) {
+    const float s = __builtin_ldexpf(1.0f, -l);
+    const int xf = __builtin_amdgcn_readfirstlane((int)floorf(px_x[k]));
+    const int yf = __builtin_amdgcn_readfirstlane((int)floorf(px_y[k]));
+    axis_entry<R>(px_x[k] * s, xf >> l, ix, prm[0], prm[1], xw[k], xt[k], xi[k]);
+    int yw, yi;
+    float yt;
+    axis_entry<R>(px_y[k] * s, yf >> l, ix, prm[2], prm[3], yw, yt, yi);
+    onp[k] = xw[k] >= 0 && yw >= 0;
+    if (col) ytab[k * LC_L * RD + lane] = int4{yw >= 0 ? yw * RS * 4 : yw, __float_as_int(yt), __float_as_int(1.0f - yt), yi};
+  }
+  // the flow patch (coords - grid, zero padded)
+  float2* fl = reinterpret_cast<float2*>(smem + LC_OFF_FL);
+  if (fi < LC_FPH * LC_FPW) {
+    float2 fv = {0.f, 0.f};
+    if (fin) {
+      fv.x = fc[0] - (float)fxx;
+      fv.y = fc[1] - (float)fyy;
+    }
+    fl[fi] = fv;
+  }
+  LC_STAMP(2);
+#if LC_A1EARLY
+  // convf1's A operand before the taps, while the window tiles are still in flight
+  __syncthreads();  // the flow patch is visible
+  // convf1's im2col A operand: row mm, K = 2 (dy*7 + dx) + ci (the GATHER packing), 8 K per thread
+  {
+    const int mm = threadIdx.x >> 4, q = threadIdx.x & 15;
+    const int py = mm >> 4, px = mm & 15;
+    float e[8];
 #pragma unroll
-        for (int l = 0; l < LC_L; ++l) {
-          const int wx0 = (xf >> l) - R, wy0 = (yf >> l) - R;
-          const int tyo = wy0 >> 2, txo = wx0 >> 2;
-          const int ntx = ((wx0 + WD - 1) >> 2) - txo + 1;
-          // map row / tile column this lane reads; inside the window and the map, or no access (tests
-          // combined bitwise and the offset selected: no branch around the load)
-          const int rowm = 4 * tyo + lrow, colt = txo + tj;
-          const bool tok = px_ok[k] & ((unsigned)(rowm - wy0) < (unsigned)WD) &
-                           ((unsigned)rowm < (unsigned)(4 * lth[l])) & ((unsigned)tj < (unsigned)ntx) &
-                           ((unsigned)colt < (unsigned)ltw[l]);
-          const unsigned sb = gp * lmsz4[l] + (unsigned)(tyo * ltw[l] + txo) * 64u;
-          unsigned offv = sb + lano[l];
-          asm volatile("" : "+v"(offv));  // (computed for every lane: a select, not a branch around it)
-          const unsigned off = tok ? offv : 0x80000000u;
-          v[k][l] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsl[l], off, 0, 0));
+    for (int i = 0; i < 8; ++i) {
+      const int k = 8 * q + i, t = k >> 1;
+      const int dy = t / LC_F1K, dx = t - dy * LC_F1K;
+      const float2 fv = fl[(py + (k < 2 * LC_F1KK ? dy : 0)) * LC_FPW + px + (k < 2 * LC_F1KK ? dx : 0)];
+      e[i] = k < 2 * LC_F1KK ? ((k & 1) ? fv.y : fv.x) : 0.f;
+    }
+    h8 hi, lo;
+    split8<X3, BF>(f32x4{e[0], e[1], e[2], e[3]}, f32x4{e[4], e[5], e[6], e[7]}, hi, lo);
+    const int j = q >> 2, qd = q & 3, sw = (mm >> 1) & 7;
+    char* row = smem + LC_OFF_A1 + j * (LC_M * 128) + mm * 128;
+    *reinterpret_cast<h8*>(row + ((qd ^ sw) << 4)) = hi;
+    if constexpr (X3) *reinterpret_cast<h8*>(row + (((4 + qd) ^ sw) << 4)) = lo;
+  }
+#endif
+
+  // ---- 3. the taps of each pixel -> split rows of convc1's A operand ------------------------
+  // (default: the first PF K-steps of the weight stream are issued here, behind the tiles, so they
+  // land during the taps)
+#ifndef LC_EARLY
+#pragma unroll
+  for (int j = 0; j < PF; ++j) load_w(j, wb[j]);
+#endif
+  char* Abase = smem;
+  bool big = false;
+  auto patch_of = [&](int k) {
+    return reinterpret_cast<float*>(smem + LC_OFF_PATCH) + (wv * 2 + (k & 1)) * LC_PATCH_FLOATS;
+  };
+  // this lane's nine output channels c = l*81 + ix*9 + iy
+  const int cbase = l * RD * RD + ix * RD;
+  // the nine taps of pixel k from its staged patch
+  auto taps = [&](int k, float (&val)[RD]) {
+    const float* patch = patch_of(k);
+    const int4* yt = ytab + k * LC_L * RD;
+    const float ex = 1.0f - xt[k];
+    const int xwk = xw[k];
+    // the common case: every entry of the wave is finite and on the patch
+    if (__all(!col || onp[k])) {
+      if (col) {
+        const char* p0 = reinterpret_cast<const char*>(&patch[pidx<4>(0, xwk, l)]);
+        const char* p1 = reinterpret_cast<const char*>(&patch[pidx<4>(0, xwk + 1, l)]);
+        auto at = [](const char* bp, int byte) { return *reinterpret_cast<const float*>(bp + byte); };
+#pragma unroll
+        for (int iy = 0; iy < RD; ++iy) {
+#if LC_TAPS2
+          // (8 of the entry's 16 bytes: one ds_read_b64, 2 LDS cycles, instead of a b96 read's 8; 1 - ty
+          // is the same fp32 subtraction axis_entry stored)
+          const int2 ye = *reinterpret_cast<const int2*>(&yt[l * RD + iy]);
+          const int ro = ye.x;
+          const float ty = __int_as_float(ye.y), sS = 1.0f - ty;
+#else
+          const int4 ye = yt[l * RD + iy];
+          const int ro = ye.x;
+          const float ty = __int_as_float(ye.y), sS = __int_as_float(ye.z);
+#endif
+          const f32x2 c0 = {at(p0, ro), at(p0, ro + 4 * RS)}, c1 = {at(p1, ro), at(p1, ro + 4 * RS)};
+          const f32x2 hh = __builtin_elementwise_fma(c0, (f32x2){ex, ex}, c1 * (f32x2){xt[k], xt[k]});
+          val[iy] = fmaf(sS, hh.x, ty * hh.y);
         }
       }
-    } else {
+    } else if (col) {
+      unsigned deferred = 0;
 #pragma unroll
-      for (int k = 0; k < LC_PX; ++k) {
-        const bool ok = px_ok[k];
-        const int gp = px_gp[k];
-        const int xf = __builtin_amdgcn_readfirstlane((int)floorf(px_x[k]));
-        const int yf = __builtin_amdgcn_readfirstlane((int)floorf(px_y[k]));
+      for (int iy = 0; iy < RD; ++iy) {
+        const int4 ye = yt[l * RD + iy];
+        const int yw2 = ye.x;
+        const float ty = __int_as_float(ye.y), sS = __int_as_float(ye.z);
+        const bool on = (xwk | yw2) >= 0;
+        const bool nan = xwk == NAN_POS || yw2 == NAN_POS;
+        const int r0 = on ? yw2 / (4 * RS) : 0, c0 = on ? xwk : 0;
+        const float vv = patch[pidx<4>(r0, c0, l)] * (sS * ex) + patch[pidx<4>(r0, c0 + 1, l)] * (sS * xt[k]) +
+                         patch[pidx<4>(r0 + 1, c0, l)] * (ty * ex) + patch[pidx<4>(r0 + 1, c0 + 1, l)] * (ty * xt[k]);
+        val[iy] = nan ? __builtin_nanf("") : vv;
+        deferred |= (!on && !nan) ? 1u << iy : 0u;
+      }
+      if (deferred != 0) {
+        // taps whose floor the float round trip moved off the staged patch: the four
+        // corners from global memory (zeros outside the map)
+        const Level& lvl = a.lv[l];
+        const float* mp = a.pyr + lvl.off + (long)px_gp[k] * lvl.mapsz;
+        auto at = [&](int yy, int xx) {
+          return ((unsigned)yy < (unsigned)lvl.h && (unsigned)xx < (unsigned)lvl.w) ? mp[tiled_index(yy, xx, lvl.tw)]
+                                                                                    : 0.f;
+        };
 #pragma unroll
-        for (int l = 0; l < LC_L; ++l) {
-          const int wx0 = (xf >> l) - R, wy0 = (yf >> l) - R;
-          const int tyo = wy0 >> 2, txo = wx0 >> 2;
-          const int ntx = ((wx0 + WD - 1) >> 2) - txo + 1;
-          // (the scalar-interval window test of corr_lookup_kernel<..., SCAL>)
-          const int rlo = max(wy0, 0), rhi = min(wy0 + WD, 4 * lth[l]);
-          const int clo = max(txo, 0), chi = min(txo + ntx, ltw[l]);
-          const int rb = __builtin_amdgcn_readfirstlane(rlo - 4 * tyo), cb = __builtin_amdgcn_readfirstlane(clo - txo);
-          const bool tok = ok && ((unsigned)(lrow - rb) < (unsigned)max(rhi - rlo, 0)) &&
-                           ((unsigned)(tj - cb) < (unsigned)max(chi - clo, 0));
-          const float* wbase =
-              lbs[l] + (long)((unsigned long long)(unsigned)gp * lmsz[l]) + ((long)tyo * ltw[l] + txo) * 16;
-          const __amdgpu_buffer_rsrc_t rs =
-              __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wbase), (short)0, 0x7FFFFFFF, 0x00020000);
-          const unsigned off = tok ? __umul24((unsigned)ti, (unsigned)(64 * ltw[l])) + 16u * (unsigned)(lane & 15)
-                                   : 0x80000000u;
-          v[k][l] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+        for (int iy = 0; iy < RD; ++iy) {
+          if (!((deferred >> iy) & 1u)) continue;
+          const int4 ye = yt[l * RD + iy];
+          const int yi = ye.w;
+          const float ty = __int_as_float(ye.y), sS = __int_as_float(ye.z);
+          val[iy] = at(yi, xi[k]) * (sS * ex) + at(yi, xi[k] + 1) * (sS * xt[k]) + at(yi + 1, xi[k]) * (ty * ex) +
+                    at(yi + 1, xi[k] + 1) * (ty * xt[k]);
         }
       }
     }
   };
-  issue_windows();
-  LC_STAMP(1);
-
-  bool big = false;
-  const bool f1w = wv < LC_F1N / 32;  // (wave-uniform)
-  int xw[LC_PX], xi[LC_PX];
-  float xt[LC_PX];
-  bool onp[LC_PX];  // this lane's x- and y-entry lie on the staged patch
-
-  for (;;) {
-    // (the lane index as a loop-variant value, and every lane constant of the body derived from it
-    // here: otherwise the compiler hoists each lane's LDS addresses and swizzles out of the tile loop
-    // and keeps them live across it, 256 VGPRs with spills)
-    int lz = 0;
-    if constexpr (PERS) asm volatile("" : "+v"(lz));
-    const int lane = (int)(threadIdx.x & 63) + lz;
-    const int tj = (lane >> 2) & 3, lrow = (lane >> 4) * 4 + (lane & 3);
-    const bool col = lane < LC_L * RD;
-    int lq = 0;
-#pragma unroll
-    for (int k = 1; k < LC_L; ++k) lq += lane >= k * RD ? 1 : 0;
-    const int l = col ? lq : 0;
-    const int ix = lane - l * RD;
-    const int cbase = l * RD * RD + ix * RD;
-    const int m = lane & 31, h = lane >> 5;
-    const int sw = (m >> 1) & 7;
-    char* const sm = smem;
-    int4* ytab = reinterpret_cast<int4*>(sm + LC_OFF_YT) + wv * LC_PX * LC_L * RD;
-    float2* fl = reinterpret_cast<float2*>(sm + LC_OFF_FL);
-    char* Abase = sm;
-    auto patch_of = [&](int k) {
-      return reinterpret_cast<float*>(sm + LC_OFF_PATCH) + (wv * 2 + (k & 1)) * LC_PATCH_FLOATS;
-    };
-    // ---- 2. while the tiles fly: the per-axis sampling entries of the four pixels ------------
-    // lane (l, ix) = (lane / 9, lane % 9), lanes 0 .. 35: x-entry ix kept in registers, y-entry
-    // ix through LDS (the reference's arithmetic, see axis_entry)
-#pragma unroll
-    for (int k = 0; k < LC_PX; ++k) {
-      const float s = __builtin_ldexpf(1.0f, -l);
-      const int xf = __builtin_amdgcn_readfirstlane((int)floorf(px_x[k]));
-      const int yf = __builtin_amdgcn_readfirstlane((int)floorf(px_y[k]));
-      axis_entry<R>(px_x[k] * s, xf >> l, ix, prm[0], prm[1], xw[k], xt[k], xi[k]);
-      int yw, yi;
-      float yt;
-      axis_entry<R>(px_y[k] * s, yf >> l, ix, prm[2], prm[3], yw, yt, yi);
-      onp[k] = xw[k] >= 0 && yw >= 0;
-      if (col) ytab[k * LC_L * RD + lane] = int4{yw >= 0 ? yw * RS * 4 : yw, __float_as_int(yt), __float_as_int(1.0f - yt), yi};
-    }
-    // the flow patch (coords - grid, zero padded)
-    if (fi < LC_FPH * LC_FPW) {
-      float2 fv = {0.f, 0.f};
-      if (fin) {
-        fv.x = fc[0] - (float)fxx;
-        fv.y = fc[1] - (float)fyy;
-      }
-      fl[fi] = fv;
-    }
-    LC_STAMP(2);
-
-    // ---- 3. the taps of each pixel -> split rows of convc1's A operand ------------------------
-    // (the first PF K-steps of the weight stream are issued here, behind the tiles, so they land
-    // during the taps)
-#pragma unroll
-    for (int j = 0; j < PF; ++j) load_w(j, wb[j]);
-    // the next tile's coords, under the taps (issued on the last tile too, for the current one: the
-    // same loads on every path keep the compiler's load counts exact)
-    const int ntile = tile + (int)gridDim.x;
-    const bool more = PERS && ntile < g.ntiles;  // (uniform)
-    int nb = b, ny0 = y0, nx0 = x0;
-    if constexpr (PERS) {
-      if (more) geom(ntile, nb, ny0, nx0);
-      issue_coords(nb, ny0, nx0);
-    }
-    // the nine taps of pixel k from its staged patch
-    auto taps = [&](int k, float (&val)[RD]) {
-      const float* patch = patch_of(k);
-      const int4* yt = ytab + k * LC_L * RD;
-      const float ex = 1.0f - xt[k];
-      const int xwk = xw[k];
-      // the common case: every entry of the wave is finite and on the patch
-      if (__all(!col || onp[k])) {
-        if (col) {
-          const char* p0 = reinterpret_cast<const char*>(&patch[pidx<4>(0, xwk, l)]);
-          const char* p1 = reinterpret_cast<const char*>(&patch[pidx<4>(0, xwk + 1, l)]);
-          auto at = [](const char* bp, int byte) { return *reinterpret_cast<const float*>(bp + byte); };
-#pragma unroll
-          for (int iy = 0; iy < RD; ++iy) {
+  // pixel k's taps, split, straight into its row of the A operand (2-B writes); lanes 36 .. 63
+  // write the row's zero K padding (channels 324 .. 351)
+  auto write_row = [&](int k, const float (&val)[RD]) {
+    const int mk = LC_PX * wv + k;
+    const int sw = (mk >> 1) & 7;
 #if LC_TAPS2
-            // (8 of the entry's 16 bytes: one ds_read_b64, 2 LDS cycles, instead of a b96 read's 8; 1 - ty
-            // is the same fp32 subtraction axis_entry stored)
-            const int2 ye = *reinterpret_cast<const int2*>(&yt[l * RD + iy]);
-            const int ro = ye.x;
-            const float ty = __int_as_float(ye.y), sS = 1.0f - ty;
-#else
-            const int4 ye = yt[l * RD + iy];
-            const int ro = ye.x;
-            const float ty = __int_as_float(ye.y), sS = __int_as_float(ye.z);
-#endif
-            const f32x2 c0 = {at(p0, ro), at(p0, ro + 4 * RS)}, c1 = {at(p1, ro), at(p1, ro + 4 * RS)};
-            const f32x2 hh = __builtin_elementwise_fma(c0, (f32x2){ex, ex}, c1 * (f32x2){xt[k], xt[k]});
-            val[iy] = fmaf(sS, hh.x, ty * hh.y);
-          }
-        }
-      } else if (col) {
-        unsigned deferred = 0;
+    // the lane's nine consecutive channels as four 4-B writes of channel pairs (c even, c + 1: one
+    // f16 pair of one quad) and one 2-B write, per half: 10 LDS writes instead of 18
+    if (col) {
+      const int par = cbase & 1;
+      float vv[RD];
 #pragma unroll
-        for (int iy = 0; iy < RD; ++iy) {
-          const int4 ye = yt[l * RD + iy];
-          const int yw2 = ye.x;
-          const float ty = __int_as_float(ye.y), sS = __int_as_float(ye.z);
-          const bool on = (xwk | yw2) >= 0;
-          const bool nan = xwk == NAN_POS || yw2 == NAN_POS;
-          const int r0 = on ? yw2 / (4 * RS) : 0, c0 = on ? xwk : 0;
-          const float vv = patch[pidx<4>(r0, c0, l)] * (sS * ex) + patch[pidx<4>(r0, c0 + 1, l)] * (sS * xt[k]) +
-                           patch[pidx<4>(r0 + 1, c0, l)] * (ty * ex) + patch[pidx<4>(r0 + 1, c0 + 1, l)] * (ty * xt[k]);
-          val[iy] = nan ? __builtin_nanf("") : vv;
-          deferred |= (!on && !nan) ? 1u << iy : 0u;
-        }
-        if (deferred != 0) {
-          // taps whose floor the float round trip moved off the staged patch: the four
-          // corners from global memory (zeros outside the map)
-          const Level& lvl = a.lv[l];
-          const float* mp = a.pyr + lvl.off + (long)px_gp[k] * lvl.mapsz;
-          auto at = [&](int yy, int xx) {
-            return ((unsigned)yy < (unsigned)lvl.h && (unsigned)xx < (unsigned)lvl.w) ? mp[tiled_index(yy, xx, lvl.tw)]
-                                                                                      : 0.f;
-          };
-#pragma unroll
-          for (int iy = 0; iy < RD; ++iy) {
-            if (!((deferred >> iy) & 1u)) continue;
-            const int4 ye = yt[l * RD + iy];
-            const int yi = ye.w;
-            const float ty = __int_as_float(ye.y), sS = __int_as_float(ye.z);
-            val[iy] = at(yi, xi[k]) * (sS * ex) + at(yi, xi[k] + 1) * (sS * xt[k]) + at(yi + 1, xi[k]) * (ty * ex) +
-                      at(yi + 1, xi[k] + 1) * (ty * xt[k]);
-          }
-        }
+      for (int iy = 0; iy < RD; ++iy) {
+        vv[iy] = px_ok[k] ? val[iy] : 0.f;
+        big |= fabsf(vv[iy]) > RAFT_RANGE_LIMIT;
       }
-    };
-    // pixel k's taps, split, straight into its row of the A operand (2-B writes); lanes 36 .. 63
-    // write the row's zero K padding (channels 324 .. 351)
-    auto write_row = [&](int k, const float (&val)[RD]) {
-      const int mk = LC_PX * wv + k;
-      const int swr = (mk >> 1) & 7;
-#if LC_TAPS2
-      // the lane's nine consecutive channels as four 4-B writes of channel pairs (c even, c + 1: one
-      // f16 pair of one quad) and one 2-B write, per half: 10 LDS writes instead of 18
-      if (col) {
-        const int par = cbase & 1;
-        float vv[RD];
-#pragma unroll
-        for (int iy = 0; iy < RD; ++iy) {
-          vv[iy] = px_ok[k] ? val[iy] : 0.f;
-          big |= fabsf(vv[iy]) > RAFT_RANGE_LIMIT;
-        }
-        auto at_c = [&](int c, int half) {  // byte address of channel c's f16 in half 0 (hi) / 1 (lo)
-          const int j = c >> 5, kk = c & 31;
-          return Abase + j * (LC_M * 128) + mk * 128 + (((4 * half + (kk >> 3)) ^ swr) << 4) + 2 * (kk & 7);
-        };
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float a0 = par ? vv[2 * q + 1] : vv[2 * q], a1 = par ? vv[2 * q + 2] : vv[2 * q + 1];
-          _Float16 h0, l0, h1, l1;
-          split1<X3, BF>(a0, h0, l0);
-          split1<X3, BF>(a1, h1, l1);
-          const int c = cbase + 2 * q + par;  // even
-          *reinterpret_cast<h2*>(at_c(c, 0)) = h2{h0, h1};
-          if constexpr (X3) *reinterpret_cast<h2*>(at_c(c, 1)) = h2{l0, l1};
-        }
-        {
-          const float av = par ? vv[0] : vv[RD - 1];
-          _Float16 hs, ls;
-          split1<X3, BF>(av, hs, ls);
-          const int c = cbase + (par ? 0 : RD - 1);
-          *reinterpret_cast<_Float16*>(at_c(c, 0)) = hs;
-          if constexpr (X3) *reinterpret_cast<_Float16*>(at_c(c, 1)) = ls;
-        }
-      } else if (lane - LC_L * RD < 32 * LC_KS - LC_NTAP) {
-#else
-      if (col) {
-#pragma unroll
-        for (int iy = 0; iy < RD; ++iy) {
-          const float vv = px_ok[k] ? val[iy] : 0.f;
-          big |= fabsf(vv) > RAFT_RANGE_LIMIT;
-          const int c = cbase + iy;
-          const int j = c >> 5, kk = c & 31;
-          _Float16 hi, lo;
-          split1<X3, BF>(vv, hi, lo);
-          char* rb = Abase + j * (LC_M * 128) + mk * 128;
-          *reinterpret_cast<_Float16*>(rb + (((kk >> 3) ^ swr) << 4) + 2 * (kk & 7)) = hi;
-          if constexpr (X3) *reinterpret_cast<_Float16*>(rb + (((4 + (kk >> 3)) ^ swr) << 4) + 2 * (kk & 7)) = lo;
-        }
-      } else if (lane - LC_L * RD < 32 * LC_KS - LC_NTAP) {
-#endif
-        const int c = LC_NTAP + lane - LC_L * RD;
+      auto at_c = [&](int c, int half) {  // byte address of channel c's f16 in half 0 (hi) / 1 (lo)
         const int j = c >> 5, kk = c & 31;
+        return Abase + j * (LC_M * 128) + mk * 128 + (((4 * half + (kk >> 3)) ^ sw) << 4) + 2 * (kk & 7);
+      };
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float a0 = par ? vv[2 * q + 1] : vv[2 * q], a1 = par ? vv[2 * q + 2] : vv[2 * q + 1];
+        _Float16 h0, l0, h1, l1;
+        split1<X3, BF>(a0, h0, l0);
+        split1<X3, BF>(a1, h1, l1);
+        const int c = cbase + 2 * q + par;  // even
+        *reinterpret_cast<h2*>(at_c(c, 0)) = h2{h0, h1};
+        if constexpr (X3) *reinterpret_cast<h2*>(at_c(c, 1)) = h2{l0, l1};
+      }
+      {
+        const float a = par ? vv[0] : vv[RD - 1];
+        _Float16 hs, ls;
+        split1<X3, BF>(a, hs, ls);
+        const int c = cbase + (par ? 0 : RD - 1);
+        *reinterpret_cast<_Float16*>(at_c(c, 0)) = hs;
+        if constexpr (X3) *reinterpret_cast<_Float16*>(at_c(c, 1)) = ls;
+      }
+    } else if (lane - LC_L * RD < 32 * LC_KS - LC_NTAP) {
+#else
+    if (col) {
+#pragma unroll
+      for (int iy = 0; iy < RD; ++iy) {
+        const float vv = px_ok[k] ? val[iy] : 0.f;
+        big |= fabsf(vv) > RAFT_RANGE_LIMIT;
+        const int c = cbase + iy;
+        const int j = c >> 5, kk = c & 31;
+        _Float16 hi, lo;
+        split1<X3, BF>(vv, hi, lo);
         char* rb = Abase + j * (LC_M * 128) + mk * 128;
-        *reinterpret_cast<_Float16*>(rb + (((kk >> 3) ^ swr) << 4) + 2 * (kk & 7)) = (_Float16)0.f;
-        if constexpr (X3) *reinterpret_cast<_Float16*>(rb + (((4 + (kk >> 3)) ^ swr) << 4) + 2 * (kk & 7)) = (_Float16)0.f;
+        *reinterpret_cast<_Float16*>(rb + (((kk >> 3) ^ sw) << 4) + 2 * (kk & 7)) = hi;
+        if constexpr (X3) *reinterpret_cast<_Float16*>(rb + (((4 + (kk >> 3)) ^ sw) << 4) + 2 * (kk & 7)) = lo;
       }
-      if (a.flow && lane < 2 && px_ok[k]) {
-        const int p = px_gp[k] - b * P;
-        const float gcoord = lane == 0 ? (float)(p % W) : (float)(p / W);
-        a.flow[(long)px_gp[k] * a.flow_ld + lane] = (lane == 0 ? px_x[k] : px_y[k]) - gcoord;
-      }
-    };
-    // two pixels per round: both patches staged, one wave sync, both pixels' taps interleaved
-#pragma unroll
-    for (int k = 0; k < LC_PX; k += 2) {
-#pragma unroll
-      for (int lv_ = 0; lv_ < LC_L; ++lv_) {
-        *reinterpret_cast<f32x4*>(&patch_of(k)[pidx<4>(lrow, tj * 4, lv_)]) = v[k][lv_];
-        *reinterpret_cast<f32x4*>(&patch_of(k + 1)[pidx<4>(lrow, tj * 4, lv_)]) = v[k + 1][lv_];
-      }
-      wave_sync();
-      float va[RD], vb[RD];
-      taps(k, va);
-      taps(k + 1, vb);
-      write_row(k, va);
-      write_row(k + 1, vb);
-      wave_sync();  // (the patches are read before the next round overwrites them)
-    }
-    LC_STAMP(3);
-#ifndef LC_PERS_EARLY
-#define LC_PERS_EARLY 0
+    } else if (lane - LC_L * RD < 32 * LC_KS - LC_NTAP) {
 #endif
-    // the next tile's window tiles, issued so that their round trip runs under this tile's convs
-    // (LC_PERS_EARLY) or epilogue (on the last tile: its own pixels, no access)
-    auto next_windows = [&]() {
-      set_px(nb, ny0, nx0);
-#pragma unroll
-      for (int k = 0; k < LC_PX; ++k) px_ok[k] &= more;
-      resolve_coords();
-      issue_windows();
-    };
-    if constexpr (PERS && LC_PERS_EARLY) next_windows();
-    __syncthreads();  // the flow patch is visible
-    // convf1's im2col A operand: row mm, K = 2 (dy*7 + dx) + ci (the GATHER packing), 8 K per thread
-    {
-      const int tid = wv * 64 + lane;  // (loop-variant, see lane)
-      const int mm = tid >> 4, q = tid & 15;
-      const int py = mm >> 4, px = mm & 15;
-      float e[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int k = 8 * q + i, t = k >> 1;
-        const int dy = t / LC_F1K, dx = t - dy * LC_F1K;
-        const float2 fv = fl[(py + (k < 2 * LC_F1KK ? dy : 0)) * LC_FPW + px + (k < 2 * LC_F1KK ? dx : 0)];
-        e[i] = k < 2 * LC_F1KK ? ((k & 1) ? fv.y : fv.x) : 0.f;
-      }
-      h8 hi, lo;
-      split8<X3, BF>(f32x4{e[0], e[1], e[2], e[3]}, f32x4{e[4], e[5], e[6], e[7]}, hi, lo);
-      const int j = q >> 2, qd = q & 3, swa = (mm >> 1) & 7;
-      char* row = sm + LC_OFF_A1 + j * (LC_M * 128) + mm * 128;
-      *reinterpret_cast<h8*>(row + ((qd ^ swa) << 4)) = hi;
-      if constexpr (X3) *reinterpret_cast<h8*>(row + (((4 + qd) ^ swa) << 4)) = lo;
+      const int c = LC_NTAP + lane - LC_L * RD;
+      const int j = c >> 5, kk = c & 31;
+      char* rb = Abase + j * (LC_M * 128) + mk * 128;
+      *reinterpret_cast<_Float16*>(rb + (((kk >> 3) ^ sw) << 4) + 2 * (kk & 7)) = (_Float16)0.f;
+      if constexpr (X3) *reinterpret_cast<_Float16*>(rb + (((4 + (kk >> 3)) ^ sw) << 4) + 2 * (kk & 7)) = (_Float16)0.f;
     }
-    __syncthreads();  // every A row is in LDS
-    LC_STAMP(4);
-
-    // ---- 4. convc1 (all waves, 32 outputs each) then convf1 (waves 0-3) on MFMA: one K stream ----
-    auto kstep = [&](const char* A, const h8 (&B)[NT], f32x16& c, f32x16& cx_) {
-      const char* row = A + m * 128;
-      h8 ah[2], al[2];
-#pragma unroll
-      for (int qq = 0; qq < 2; ++qq) {
-        ah[qq] = *reinterpret_cast<const h8*>(row + (((2 * h + qq) ^ sw) << 4));
-        if constexpr (X3) al[qq] = *reinterpret_cast<const h8*>(row + (((4 + 2 * h + qq) ^ sw) << 4));
-      }
-#pragma unroll
-      for (int qq = 0; qq < 2; ++qq) {
-        if constexpr (BF) {
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8, ah[qq]), __builtin_bit_cast(bf8, B[qq]), c,
-                                                      0, 0, 0);
-        } else {
-          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[qq], B[qq], c, 0, 0, 0);
-        }
-        if constexpr (X3) {
-          cx_ = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[qq], B[2 + qq], cx_, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[qq], B[qq], c, 0, 0, 0);
-        }
-      }
-    };
-    f32x16 acc = {}, accx = {}, facc = {}, faccx = {};
-#pragma unroll
-    for (int j = 0; j < LC_KS; ++j) {
-      // (the K stream continues into convf1's steps on waves 0-3)
-      if (j + PF < LC_KS || f1w) load_w(j + PF, wb[(j + PF) % (PF + 1)]);
-      kstep(Abase + j * (LC_M * 128), wb[j % (PF + 1)], acc, accx);
+    if (a.flow && lane < 2 && px_ok[k]) {
+      const int p = px_gp[k] - b * P;
+      const float gcoord = lane == 0 ? (float)(p % W) : (float)(p / W);
+      a.flow[(long)px_gp[k] * a.flow_ld + lane] = (lane == 0 ? px_x[k] : px_y[k]) - gcoord;
     }
-    if (f1w) {
+  };
+  // two pixels per round: both patches staged, one wave sync, both pixels' taps interleaved
 #pragma unroll
-      for (int j = LC_KS; j < LC_KS + LC_F1KS; ++j) {
-        if (j + PF < LC_KS + LC_F1KS) load_w(j + PF, wb[(j + PF) % (PF + 1)]);
-        kstep(sm + LC_OFF_A1 + (j - LC_KS) * (LC_M * 128), wb[j % (PF + 1)], facc, faccx);
-      }
+  for (int k = 0; k < LC_PX; k += 2) {
+#pragma unroll
+    for (int lv_ = 0; lv_ < LC_L; ++lv_) {
+      *reinterpret_cast<f32x4*>(&patch_of(k)[pidx<4>(lrow, tj * 4, lv_)]) = v[k][lv_];
+      *reinterpret_cast<f32x4*>(&patch_of(k + 1)[pidx<4>(lrow, tj * 4, lv_)]) = v[k + 1][lv_];
     }
-    if constexpr (X3) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        acc[r] += accx[r] * (1.0f / SPLIT_SCALE);
-        facc[r] += faccx[r] * (1.0f / SPLIT_SCALE);
-      }
-    }
-#ifdef LC_STAMPS
-    asm volatile("" ::"v"(acc[0]), "v"(acc[15]), "v"(facc[0]));
-#endif
-    LC_STAMP(5);
-    if constexpr (PERS && !LC_PERS_EARLY) next_windows();
-
-    // ---- 5. epilogues: bias, relu, range guard, NHWC rows ----------------------------------------
-    auto store = [&](const f32x16& c, float bias, float* out, int ld, int n, int* flag) {
-      bool obig = false;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int mm = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int yy = y0 + (mm >> 4), xx = x0 + (mm & 15);
-        const float o = fmaxf(c[r] + bias, 0.f);
-        if (yy < H && xx < W) {
-          obig |= o > RAFT_RANGE_LIMIT;
-          out[((long)b * P + yy * W + xx) * ld + n] = o;
-        }
-      }
-      if (flag && obig) *flag = 1;
-    };
-    store(acc, c1b, g.out, g.out_ld, 32 * wv + m, g.out_flag);
-    if (f1w) store(facc, f1b, g.f1out, g.f1out_ld, 32 * wv + m, g.f1flag);
-    if (!more) break;
-    // the next tile
-    tile = ntile;
-    b = nb;
-    y0 = ny0;
-    x0 = nx0;
-    __syncthreads();  // this tile's A operands are read before the next tile's taps overwrite them
+    wave_sync();
+    float va[RD], vb[RD];
+    taps(k, va);
+    taps(k + 1, vb);
+    write_row(k, va);
+    write_row(k + 1, vb);
+    wave_sync();  // (the patches are read before the next round overwrites them)
   }
   if (a.range_flag && big) *a.range_flag = 1;
+  LC_STAMP(3);
+#if LC_A1EARLY
+  __syncthreads();  // every A row is in LDS
+#else
+  __syncthreads();  // the flow patch is visible
+  // convf1's im2col A operand: row mm, K = 2 (dy*7 + dx) + ci (the GATHER packing), 8 K per thread
+  {
+    const int mm = threadIdx.x >> 4, q = threadIdx.x & 15;
+    const int py = mm >> 4, px = mm & 15;
+    float e[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int k = 8 * q + i, t = k >> 1;
+      const int dy = t / LC_F1K, dx = t - dy * LC_F1K;
+      const float2 fv = fl[(py + (k < 2 * LC_F1KK ? dy : 0)) * LC_FPW + px + (k < 2 * LC_F1KK ? dx : 0)];
+      e[i] = k < 2 * LC_F1KK ? ((k & 1) ? fv.y : fv.x) : 0.f;
+    }
+    h8 hi, lo;
+    split8<X3, BF>(f32x4{e[0], e[1], e[2], e[3]}, f32x4{e[4], e[5], e[6], e[7]}, hi, lo);
+    const int j = q >> 2, qd = q & 3, sw = (mm >> 1) & 7;
+    char* row = smem + LC_OFF_A1 + j * (LC_M * 128) + mm * 128;
+    *reinterpret_cast<h8*>(row + ((qd ^ sw) << 4)) = hi;
+    if constexpr (X3) *reinterpret_cast<h8*>(row + (((4 + qd) ^ sw) << 4)) = lo;
+  }
+  __syncthreads();  // every A row is in LDS
+#endif
+  LC_STAMP(4);
+
+  // ---- 4. convc1 (all waves, 32 outputs each) then convf1 (waves 0-3) on MFMA: one K stream ----
+  const int sw = (m >> 1) & 7;
+  auto kstep = [&](const char* A, const h8 (&B)[NT], f32x16& c, f32x16& cx) {
+    const char* row = A + m * 128;
+    h8 ah[2], al[2];
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      ah[qq] = *reinterpret_cast<const h8*>(row + (((2 * h + qq) ^ sw) << 4));
+      if constexpr (X3) al[qq] = *reinterpret_cast<const h8*>(row + (((4 + 2 * h + qq) ^ sw) << 4));
+    }
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      if constexpr (BF) {
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8, ah[qq]), __builtin_bit_cast(bf8, B[qq]), c,
+                                                    0, 0, 0);
+      } else {
+        c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[qq], B[qq], c, 0, 0, 0);
+      }
+      if constexpr (X3) {
+        cx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[qq], B[2 + qq], cx, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[qq], B[qq], c, 0, 0, 0);
+      }
+    }
+  };
+  f32x16 acc = {}, accx = {}, facc = {}, faccx = {};
+  const bool f1w = wv < LC_F1N / 32;  // (wave-uniform)
+#pragma unroll
+  for (int j = 0; j < LC_KS; ++j) {
+    // (the K stream continues into convf1's steps on waves 0-3)
+    if (j + PF < LC_KS || f1w) load_w(j + PF, wb[(j + PF) % (PF + 1)]);
+    kstep(Abase + j * (LC_M * 128), wb[j % (PF + 1)], acc, accx);
+  }
+  if (f1w) {
+#pragma unroll
+    for (int j = LC_KS; j < LC_KS + LC_F1KS; ++j) {
+      if (j + PF < LC_KS + LC_F1KS) load_w(j + PF, wb[(j + PF) % (PF + 1)]);
+      kstep(smem + LC_OFF_A1 + (j - LC_KS) * (LC_M * 128), wb[j % (PF + 1)], facc, faccx);
+    }
+  }
+  if constexpr (X3) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      acc[r] += accx[r] * (1.0f / SPLIT_SCALE);
+      facc[r] += faccx[r] * (1.0f / SPLIT_SCALE);
+    }
+  }
+#ifdef LC_STAMPS
+  asm volatile("" ::"v"(acc[0]), "v"(acc[15]), "v"(facc[0]));
+#endif
+  LC_STAMP(5);
+
+  // ---- 5. epilogues: bias, relu, range guard, NHWC rows ----------------------------------------
+  auto store = [&](const f32x16& c, float bias, float* out, int ld, int n, int* flag) {
+    bool obig = false;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int mm = (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int yy = y0 + (mm >> 4), xx = x0 + (mm & 15);
+      const float o = fmaxf(c[r] + bias, 0.f);
+      if (yy < H && xx < W) {
+        obig |= o > RAFT_RANGE_LIMIT;
+        out[((long)b * P + yy * W + xx) * ld + n] = o;
+      }
+    }
+    if (flag && obig) *flag = 1;
+  };
+  store(acc, c1b, g.out, g.out_ld, 32 * wv + m, g.out_flag);
+  if (wv < LC_F1N / 32) store(facc, f1b, g.f1out, g.f1out_ld, 32 * wv + m, g.f1flag);
   if (g.span_slot >= 0) {  // (uniform) the work-group's end once its stores have completed
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     if (threadIdx.x == 0)
       atomicMax(&g_lc_span[2 * g.span_slot + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
   }
+#ifdef LC_END_FENCE  // dev experiment: agent-scope release of the outputs before the waves exit
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __builtin_amdgcn_s_waitcnt(0);
+#endif
 #ifdef LC_STAMPS
   __builtin_amdgcn_s_waitcnt(0);
   LC_STAMP(6);
@@ -706,37 +672,6 @@ extern "C" size_t raft_lookup_conv_weight_floats(int n, int k_pad) {
   if (n <= 0 || n % 32 || k_pad <= 0) return 0;
   return (size_t)((k_pad + 31) / 32) * (size_t)n * 32;
 }
-
-namespace raft {
-namespace {
-// the device's CU count (one work-group per CU), cached per device
-long lc_cus() {
-  constexpr int MAXDEV = 64;
-  static std::atomic<int> cache[MAXDEV];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 256L;
-  if (dev >= 0 && dev < MAXDEV) {
-    const int c = cache[dev].load(std::memory_order_relaxed);
-    if (c > 0) return (long)c;
-  }
-  int cus = 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  if (dev >= 0 && dev < MAXDEV) cache[dev].store(cus, std::memory_order_relaxed);
-  return (long)cus;
-}
-// persistent work-groups for multi-round launches: RAFT_LC_PERSIST=0 (or the setter) turns them off
-std::atomic<int> g_lc_pers{-1};
-bool lc_persistent() {
-  int v = g_lc_pers.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char* e = std::getenv("RAFT_LC_PERSIST");
-    v = (e && e[0] == '0') ? 0 : 1;
-    g_lc_pers.store(v, std::memory_order_relaxed);
-  }
-  return v != 0;
-}
-}  // namespace
-}  // namespace raft
 
 extern "C" int raft_lookup_conv_pack_weight(const void* split_weight, int n_pad, int k_pad, int n, void* out,
                                             raft_stream_t stream) {
@@ -789,34 +724,15 @@ extern "C" int raft_corr_lookup_conv(const float* pyramid, int B, int H, int W, 
   g.span_slot = !capturing && g_lc_span_next >= 0 && g_lc_span_next < LC_SPAN_SLOTS ? g_lc_span_next++ : -1;
   const long nt = (long)B * g.tx_n * g.ty_n;
   RAFT_REQUIRE(nt < (1L << 31), "raft_corr_lookup_conv: grid too large");
-  g.ntiles = (int)nt;
   hipStream_t s = as_stream(stream);
-  // more tiles than one round (one work-group per CU: 151 KB of LDS): persistent work-groups
-  const long cus = lc_cus();
-  const bool pers = lc_persistent() && nt > cus;
-  const dim3 grid((unsigned)(pers ? cus : nt));
-#define RAFT_LC_LAUNCH(PR)                                                     \
-  if (pers)                                                                   \
-    hipLaunchKernelGGL((lookup_conv_kernel<PR, true>), grid, dim3(512), 0, s, g); \
-  else                                                                        \
-    hipLaunchKernelGGL((lookup_conv_kernel<PR, false>), grid, dim3(512), 0, s, g)
-  if (precision == RAFT_PREC_F16X3) {
-    RAFT_LC_LAUNCH(RAFT_PREC_F16X3);
-  } else if (precision == RAFT_PREC_F16) {
-    RAFT_LC_LAUNCH(RAFT_PREC_F16);
-  } else {
-    RAFT_LC_LAUNCH(RAFT_PREC_BF16);
-  }
-#undef RAFT_LC_LAUNCH
+  const dim3 grid((unsigned)nt);
+  if (precision == RAFT_PREC_F16X3)
+    hipLaunchKernelGGL(lookup_conv_kernel<RAFT_PREC_F16X3>, grid, dim3(512), 0, s, g);
+  else if (precision == RAFT_PREC_F16)
+    hipLaunchKernelGGL(lookup_conv_kernel<RAFT_PREC_F16>, grid, dim3(512), 0, s, g);
+  else
+    hipLaunchKernelGGL(lookup_conv_kernel<RAFT_PREC_BF16>, grid, dim3(512), 0, s, g);
   return check_launch("raft_corr_lookup_conv");
-}
-
-// raft_corr_lookup_conv_set_persistent (include/raft_hip.h): 1 = on (default), 0 = one tile per work-group
-extern "C" int raft_corr_lookup_conv_set_persistent(int on) {
-  using namespace raft;
-  const int prev = lc_persistent() ? 1 : 0;
-  if (on == 0 || on == 1) g_lc_pers.store(on, std::memory_order_relaxed);
-  return prev;
 }
 
 // launch-span timing of raft_corr_lookup_conv (include/raft_hip.h)

@@ -156,27 +156,3 @@ def test_raft_fused_lookup_conv_matches_unfused(monkeypatch):
     assert names.count("raft_corr_lookup_conv") == 12
     assert float((up_a - up_b).abs().max()) < 1e-3
     assert float((lo_a - lo_b).abs().max()) < 1e-3
-
-
-@pytest.mark.parametrize("B,h,w", [(2, 55, 128), (1, 514, 16), (5, 33, 70)])
-@pytest.mark.parametrize("prec", ["f16x3", "bf16"])
-def test_lookup_conv_persistent_equals_one_tile_per_workgroup(B, h, w, prec):
-    """More tiles than CUs (448, 257 = one past a round, 425 ragged): the persistent work-groups
-    (next tile's loads under the current tile's convs) give the same bytes as one tile per
-    work-group, and both match the unfused reference."""
-    from raft_optical_flow_amd import _lib
-    lib = _lib.load()
-    assert lib.raft_corr_lookup_conv_set_persistent(-1) == 1  # the default
-    d1 = _case(B, h, w, prec)
-    prev = lib.raft_corr_lookup_conv_set_persistent(0)
-    try:
-        d0 = _case(B, h, w, prec)
-    finally:
-        lib.raft_corr_lookup_conv_set_persistent(prev)
-    for k in ("c1", "f1", "flow_b"):
-        assert torch.equal(d1[k], d0[k]), k
-    got = d1["c1"][:, :256].cpu().double()
-    scale = float(d1["ref"].abs().max())
-    assert float((got - d1["ref"]).abs().max()) <= TOL[prec] * max(1.0, scale)
-    assert torch.equal(d1["flow_a"], d1["flow_b"])
-    assert d1["flags"] == [0, 0, 0]
