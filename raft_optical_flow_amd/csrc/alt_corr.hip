@@ -658,6 +658,41 @@ __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevel
       ALT_ST(3);
       if (r0 + cur.br < cur.bh) load_band(l, cur, r0 + cur.br);  // in flight under the MFMAs
       ALT_ST(4);
+#ifndef ALT_MFMA16
+#define ALT_MFMA16 1
+#endif
+#if ALT_MFMA16
+      // all 8 waves on 16x16 blocks: wave g owns query rows 16 (g & 3) .. +15 and band pixels
+      // 48 (g >> 2) .. +47 (three 16x16 blocks), so each SIMD carries two waves' equal share
+      // (the 32x32 form ran on waves 0-5: SIMDs 0 and 1 did two waves' MFMAs, SIMDs 2 and 3 one)
+      f32x4 c0[3] = {}, c1[3] = {}, c2[3] = {};
+      const int rb = g & 3, cg = g >> 2, rl = lane & 15, kg = lane >> 4;
+      for (int s = 0; s < ks; ++s) {
+        const int ar = s * (AT * AT) + 16 * rb + rl;
+        const char* Ar = As + ar * AM_ROW;
+        const h8 xh = *reinterpret_cast<const h8*>(Ar + am_chunk(ar, kg));
+        const h8 xl = *reinterpret_cast<const h8*>(Ar + am_chunk(ar, 4 + kg));
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          const int brow = s * AM_NB + 48 * cg + 16 * t + rl;
+          const char* Br = Bs + brow * AM_ROW;
+          const h8 yh = *reinterpret_cast<const h8*>(Br + am_chunk(brow, kg));
+          const h8 yl = *reinterpret_cast<const h8*>(Br + am_chunk(brow, 4 + kg));
+          c0[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, yh, c0[t], 0, 0, 0);
+          c1[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, yh, c1[t], 0, 0, 0);
+          c2[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, yl, c2[t], 0, 0, 0);
+        }
+      }
+      ALT_ST(5);  // MFMAs
+      __syncthreads();  // every MFMA wave has read the band: its region takes S
+      ALT_ST(6);
+      // register r of block t holds S[query 16 rb + 4 kg + r][band pixel 48 cg + 16 t + rl]
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          S[(16 * rb + 4 * kg + r) * AM_SLD + 48 * cg + 16 * t + rl] = c0[t][r] + c1[t][r] + c2[t][r];
+#else
       f32x16 acc = {}, acc2 = {}, acc3 = {};
       if (g < 6) {
         for (int s = 0; s < ks; ++s) {
@@ -686,6 +721,7 @@ __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevel
         for (int r = 0; r < 16; ++r)
           S[(32 * mi + (r & 3) + 8 * (r >> 2) + 4 * h) * AM_SLD + 32 * ni + m] = acc[r] + acc2[r] + acc3[r];
       }
+#endif
       ALT_ST(7);  // S stores
       __syncthreads();
       ALT_ST(8);
