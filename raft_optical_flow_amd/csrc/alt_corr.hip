@@ -425,6 +425,9 @@ __global__ __launch_bounds__(256) void alt_corr_tile_kernel(AltArgs a) {
 //   per CU; 8 waves load, waves 0-5 own one 32x32 S subtile each, all 8 pick taps.
 // The next band's fmap2 loads are issued before the current band's MFMAs.
 // ============================================================================
+#ifndef ALT_MFMA16
+#define ALT_MFMA16 1  // the box GEMM on 8 waves of 16x16 blocks (0: 6 waves of 32x32 blocks)
+#endif
 constexpr int AM_KS = 8;                 // 32-channel K-steps (C <= 256)
 constexpr int AM_ROW = 128;              // bytes per (row, K-step): 32 hi | 32 lo halves, 16-B chunks
                                          // XOR-swizzled by row & 7 (conflict-free fragment reads)
@@ -547,8 +550,10 @@ __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevel
     }
   }
   ALT_ST(0);  // F1 tile
+#if !ALT_MFMA16
   const int mi = g & 1, ni = g >> 1;  // S subtile of MFMA waves 0-5
   const int m = lane & 31, h = lane >> 5;
+#endif
   // ---- per-level window box (wave-uniform) and the band loads, set up one level ahead ------
   struct Lvl {
     float x, y;       // this lane's query at the level
@@ -609,7 +614,14 @@ __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevel
 #pragma unroll
     for (int k = 0; k < AM_PER; ++k) {
       const int j = g + 8 * k, s = lane >> 3;
+#ifdef ALT_ABL_NOSPLIT  // dev ablation (wrong results): the band stored as loaded, one 16-B write per load
+      if (s < ks) {
+        const int row = s * AM_NB + j;
+        *reinterpret_cast<f32x4*>(Bs + row * AM_ROW + am_chunk(row, lane & 7)) = bv[k];
+      }
+#else
       if (s < ks) am_split_store(Bs, s * AM_NB + j, lane & 7, bv[k]);
+#endif
     }
   };
   Lvl cur;
@@ -658,9 +670,6 @@ __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevel
       ALT_ST(3);
       if (r0 + cur.br < cur.bh) load_band(l, cur, r0 + cur.br);  // in flight under the MFMAs
       ALT_ST(4);
-#ifndef ALT_MFMA16
-#define ALT_MFMA16 1
-#endif
 #if ALT_MFMA16
       // all 8 waves on 16x16 blocks: wave g owns query rows 16 (g & 3) .. +15 and band pixels
       // 48 (g >> 2) .. +47 (three 16x16 blocks), so each SIMD carries two waves' equal share
