@@ -426,7 +426,7 @@ __global__ __launch_bounds__(256) void alt_corr_tile_kernel(AltArgs a) {
 // The next band's fmap2 loads are issued before the current band's MFMAs.
 // ============================================================================
 #ifndef ALT_MFMA16
-#define ALT_MFMA16 1  // the box GEMM on 8 waves of 16x16 blocks (0: 6 waves of 32x32 blocks)
+#define ALT_MFMA16 1  // the box GEMM on 16x16 blocks: 1 = 8 waves, 2 = 4 waves of 32 rows (0: 6 waves of 32x32 blocks)
 #endif
 constexpr int AM_KS = 8;                 // 32-channel K-steps (C <= 256)
 constexpr int AM_ROW = 128;              // bytes per (row, K-step): 32 hi | 32 lo halves, 16-B chunks
@@ -671,36 +671,54 @@ __global__ __launch_bounds__(512) void alt_corr_mfma_kernel(AltArgs a0, AltLevel
       if (r0 + cur.br < cur.bh) load_band(l, cur, r0 + cur.br);  // in flight under the MFMAs
       ALT_ST(4);
 #if ALT_MFMA16
-      // all 8 waves on 16x16 blocks: wave g owns query rows 16 (g & 3) .. +15 and band pixels
-      // 48 (g >> 2) .. +47 (three 16x16 blocks), so each SIMD carries two waves' equal share
-      // (the 32x32 form ran on waves 0-5: SIMDs 0 and 1 did two waves' MFMAs, SIMDs 2 and 3 one)
-      f32x4 c0[3] = {}, c1[3] = {}, c2[3] = {};
-      const int rb = g & 3, cg = g >> 2, rl = lane & 15, kg = lane >> 4;
-      for (int s = 0; s < ks; ++s) {
-        const int ar = s * (AT * AT) + 16 * rb + rl;
-        const char* Ar = As + ar * AM_ROW;
-        const h8 xh = *reinterpret_cast<const h8*>(Ar + am_chunk(ar, kg));
-        const h8 xl = *reinterpret_cast<const h8*>(Ar + am_chunk(ar, 4 + kg));
+      // the band product on 16x16 blocks, every SIMD the same share.  ALT_MFMA16 == 1: all 8 waves,
+      // wave g owns query rows 16 (g & 3) .. +15 x band pixels 48 (g >> 2) .. +47 (RB = 1 row block
+      // of 3 column blocks); == 2: waves 0-3 (one per SIMD), wave g query rows 32 (g & 1) .. +31 x
+      // band pixels 48 (g >> 1) .. +47 (RB = 2): the same MFMA cycles per SIMD from 37 % fewer LDS
+      // fragment bytes (the 32x32 form ran on waves 0-5: SIMDs 0 and 1 carried two waves' MFMAs)
+      constexpr int RB = ALT_MFMA16 == 2 ? 2 : 1;
+      f32x4 c0[RB][3] = {}, c1[RB][3] = {}, c2[RB][3] = {};
+      const int rb = RB == 2 ? (g & 1) : (g & 3), cg = RB == 2 ? (g >> 1) : (g >> 2);
+      const int rl = lane & 15, kg = lane >> 4;
+      if (RB == 1 || g < 4) {
+        for (int s = 0; s < ks; ++s) {
+          h8 xh[RB], xl[RB];
 #pragma unroll
-        for (int t = 0; t < 3; ++t) {
-          const int brow = s * AM_NB + 48 * cg + 16 * t + rl;
-          const char* Br = Bs + brow * AM_ROW;
-          const h8 yh = *reinterpret_cast<const h8*>(Br + am_chunk(brow, kg));
-          const h8 yl = *reinterpret_cast<const h8*>(Br + am_chunk(brow, 4 + kg));
-          c0[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, yh, c0[t], 0, 0, 0);
-          c1[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, yh, c1[t], 0, 0, 0);
-          c2[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, yl, c2[t], 0, 0, 0);
+          for (int i = 0; i < RB; ++i) {
+            const int ar = s * (AT * AT) + 16 * (RB * rb + i) + rl;
+            const char* Ar = As + ar * AM_ROW;
+            xh[i] = *reinterpret_cast<const h8*>(Ar + am_chunk(ar, kg));
+            xl[i] = *reinterpret_cast<const h8*>(Ar + am_chunk(ar, 4 + kg));
+          }
+#pragma unroll
+          for (int t = 0; t < 3; ++t) {
+            const int brow = s * AM_NB + 48 * cg + 16 * t + rl;
+            const char* Br = Bs + brow * AM_ROW;
+            const h8 yh = *reinterpret_cast<const h8*>(Br + am_chunk(brow, kg));
+            const h8 yl = *reinterpret_cast<const h8*>(Br + am_chunk(brow, 4 + kg));
+#pragma unroll
+            for (int i = 0; i < RB; ++i) {
+              c0[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh[i], yh, c0[i][t], 0, 0, 0);
+              c1[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl[i], yh, c1[i][t], 0, 0, 0);
+              c2[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh[i], yl, c2[i][t], 0, 0, 0);
+            }
+          }
         }
       }
       ALT_ST(5);  // MFMAs
       __syncthreads();  // every MFMA wave has read the band: its region takes S
       ALT_ST(6);
-      // register r of block t holds S[query 16 rb + 4 kg + r][band pixel 48 cg + 16 t + rl]
+      // register r of block (i, t) holds S[query 16 (RB rb + i) + 4 kg + r][band pixel 48 cg + 16 t + rl]
+      if (RB == 1 || g < 4) {
 #pragma unroll
-      for (int t = 0; t < 3; ++t)
+        for (int i = 0; i < RB; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          S[(16 * rb + 4 * kg + r) * AM_SLD + 48 * cg + 16 * t + rl] = c0[t][r] + c1[t][r] + c2[t][r];
+          for (int t = 0; t < 3; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              S[(16 * (RB * rb + i) + 4 * kg + r) * AM_SLD + 48 * cg + 16 * t + rl] =
+                  c0[i][t][r] + c1[i][t][r] + c2[i][t][r];
+      }
 #else
       f32x16 acc = {}, acc2 = {}, acc3 = {};
       if (g < 6) {
