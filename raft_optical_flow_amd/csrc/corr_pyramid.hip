@@ -437,7 +437,7 @@ struct CB4Args {
   int H, W, P, nh;  // nh = C / 16 half-steps
   float sqrt_c;
   float* pyr;
-  Level l0, l1;
+  Level l0, l1, l2;
   int nt;
   int qt, ttx, tt;  // query tiles per image; target tiles along w2; target tiles per image
   long units;       // B * qt * tt
@@ -484,15 +484,19 @@ __device__ __forceinline__ unsigned long long cb4_clock() {
 #define CB4_ST(k)
 #endif
 
-template <bool L1>
+// L2 (round 5): level 2 from registers too.  A level-2 cell is 4x4 level-0 pixels, i.e. exactly the
+// lane's level-0 tile: avg_pool2d of the lane's four level-1 values in pool2_tiled_kernel's order (the
+// same fp32 values it would read back), so the level-1 re-read pass (config 5: 1.05 GB) goes away.
+template <bool L1, bool L2 = false>
 __global__ __launch_bounds__(512) void corr_build4_kernel(CB4Args a) {
+  static_assert(L1 || !L2, "level 2 pools level 1");
 #ifdef CB4_STAMPS
   unsigned long long cb4_t[6] = {}, cb4_prev = cb4_clock();
   const unsigned long long cb4_start = cb4_prev;
   int cb4_units = 0;
 #endif
   // store instructions of one epilogue per wave: 2 x 4 blocks x (4 level-0 + 1 level-1 row)
-  constexpr int NSTORE = 8 * (4 + (L1 ? 1 : 0));
+  constexpr int NSTORE = 8 * (4 + (L1 ? 1 : 0)) + (L2 ? 4 : 0);
   __shared__ __attribute__((aligned(1024))) char smem[CB4_NS * CB4_STAGE];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -620,6 +624,7 @@ __global__ __launch_bounds__(512) void corr_build4_kernel(CB4Args a) {
       const int p1 = t.q0 + wn * 128 + j * 32 + m;
       const bool qok = p1 < a.P;
       const long qb = (long)t.b * a.P + (qok ? p1 : 0);
+      float l2v[2];  // L2: the level-2 cells (ty, t.tx0 / 4 + 2c + h)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int tx = t.tx0 / 4 + 2 * c + h;
@@ -676,7 +681,25 @@ __global__ __launch_bounds__(512) void corr_build4_kernel(CB4Args a) {
             __builtin_nontemporal_store(row4, dst);
           else
             *dst = row4;
+          if constexpr (L2) {
+            const bool in2 = ty < a.l2.h && tx < a.l2.w;
+            l2v[c] = in2 ? (((pv[0][0] + pv[0][1]) + pv[1][0]) + pv[1][1]) / 4.0f : 0.f;
+          }
         }
+      }
+      if constexpr (L2) {
+        // level-2 tile (ty0 / 16, tx0 / 16), row wm: columns 2c + h; lane h = 0 stores the row
+        const float o0 = __shfl_xor(l2v[0], 32), o1 = __shfl_xor(l2v[1], 32);
+        const int ty2 = t.ty0 >> 4, tx2 = t.tx0 >> 4;
+        const bool ok = qok && h == 0 && ty2 < a.l2.th && tx2 < a.l2.tw;
+        f32x4* dst = ok ? reinterpret_cast<f32x4*>(a.pyr + a.l2.off + qb * a.l2.mapsz + ((long)ty2 * a.l2.tw + tx2) * 16 +
+                                                   wm * 4)
+                        : a.sink + 4 * lane;
+        const f32x4 row4 = {l2v[0], o0, l2v[1], o1};
+        if (a.nt)
+          __builtin_nontemporal_store(row4, dst);
+        else
+          *dst = row4;
       }
     }
 #pragma unroll
@@ -1387,6 +1410,13 @@ extern "C" int raft_corr_build_ws(const float* fmap1, const float* fmap2, int ld
   a.pyr = pyramid;
   a.l0 = lv[0];
   a.l1 = lv[L > 1 ? 1 : 0];
+  a.l2 = lv[L > 2 ? 2 : 0];
+  // level 2 from the build's registers (RAFT_CB4_L2=0: from level 1 by pool2_tiled_kernel, the same bytes)
+  static const bool l2_on = [] {
+    const char* e = getenv("RAFT_CB4_L2");
+    return !(e && e[0] == '0');
+  }();
+  const bool l2 = l2_on && L > 2;
   {
     const char* e = getenv("RAFT_CORR_NT");
     const double l0_bytes = 4.0 * B * (double)P * lv[0].mapsz;
@@ -1402,13 +1432,15 @@ extern "C" int raft_corr_build_ws(const float* fmap1, const float* fmap2, int ld
       cus <= 0)
     cus = 256;
   const dim3 grid((unsigned)(a.units < cus ? a.units : cus));  // one work-group per CU (128 KiB LDS), persistent
-  if (L > 1)
+  if (l2)
+    hipLaunchKernelGGL((corr_build4_kernel<true, true>), grid, dim3(512), 0, s, a);
+  else if (L > 1)
     hipLaunchKernelGGL(corr_build4_kernel<true>, grid, dim3(512), 0, s, a);
   else
     hipLaunchKernelGGL(corr_build4_kernel<false>, grid, dim3(512), 0, s, a);
   rc = check_launch("raft_corr_build_ws");
   if (rc) return rc;
-  for (int l = 2; l < L; ++l) {
+  for (int l = l2 ? 3 : 2; l < L; ++l) {
     const long n = (long)B * P * lv[l].mapsz;
     hipLaunchKernelGGL(pool2_tiled_kernel, dim3(grid_for(n)), dim3(256), 0, s, pyramid, pyramid, (long)B * P, lv[l - 1],
                        lv[l]);

@@ -92,6 +92,13 @@ def test_corr_build_ws_vs_fp64(B, H, W, C, L, ld):
         a = l0[:, 0:2 * h1:2, 0:2 * w1:2] + l0[:, 0:2 * h1:2, 1:2 * w1:2]
         a = (a + l0[:, 1:2 * h1:2, 0:2 * w1:2]) + l0[:, 1:2 * h1:2, 1:2 * w1:2]
         assert torch.equal(levels[1], a / 4.0)
+    if L > 2:
+        # level 2 (pooled in the build's registers since round 5): the exact avg_pool2d of level 1
+        l1 = levels[1]
+        h2, w2 = dims[2]
+        a = l1[:, 0:2 * h2:2, 0:2 * w2:2] + l1[:, 0:2 * h2:2, 1:2 * w2:2]
+        a = (a + l1[:, 1:2 * h2:2, 0:2 * w2:2]) + l1[:, 1:2 * h2:2, 1:2 * w2:2]
+        assert torch.equal(levels[2], a / 4.0)
 
 
 def test_corr_build_ws_matches_the_plain_build():
