@@ -487,9 +487,22 @@ __device__ __forceinline__ unsigned long long cb4_clock() {
 // L2 (round 5): level 2 from registers too.  A level-2 cell is 4x4 level-0 pixels, i.e. exactly the
 // lane's level-0 tile: avg_pool2d of the lane's four level-1 values in pool2_tiled_kernel's order (the
 // same fp32 values it would read back), so the level-1 re-read pass (config 5: 1.05 GB) goes away.
-template <bool L1, bool L2 = false>
-__global__ __launch_bounds__(512) void corr_build4_kernel(CB4Args a) {
+// NW (round 5): 8 waves per work-group, one per CU (units of 256 targets x 256 queries, 4 stages of
+// 32 KiB), or 4 waves (units of 256 targets x 128 queries, 3 stages of 24 KiB) with TWO work-groups per
+// CU, so that one work-group's epilogue stores run under the other's MFMAs (with one work-group per
+// CU its 8 waves store in lock-step and the MFMA pipe idles: stamps, the epilogue ~60 % of a wave).
+// Measured (r05p) the 4-wave form pays only at one-round maps; it is an opt-in (RAFT_CB4_W4=1).
+template <bool L1, bool L2 = false, int NW = 8>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void corr_build4_kernel(CB4Args a) {
   static_assert(L1 || !L2, "level 2 pools level 1");
+  static_assert(NW == 8 || NW == 4, "8 or 4 waves");
+  constexpr int TQ = NW == 8 ? CB4_T : CB4_T / 2;  // queries per unit
+  constexpr int ROWS = CB4_T + TQ;                  // LDS rows of one half-step (targets | queries)
+  constexpr int NS = NW == 8 ? CB4_NS : 3;          // stages
+  constexpr int AHEAD = NS - 1;                     // half-steps in flight ahead of the one read
+  constexpr int STAGE = ROWS * CB4_ROW;
+  constexpr int NDMA = ROWS / 16 / NW;              // 1-KiB DMAs per wave and half-step
+  constexpr int TDMA = 16 / NW;                     // ... of which target rows (k < TDMA)
 #ifdef CB4_STAMPS
   unsigned long long cb4_t[6] = {}, cb4_prev = cb4_clock();
   const unsigned long long cb4_start = cb4_prev;
@@ -497,10 +510,10 @@ __global__ __launch_bounds__(512) void corr_build4_kernel(CB4Args a) {
 #endif
   // store instructions of one epilogue per wave: 2 x 4 blocks x (4 level-0 + 1 level-1 row)
   constexpr int NSTORE = 8 * (4 + (L1 ? 1 : 0)) + (L2 ? 4 : 0);
-  __shared__ __attribute__((aligned(1024))) char smem[CB4_NS * CB4_STAGE];
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = w & 3, wn = w >> 2;
+  const int wm = w & 3, wn = NW == 8 ? w >> 2 : 0;
   const int m = lane & 31, h = lane >> 5;
   const long grid = gridDim.x;
   const unsigned rowb = (unsigned)a.nh * CB4_ROW;  // bytes per pixel row of a split map
@@ -514,22 +527,22 @@ __global__ __launch_bounds__(512) void corr_build4_kernel(CB4Args a) {
     t.b = (int)(u / per);
     const long r = u - (long)t.b * per;
     const int qi = (int)(r / a.tt), ti = (int)(r - (long)qi * a.tt);
-    t.q0 = qi * CB4_T;
+    t.q0 = qi * TQ;
     t.ty0 = (ti / a.ttx) * 16;
     t.tx0 = (ti % a.ttx) * 16;
     return t;
   };
-  // DMA k (0..3) of this wave per half-step: instruction i = w + 8k moves LDS rows 16i .. 16i+15
-  // (rows 0..255 targets, 256..511 queries); lane: row 16i + lane/4, physical quad lane & 3
-  unsigned voff[4];
+  // DMA k (0..NDMA-1) of this wave per half-step: instruction i = w + NW k moves LDS rows 16i .. 16i+15
+  // (rows 0..255 targets, 256.. queries); lane: row 16i + lane/4, physical quad lane & 3
+  unsigned voff[NDMA];
   auto set_offsets = [&](const Unit& t) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int row = 16 * (w + 8 * k) + (lane >> 2);
+    for (int k = 0; k < NDMA; ++k) {
+      const int row = 16 * (w + NW * k) + (lane >> 2);
       const unsigned lq = (unsigned)((lane & 3) ^ ((row >> 1) & 3));
       bool ok;
       long px;
-      if (k < 2) {  // target row R = 64 wm' + 32 c + m'
+      if (k < TDMA) {  // target row R = 64 wm' + 32 c + m'
         const int R = row, mm = R & 31, c = (R >> 5) & 1;
         const int h2 = t.ty0 + 4 * (R >> 6) + (mm >> 3), w2 = t.tx0 + 8 * c + 4 * ((mm >> 2) & 1) + (mm & 3);
         ok = h2 < a.H && w2 < a.W;
@@ -550,10 +563,10 @@ __global__ __launch_bounds__(512) void corr_build4_kernel(CB4Args a) {
   set_offsets(unit_at(u_is));
   auto issue = [&]() {  // the next half-step's DMAs (zeros past the last unit)
     const bool live = u_is < total;
-    char* st = smem + (g_is % CB4_NS) * CB4_STAGE;
+    char* st = smem + (g_is % NS) * STAGE;
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      dma16(k < 2 ? rt : rq, st + (w + 8 * k) * 1024, live ? voff[k] : OFF_INVALID, (unsigned)s_is * CB4_ROW);
+    for (int k = 0; k < NDMA; ++k)
+      dma16(k < TDMA ? rt : rq, st + (w + NW * k) * 1024, live ? voff[k] : OFF_INVALID, (unsigned)s_is * CB4_ROW);
     ++g_is;
     if (++s_is == a.nh) {
       s_is = 0;
@@ -561,9 +574,8 @@ __global__ __launch_bounds__(512) void corr_build4_kernel(CB4Args a) {
       if (u_is < total) set_offsets(unit_at(u_is));
     }
   };
-  issue();
-  issue();
-  issue();
+#pragma unroll
+  for (int k = 0; k < AHEAD; ++k) issue();
   const int arow0 = wm * 64 + m, brow0 = CB4_T + wn * 128 + m;
   f32x16 acc[2][4];
 #pragma unroll
@@ -571,24 +583,24 @@ __global__ __launch_bounds__(512) void corr_build4_kernel(CB4Args a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[c][j] = f32x16{};
   long g = 0;
-  int since = 3;  // half-steps since the last epilogue (3: none in flight)
+  int since = AHEAD;  // half-steps since the last epilogue (AHEAD: none in flight)
   for (long u = blockIdx.x; u < total; u += grid) {
     for (int s = 0; s < a.nh; ++s, ++g, ++since) {
       // this wave's DMAs of half-step g (those of the two younger half-steps may fly; in the three
       // half-steps after an epilogue its NSTORE stores, younger than g's DMAs, may fly too)
       CB4_ST(5);  // loop overhead
-      if (since <= 2)
-        wait_vm<8 + NSTORE>();
+      if (since <= AHEAD - 1)
+        wait_vm<NDMA * (AHEAD - 1) + NSTORE>();
       else
-        wait_vm<8>();
+        wait_vm<NDMA * (AHEAD - 1)>();
       CB4_ST(0);  // DMA wait
-      // every wave's: stage g % 4 readable, stage (g - 1) % 4 free (the asm's memory clobber keeps
+      // every wave's: stage g % NS readable, stage (g - 1) % NS free (the asm's memory clobber keeps
       // the compiler from moving this step's LDS reads above the barrier)
       asm volatile("s_barrier" ::: "memory");
       CB4_ST(1);  // barrier
-      issue();  // half-step g + 3
+      issue();  // half-step g + AHEAD
       CB4_ST(2);  // DMA issue
-      const char* st = smem + (g % CB4_NS) * CB4_STAGE;
+      const char* st = smem + (g % NS) * STAGE;
       h8 ah[2], al[2], bh[4], bl[4];
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
@@ -1422,7 +1434,14 @@ extern "C" int raft_corr_build_ws(const float* fmap1, const float* fmap2, int ld
     const double l0_bytes = 4.0 * B * (double)P * lv[0].mapsz;
     a.nt = e && (e[0] == '0' || e[0] == '1') ? e[0] == '1' : l0_bytes > 512.0 * 1024 * 1024;
   }
-  a.qt = (int)cdiv_l(P, CB4_T);
+  // RAFT_CB4_W4=1: 4-wave work-groups, two per CU (r05p: config 2's map 156 -> 142 us alone, config 4's
+  // 1.50 -> 1.54 ms, config 5's 2.47 -> 2.80 ms: the half-size units move 1.5x the operand bytes per
+  // flop; the forward unchanged at config 2, 1.5 % slower at config 5), default: 8 waves, one per CU
+  static const bool w4 = [] {
+    const char* e = getenv("RAFT_CB4_W4");
+    return e && e[0] == '1';
+  }();
+  a.qt = (int)cdiv_l(P, w4 ? CB4_T / 2 : CB4_T);
   a.ttx = cdiv(W, 16);
   a.tt = cdiv(H, 16) * a.ttx;
   a.units = (long)B * a.qt * a.tt;
@@ -1431,13 +1450,23 @@ extern "C" int raft_corr_build_ws(const float* fmap1, const float* fmap2, int ld
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       cus <= 0)
     cus = 256;
-  const dim3 grid((unsigned)(a.units < cus ? a.units : cus));  // one work-group per CU (128 KiB LDS), persistent
-  if (l2)
+  // persistent: one 8-wave work-group per CU (128 KiB LDS) or two 4-wave ones (72 KiB each)
+  const long wgs = w4 ? 2L * cus : (long)cus;
+  const dim3 grid((unsigned)(a.units < wgs ? a.units : wgs));
+  if (w4) {
+    if (l2)
+      hipLaunchKernelGGL((corr_build4_kernel<true, true, 4>), grid, dim3(256), 0, s, a);
+    else if (L > 1)
+      hipLaunchKernelGGL((corr_build4_kernel<true, false, 4>), grid, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((corr_build4_kernel<false, false, 4>), grid, dim3(256), 0, s, a);
+  } else if (l2) {
     hipLaunchKernelGGL((corr_build4_kernel<true, true>), grid, dim3(512), 0, s, a);
-  else if (L > 1)
+  } else if (L > 1) {
     hipLaunchKernelGGL(corr_build4_kernel<true>, grid, dim3(512), 0, s, a);
-  else
+  } else {
     hipLaunchKernelGGL(corr_build4_kernel<false>, grid, dim3(512), 0, s, a);
+  }
   rc = check_launch("raft_corr_build_ws");
   if (rc) return rc;
   for (int l = l2 ? 3 : 2; l < L; ++l) {
