@@ -255,6 +255,61 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
       lano[l] = __umul24((unsigned)ti, (unsigned)(64 * ltw[l])) + 16u * (unsigned)(lane & 15);
       lmsz4[l] = lmsz[l] * 4u;
     }
+#ifndef LC_TAB
+#define LC_TAB 1
+#endif
+#if LC_TAB
+    // The 16 (pixel, level) windows' parameters computed once, window (k, l) on lane 4k + l, on the VALU,
+    // and read back per load (3 v_readlane): the window's origin offset and its row / tile-column
+    // intervals clipped to the map (relative to the lane's row / column in the window, 16 + 16 bits).
+    // The per-load scalar chain (~19 SALU on the unit the CU's 8 waves share) becomes ~4.
+    int t_sb, t_row, t_col;
+    {
+      const int ik = (lane >> 2) & 3, il = lane & 3;
+      float fx = px_x[0], fy = px_y[0];
+      int gpk = px_gp[0];
+      bool okk = px_ok[0];
+#pragma unroll
+      for (int k = 1; k < LC_PX; ++k) {
+        fx = ik == k ? px_x[k] : fx;
+        fy = ik == k ? px_y[k] : fy;
+        gpk = ik == k ? px_gp[k] : gpk;
+        okk = ik == k ? px_ok[k] : okk;
+      }
+      int thl = lth[0], twl = ltw[0];
+      unsigned msl = lmsz4[0];
+#pragma unroll
+      for (int l = 1; l < LC_L; ++l) {
+        thl = il == l ? lth[l] : thl;
+        twl = il == l ? ltw[l] : twl;
+        msl = il == l ? lmsz4[l] : msl;
+      }
+      const int wx0 = ((int)floorf(fx) >> il) - R, wy0 = ((int)floorf(fy) >> il) - R;
+      const int tyo = wy0 >> 2, txo = wx0 >> 2;
+      const int ntx = ((wx0 + WD - 1) >> 2) - txo + 1;
+      const int rlo = max(wy0, 0), rhi = min(wy0 + WD, 4 * thl);
+      const int clo = max(txo, 0), chi = min(txo + ntx, twl);
+      const int rn = okk ? max(rhi - rlo, 0) : 0, cn = max(chi - clo, 0);
+      t_sb = (int)((unsigned)gpk * msl + (unsigned)(tyo * twl + txo) * 64u);
+      t_row = ((rlo - 4 * tyo) & 0xFFFF) | (rn << 16);
+      t_col = ((clo - txo) & 0xFFFF) | (cn << 16);
+    }
+#pragma unroll
+    for (int k = 0; k < LC_PX; ++k) {
+#pragma unroll
+      for (int l = 0; l < LC_L; ++l) {
+        const unsigned sb = (unsigned)__builtin_amdgcn_readlane(t_sb, 4 * k + l);
+        const int rp = __builtin_amdgcn_readlane(t_row, 4 * k + l), cp = __builtin_amdgcn_readlane(t_col, 4 * k + l);
+        // inside the window and the map (rows [rlo, rhi), tile columns [clo, chi)), or no access
+        const bool tok = ((unsigned)(lrow - (rp & 0xFFFF)) < (unsigned)(rp >> 16)) &
+                         ((unsigned)(tj - (cp & 0xFFFF)) < (unsigned)(cp >> 16));
+        unsigned offv = sb + lano[l];
+        asm volatile("" : "+v"(offv));  // (computed for every lane: a select, not a branch around it)
+        const unsigned off = tok ? offv : 0x80000000u;
+        v[k][l] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsl[l], off, 0, 0));
+      }
+    }
+#else
 #pragma unroll
     for (int k = 0; k < LC_PX; ++k) {
       const unsigned gp = (unsigned)px_gp[k];
@@ -277,6 +332,7 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
         v[k][l] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsl[l], off, 0, 0));
       }
     }
+#endif
   } else {
 #pragma unroll
   for (int k = 0; k < LC_PX; ++k) {
