@@ -241,6 +241,9 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
 #ifndef LC_OFF32
 #define LC_OFF32 1
 #endif
+#ifndef LC_TAB
+#define LC_TAB 1
+#endif
   bool off32 = LC_OFF32 != 0;
   const unsigned nmaps = (unsigned)(a.B * P);
 #pragma unroll
@@ -255,9 +258,6 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
       lano[l] = __umul24((unsigned)ti, (unsigned)(64 * ltw[l])) + 16u * (unsigned)(lane & 15);
       lmsz4[l] = lmsz[l] * 4u;
     }
-#ifndef LC_TAB
-#define LC_TAB 1
-#endif
 #if LC_TAB
     // The 16 (pixel, level) windows' parameters computed once, window (k, l) on lane 4k + l, on the VALU,
     // and read back per load (3 v_readlane): the window's origin offset and its row / tile-column
@@ -334,6 +334,65 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
     }
 #endif
   } else {
+#if LC_TAB
+    // (pyramids past 2^31 bytes per level, e.g. config 5: 4.2 GB of level 0) the same table with each
+    // window's 64-bit base address instead of the 32-bit offset (4 v_readlane per load, a resource per
+    // window as before)
+    int t_lo, t_hi, t_row, t_col;
+    {
+      const int ik = (lane >> 2) & 3, il = lane & 3;
+      float fx = px_x[0], fy = px_y[0];
+      int gpk = px_gp[0];
+      bool okk = px_ok[0];
+#pragma unroll
+      for (int k = 1; k < LC_PX; ++k) {
+        fx = ik == k ? px_x[k] : fx;
+        fy = ik == k ? px_y[k] : fy;
+        gpk = ik == k ? px_gp[k] : gpk;
+        okk = ik == k ? px_ok[k] : okk;
+      }
+      int thl = lth[0], twl = ltw[0];
+      unsigned msl = lmsz[0];
+      const float* bsl = lbs[0];
+#pragma unroll
+      for (int l = 1; l < LC_L; ++l) {
+        thl = il == l ? lth[l] : thl;
+        twl = il == l ? ltw[l] : twl;
+        msl = il == l ? lmsz[l] : msl;
+        bsl = il == l ? lbs[l] : bsl;
+      }
+      const int wx0 = ((int)floorf(fx) >> il) - R, wy0 = ((int)floorf(fy) >> il) - R;
+      const int tyo = wy0 >> 2, txo = wx0 >> 2;
+      const int ntx = ((wx0 + WD - 1) >> 2) - txo + 1;
+      const int rlo = max(wy0, 0), rhi = min(wy0 + WD, 4 * thl);
+      const int clo = max(txo, 0), chi = min(txo + ntx, twl);
+      const int rn = okk ? max(rhi - rlo, 0) : 0, cn = max(chi - clo, 0);
+      const float* wbase = bsl + (long)((unsigned long long)(unsigned)gpk * msl) + ((long)tyo * twl + txo) * 16;
+      const unsigned long long wa = reinterpret_cast<unsigned long long>(wbase);
+      t_lo = (int)(unsigned)wa;
+      t_hi = (int)(unsigned)(wa >> 32);
+      t_row = ((rlo - 4 * tyo) & 0xFFFF) | (rn << 16);
+      t_col = ((clo - txo) & 0xFFFF) | (cn << 16);
+    }
+#pragma unroll
+    for (int k = 0; k < LC_PX; ++k) {
+#pragma unroll
+      for (int l = 0; l < LC_L; ++l) {
+        const unsigned lo = (unsigned)__builtin_amdgcn_readlane(t_lo, 4 * k + l);
+        const unsigned hi = (unsigned)__builtin_amdgcn_readlane(t_hi, 4 * k + l);
+        const int rp = __builtin_amdgcn_readlane(t_row, 4 * k + l), cp = __builtin_amdgcn_readlane(t_col, 4 * k + l);
+        const bool tok = ((unsigned)(lrow - (rp & 0xFFFF)) < (unsigned)(rp >> 16)) &
+                         ((unsigned)(tj - (cp & 0xFFFF)) < (unsigned)(cp >> 16));
+        const float* wbase = reinterpret_cast<const float*>(((unsigned long long)hi << 32) | lo);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wbase), (short)0, 0x7FFFFFFF, 0x00020000);
+        unsigned offv = __umul24((unsigned)ti, (unsigned)(64 * ltw[l])) + 16u * (unsigned)(lane & 15);
+        asm volatile("" : "+v"(offv));
+        const unsigned off = tok ? offv : 0x80000000u;
+        v[k][l] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      }
+    }
+#else
 #pragma unroll
   for (int k = 0; k < LC_PX; ++k) {
     const bool ok = px_ok[k];
@@ -359,6 +418,7 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
       v[k][l] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
     }
   }
+#endif
   }
   LC_STAMP(1);
   // ---- 2. while the tiles fly: the per-axis sampling entries of the four pixels ------------

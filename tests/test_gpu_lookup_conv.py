@@ -120,6 +120,20 @@ def test_lookup_conv_equals_lookup_then_convs(B, h, w, prec):
     assert d["flags"] == [0, 0, 0]
 
 
+@pytest.mark.parametrize("prec", ["f16x3", "bf16"])
+def test_lookup_conv_large_pyramid(prec):
+    """Config 5's 1/8-res grid (135 x 240): level 0 of the pyramid is 4.2 GB, past the 32-bit window
+    offsets, so the launch takes its 64-bit window bases (a buffer resource per window)."""
+    d = _case(1, 135, 240, prec, seed=11)
+    got = d["c1"][:, :256].cpu().double()
+    scale = float(d["ref"].abs().max())
+    assert float((got - d["ref"]).abs().max()) <= TOL[prec] * max(1.0, scale)
+    fscale = float(d["fref"].abs().max())
+    assert float((d["f1"][:, :128].cpu().double() - d["fref"]).abs().max()) <= TOL[prec] * max(1.0, fscale)
+    assert torch.equal(d["flow_a"], d["flow_b"])
+    assert d["flags"] == [0, 0, 0]
+
+
 def test_lookup_conv_far_out_of_bounds():
     """Coordinates spread far past the map (zero taps, windows off every level)."""
     d = _case(1, 19, 35, "f16x3", coord_sigma=40.0, seed=9)
