@@ -349,9 +349,10 @@ typedef struct raft_conv2d_params {
  * of its <= 32 output pixels (M2 = sum of squared deviations from that mean) as 4 floats at
  * stats_part[((slot * stats_ld) + n) * 4 ..], slot = image * slots_per_image + s, s <
  * slots_per_image; raft_instnorm_merge combines them (Chan's formula in double, fixed order).
- * Only for convs with the linear epilogue (alpha 1, no add0) that run on the halo or stem kernel:
- * raft_conv2d_stats_slots returns slots_per_image for such a conv and 0 otherwise (raft_conv2d
- * then rejects stats_part). */
+ * Only for convs with the linear epilogue (alpha 1, no add0) and more than 4 outputs (VEC) that run
+ * on the halo, stem or (since round 5: the strided encoder convs) 64x64-tile GEMM kernel, whose
+ * tiles then hold one image's rows each: raft_conv2d_stats_slots returns slots_per_image for such a
+ * conv and 0 otherwise (raft_conv2d then rejects stats_part). */
 int raft_conv2d_stats_slots(const raft_conv2d_params* p);
 /* Tile rows of the halo kernel's launch of this conv: 8 (128-pixel tiles), 16 (the multi-round
  * 256-pixel tiles), 0 when the halo kernel does not run it (inspection / tests). */

@@ -395,6 +395,8 @@ int conv_halo_launch_pair(const HaloOperands& o0, const HaloOperands& o1, hipStr
 int conv_stem_launch(const raft_conv2d_params& p, int k_pad, hipStream_t s);
 // tile-statistics slots per image of a conv on the halo / stem kernel (raft_conv2d_stats_slots), 0 if none
 int conv_halo_stats_slots(const HaloOperands& o);
+// whether conv_halo_launch takes the conv
+bool conv_halo_covers(const HaloOperands& o);
 int conv_halo_tile_rows(const HaloOperands& o);
 int conv_halo_tiles_per_wg(const HaloOperands& o);
 bool conv_halo_norm_ok(const HaloOperands& o);

@@ -63,6 +63,10 @@ struct ConvArgs {
   int taps;     // kh * kw
   int gn;       // N-tiles
   unsigned w_bytes, in0_bytes, in1_bytes;  // buffer-descriptor ranges
+  // InstanceNorm partials (p.stats_part, round 5): M tiled per image (tpi tiles of BM rows of one
+  // image's hw output pixels, the last one ragged) so that each wave's 32 rows lie in one image; each
+  // wave writes its (count, mean, M2) per column to slot 2 (image tile) + wm.  tpi = 0: M tiled flat
+  int tpi, hw;
 };
 
 // Per-thread staging state: two A rows (output pixels) of the tile.
@@ -131,8 +135,14 @@ __global__ __launch_bounds__(256 * KG, 4) void conv_gemm_kernel(ConvArgs a) {  /
   // 1-D grid of gm x gn tiles in XCD order, N fastest (an M-tile's N-tiles share its A rows)
   const int q = xcd_tile(blockIdx.x, gridDim.x);
   const int gn = a.gn;
-  const int m0 = (q / gn) * BM;
-  const int n0 = (q - (q / gn) * gn) * BN;
+  const int mt = q / gn;
+  const int n0 = (q - mt * gn) * BN;
+  int m0 = mt * BM, mlim = a.M;  // the tile's first row; rows from mlim on are outside it
+  if (a.tpi > 0) {
+    const int b = mt / a.tpi;
+    m0 = b * a.hw + (mt - b * a.tpi) * BM;
+    mlim = min(a.M, (b + 1) * a.hw);
+  }
   int* ktab = reinterpret_cast<int*>(smem + KG * 2 * STAGE);
   float* gsm = smem + g * 2 * STAGE;  // this group's two LDS buffers
 
@@ -152,7 +162,7 @@ __global__ __launch_bounds__(256 * KG, 4) void conv_gemm_kernel(ConvArgs a) {  /
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int m = m0 + lr + 32 * i;
-    w.pv[i] = m < a.M;
+    w.pv[i] = m < mlim;
     const int mm = w.pv[i] ? m : 0;
     const int ox = mm % p.out_w;
     const int t = mm / p.out_w;
@@ -470,8 +480,9 @@ __global__ __launch_bounds__(256 * KG, 4) void conv_gemm_kernel(ConvArgs a) {  /
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int m = (int)row_of(m0 + wm * 32 + 4 * (lane >> 5), r);
-    rows[r] = m < a.M ? m : -1;
+    rows[r] = m < mlim ? m : -1;
   }
+  if (p.stats_part) tile_stats(p, rows, n0 + wn * 32 + (lane & 31), acc, 2L * mt + wm);
   tile_epilogue(p, rows, n0 + wn * 32 + (lane & 31), acc);
 }
 
@@ -961,16 +972,18 @@ extern "C" int raft_conv2d(const raft_conv2d_params* pp, raft_stream_t stream) {
   }
   if (p.in_norm) RAFT_REQUIRE(raft_conv2d_in_norm_ok(pp), "raft_conv2d: in_norm needs a halo-kernel 3x3 conv");
   if (p.stats_part) {
-    // InstanceNorm partials come from the halo / stem epilogues only (raft_conv2d_stats_slots)
+    // InstanceNorm partials come from the halo / stem / GEMM epilogues (raft_conv2d_stats_slots)
     RAFT_REQUIRE(raft_conv2d_stats_slots(pp) > 0,
-                 "raft_conv2d: stats_part needs a linear-epilogue conv on the halo or stem kernel");
+                 "raft_conv2d: stats_part needs a linear-epilogue conv (raft_conv2d_stats_slots > 0)");
     RAFT_REQUIRE(p.stats_ld >= p.n && ((uintptr_t)p.stats_part & 15) == 0,
                  "raft_conv2d: stats_ld >= n and a 16-B aligned stats_part");
   }
   if (p.mode == RAFT_CONV_VEC && conv_halo_launch(o, s) == 0) return check_launch("raft_conv2d(halo)");
   if (p.mode == RAFT_CONV_GATHER && conv_stem_launch(p, o.k_pad, s) == 0) return check_launch("raft_conv2d(stem)");
   a.gn = n_pad / BN;
-  const long tiles = (long)cdiv(a.M, BM) * a.gn;
+  a.hw = p.out_h * p.out_w;
+  a.tpi = p.stats_part ? cdiv(a.hw, BM) : 0;
+  const long tiles = (p.stats_part ? (long)p.batch * a.tpi : (long)cdiv(a.M, BM)) * a.gn;
   RAFT_REQUIRE(tiles < (1L << 31), "raft_conv2d: too many tiles");
   dim3 grid((unsigned)tiles);
   // few tiles (fewer than ~4 per CU): two K-groups per tile give every SIMD two waves
@@ -1008,7 +1021,17 @@ extern "C" int raft_conv2d_stats_slots(const raft_conv2d_params* pp) {
   if (!pp || conv_prepare(pp, a, o)) return 0;
   const raft_conv2d_params& p = *pp;
   if (p.epilogue != RAFT_EPI_LINEAR || p.alpha != 1.0f || p.add0 || (p.n <= 4 && p.mode == RAFT_CONV_VEC)) return 0;
-  if (p.mode == RAFT_CONV_VEC) return conv_halo_stats_slots(o);
+  if (p.mode == RAFT_CONV_VEC) {
+    const int hs = conv_halo_stats_slots(o);
+    if (hs > 0 || conv_halo_covers(o)) return hs;
+    // the 64x64-tile GEMM (strided convs): two 32-row slots per tile of one image's rows
+    // (RAFT_GEMM_STATS=0: none, the separate statistics pass)
+    static const bool on = [] {
+      const char* e = getenv("RAFT_GEMM_STATS");
+      return !(e && e[0] == '0');
+    }();
+    return on ? 2 * cdiv(p.out_h * p.out_w, BM) : 0;
+  }
   return conv_stem_stats_slots(p, o.k_pad);
 }
 

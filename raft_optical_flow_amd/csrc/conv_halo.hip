@@ -1380,6 +1380,11 @@ int conv_halo_tile_rows(const HaloOperands& o) {
   return halo_pick(o, a, wide);
 }
 
+bool conv_halo_covers(const HaloOperands& o) {
+  HaloArgs a;
+  return halo_enabled() && halo_problem(o, a);
+}
+
 int conv_halo_stats_slots(const HaloOperands& o) {
   HaloArgs a;
   if (!halo_enabled() || !halo_problem(o, a)) return 0;

@@ -57,6 +57,10 @@ def make_model(small, seed=0, alternate=False, precision=None):
     dict(cin=96, cout=96, k=1, stride=1, pad=0, H=20, W=33, B=2, mode=None),   # halo 1x1
     dict(cin=3, cout=64, k=7, stride=2, pad=3, H=90, W=150, B=2, mode="gather"),  # the stem
     dict(cin=96, cout=96, k=3, stride=1, pad=1, H=110, W=256, B=2, mode=None),  # big tiles (fnet layer2)
+    # the 64x64-tile GEMM (round 5): strided convs, M tiled per image (513 rows: a ragged last tile)
+    dict(cin=64, cout=96, k=3, stride=2, pad=1, H=37, W=53, B=3, mode=None),
+    dict(cin=64, cout=96, k=1, stride=2, pad=0, H=37, W=53, B=3, mode=None),    # the downsample 1x1
+    dict(cin=96, cout=128, k=3, stride=2, pad=1, H=9, W=11, B=3, mode=None),    # 30 rows per image
 ])
 @pytest.mark.parametrize("prec", ["f16x3", "bf16"])
 def test_conv_epilogue_instnorm_stats(case, prec):
