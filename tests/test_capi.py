@@ -135,3 +135,38 @@ def test_halo_tiles_per_work_group_host_side():
     assert mt(256, 192, 3, 3, 8, 55, 128) == 1        # convc2 at B = 8: 3 rounds of big tiles beat 4 per work-group
     assert mt(256, 192, 3, 3, 1, 135, 240) == 3       # config 5's convc2: 255 spatial tiles x 3 N-tiles
     assert mt(128, 256, 3, 3, 8, 68, 120) == 9        # config 4's fh1: 576 spatial tiles x 4 N-tiles
+
+
+def test_stats_slots_host_side():
+    """InstanceNorm statistics slots per image (raft_conv2d_stats_slots: host logic only): 4 per
+    spatial tile on the halo kernel; on the 64x64-tile GEMM (the strided encoder convs, round 5) two
+    per 64-row tile of one image's output rows; none for a non-linear epilogue."""
+    import ctypes
+    import torch
+    from raft_optical_flow_amd import _lib
+    from raft_optical_flow_amd import kernels as K
+    lib = _lib.load()
+    fake = 1 << 20
+
+    def slots(cin, cout, k, stride, B, H, W, epilogue=None):
+        pad = (k - 1) // 2
+        pc = K.pack_conv(torch.zeros(cout, cin, k, k), None, stride, pad)
+        p = _lib.ConvParams()
+        p.in0, p.in0_ld, p.in0_c = fake, cin, cin
+        ho, wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+        p.batch, p.in_h, p.in_w, p.out_h, p.out_w = B, H, W, ho, wo
+        p.kh, p.kw, p.stride_h, p.stride_w, p.pad_h, p.pad_w = k, k, stride, stride, pad, pad
+        p.mode, p.weight, p.n, p.out, p.out_ld = pc.mode, fake, cout, fake, cout
+        p.precision = _lib.PRECISIONS["f16x3"]
+        p.alpha = 1.0
+        if epilogue is not None:
+            p.epilogue = epilogue
+        return lib.raft_conv2d_stats_slots(ctypes.byref(p)), ho * wo
+
+    s, hw = slots(64, 96, 3, 2, 2, 220, 512)           # fnet layer2's strided conv at config 2
+    assert s == 2 * ((hw + 63) // 64)
+    s, hw = slots(64, 96, 1, 2, 2, 220, 512)           # its 1x1 downsample
+    assert s == 2 * ((hw + 63) // 64)
+    s, hw = slots(96, 128, 3, 2, 3, 9, 11)             # 30 output rows per image: one tile each
+    assert s == 2
+    assert slots(64, 96, 3, 2, 2, 220, 512, epilogue=_lib.EPI_RELU)[0] == 0
