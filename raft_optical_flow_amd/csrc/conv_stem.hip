@@ -69,12 +69,36 @@ __global__ __launch_bounds__(256, 3) void conv_stem_kernel(StemArgs sa) {  // 3 
     const int iy0 = oy0 * ST_S - p.pad_h, ix0 = ox0 * ST_S - p.pad_w;
     __syncthreads();  // the previous tile's patch reads are done (and, first time, the staging above)
     // the input patch: row r = 37 pixels x 3 channels (zeros off the image)
+#ifndef STEM_PIX
+#define STEM_PIX 1
+#endif
+    if (STEM_PIX && ld == ST_C) {
+      // one pixel's 3 channels per thread and step (777 per tile: 3 pixels per thread instead of 9
+      // scalar loads with their index arithmetic), zeros off the image by an out-of-range offset
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(in), (short)0, (int)((unsigned)(p.batch * in_h * in_w) * 12u), 0x00020000);
+      for (int i = tid; i < ST_PH * ST_PW; i += 256) {
+        const int r = i / ST_PW, px = i - r * ST_PW;
+        const int yy = iy0 + r, xx = ix0 + px;
+        const bool ok = (unsigned)yy < (unsigned)in_h && (unsigned)xx < (unsigned)in_w;
+        const unsigned off = ok ? (unsigned)((b * in_h + yy) * in_w + xx) * 12u : 0x80000000u;
+        // (8 + 4 B: the 12-B buffer-load builtin came out as one dword, replicated, with this compiler)
+        const f32x2 v01 = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
+        const float v2 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 8, 0));
+        float* d = patch + r * ST_ROW + px * ST_C;
+        d[0] = v01[0];
+        d[1] = v01[1];
+        d[2] = v2;
+      }
+    } else
     for (int i = tid; i < ST_PATCH; i += 256) {
       const int r = i / ST_ROW, e = i - r * ST_ROW, px = e / ST_C, c = e - px * ST_C;
       const int yy = iy0 + r, xx = ix0 + px;
       float v = 0.f;
+#ifndef STEM_ABL_NOPATCH  // (dev ablation: no input loads, wrong results)
       if ((unsigned)yy < (unsigned)in_h && (unsigned)xx < (unsigned)in_w)
         v = in[((long)b * in_h * in_w + (long)yy * in_w + xx) * ld + c];
+#endif
       patch[i] = v;
     }
     __syncthreads();
@@ -141,7 +165,9 @@ __global__ __launch_bounds__(256, 3) void conv_stem_kernel(StemArgs sa) {  // 3 
         float v = acc[sb][r] + bias;
         v = relu ? fmaxf(v, 0.f) : v;
         big |= rows[r] >= 0 && fabsf(v) > RAFT_RANGE_LIMIT;
+#ifndef STEM_ABL_NOSTORE  // (dev ablation: no output stores, wrong results)
         if (rows[r] >= 0) p.out[(long)rows[r] * p.out_ld + n] = v;
+#endif
       }
       if (p.range_flag && big) *p.range_flag = 1;
       if (p.stats_part) tile_stats(p, rows, n, acc[sb], (long)tile * 4 + w);
