@@ -578,6 +578,18 @@ __global__ __launch_bounds__(512) void conv_smalln3x3_kernel(ConvArgs a, const f
   for (int i = 0; i < PXB; ++i)
 #pragma unroll
     for (int j = 0; j < NOUT; ++j) acc[i][j] = 0.f;
+  // ADD_TO_OUT (coords1 += delta_flow): the destination value loaded here, with the patch, not after
+  // the reduction (one memory round trip fewer on the kernel's path)
+#ifndef SN_PRE
+#define SN_PRE 1
+#endif
+  const bool pre_on = SN_PRE && p.epilogue == RAFT_EPI_ADD_TO_OUT && !p.add0;
+  const int ej = threadIdx.x >> 6;
+  const int ey = y0 + (lane >> 4), ex = x0 + (lane & 15);
+  const bool eok = threadIdx.x < 64 * NOUT && ej < p.n && lane < SN_TH * SN_TW && ey < p.out_h && ex < p.out_w;
+  const long em = ((long)b * p.out_h + ey) * p.out_w + ex;
+  float pre = 0.f;
+  if (pre_on && eok) pre = p.out[em * p.out_ld + ej];
   for (int cg = 32 * w; cg < a.ctot; cg += 256) {
     // weights of this lane's quad (zero-padded to cpad in the packed matrix)
     f32x4 wr[9][NOUT];
@@ -648,13 +660,17 @@ __global__ __launch_bounds__(512) void conv_smalln3x3_kernel(ConvArgs a, const f
   }
   __syncthreads();
   if (threadIdx.x < 64 * NOUT) {
-    const int j = threadIdx.x >> 6;
+    const int j = ej;
     float v = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) v += red[k][j][lane];
-    const int y = y0 + (lane >> 4), x = x0 + (lane & 15);
-    if (j < p.n && lane < SN_TH * SN_TW && y < p.out_h && x < p.out_w)
-      epilogue(p, ((long)b * p.out_h + y) * p.out_w + x, j, v + (p.bias ? p.bias[j] : 0.f));
+    if (eok) {
+      const float vb = v + (p.bias ? p.bias[j] : 0.f);
+      if (pre_on)
+        p.out[em * p.out_ld + j] = pre + vb;  // (epilogue's ADD_TO_OUT: *o + v)
+      else
+        epilogue(p, em, j, vb);
+    }
   }
 }
 
