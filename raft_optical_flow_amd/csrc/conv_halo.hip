@@ -81,13 +81,16 @@ struct HaloLaunch {
 // part of load set cT/U, issued during super-step cT/U - D (the prologue's
 // sets 0 .. D-1 count as issued before any read); K-step j >= 1 is read
 // during super-step (j-1)/U, K-step 0 before super-step 0 (-1).
-constexpr int patch_slots(int T, int U, int D) {
+// late = 1: a K-step's reads may still be in flight one super-step later (the compute waves' relaxed
+// barrier wait, halo_body RELAX: the look-ahead reads of the next super-step's first K-step are certified
+// at the barrier after it).
+constexpr int patch_slots(int T, int U, int D, int late = 0) {
   for (int pa = 1; pa < 16; ++pa) {
     bool ok = true;
     for (int c = pa; c < 512 && ok; ++c) {
       const int last = (c - pa) * T + T - 1;  // last K-step of the slot's previous chunk
       const int rd = last == 0 ? -1 : (last - 1) / U;
-      ok = (c * T) / U - D > rd;
+      ok = (c * T) / U - D > rd + late;
     }
     if (ok) return pa;
   }
@@ -184,7 +187,10 @@ constexpr int halo_norm_bytes(int LDS_B, int LDS_A, int D) {
 // slower in the forward).
 // NL: loader waves (4, or 8 for the one-tile f16x3 update convs: RAFT_HALO_NL8, a 768-thread
 // work-group whose loaders each issue half the weight DMAs and stage half of each patch)
-template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH, bool MT = false, int NL = 4>
+// KS: compute waves per SIMD (1, or 2 for the K-split form: waves w and w + 4 own the same 32 x 64 block and
+// take its even / odd K-steps, each with its own accumulators; the two partial sums meet through LDS in the
+// epilogue, where each wave stores half the block's columns -- see halo_ks2)
+template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH, bool MT = false, int NL = 4, int KS = 1>
 __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt, int st0, int ntl_arg, char* smem) {
   constexpr bool X3 = PREC == RAFT_PREC_F16X3;
   constexpr bool BF = PREC == RAFT_PREC_BF16;
@@ -220,7 +226,29 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
   // ready fragments; 1x1 convs (a patch per K-step, D = 2) keep fp32 patches
   // moved by LDS-DMA and split in the MFMA waves.
   constexpr bool LSPLIT = T > 1 && D == 3;
+  // SGB: the pre-split path's fragment reads of K-step j+1 pinned into K-step j's MFMA stream, SGB reads
+  // per MFMA gap, one K-step per scheduling region.  Left to itself the compiler sinks each read to just
+  // before its MFMA and waits lgkmcnt(1) there (the LDS round trip exposed several times per K-step).
+  // One read per gap: the update convs -4 % (tools/conv_bench.py, profiles/r06_experiments.txt); two or
+  // more per gap, or the encoders' multi-tile bodies, run out of VGPRs at 768 threads and spill.
+#ifndef HALO_SGB
+#define HALO_SGB 1
+#endif
+  constexpr int SGB = ENC ? 0 : HALO_SGB;
+  // RELAX (with SGB's pinned regions): the barrier at the end of a super-step waits only for the reads of
+  // its own load sets, not for the look-ahead reads of the next super-step's first K-step issued in its last
+  // K-step (lgkmcnt(NRD) instead of lgkmcnt(0): LDS reads complete in order), so the last read's LDS round
+  // trip is not exposed at every barrier.  Safe for the weight ring (the next super-step overwrites the slot
+  // of the set just finished) and, where patch_slots(.., late = 1) needs no extra slot, for the patch ring.
+#ifndef HALO_RELAX
+#define HALO_RELAX 1
+#endif
+  constexpr int NRD1 = NSUB * 2 * (X3 ? 2 : 1) + MF * 2 * (X3 ? 2 : 1);  // LDS reads per K-step
+  constexpr bool RELAX = HALO_RELAX && SGB > 0 && LSPLIT && !MT && patch_slots(T, U, D, 1) == PA && NRD1 <= 15;
   static_assert(D >= 2 && C::LDS_B + C::LDS_A <= C::LB, "LDS budget");
+  static_assert(KS == 1 || (KS == 2 && !MT && !ENC && LSPLIT && SGB > 0 && MF == 1 && NSUB == 2 && NL == 4 &&
+                            SB % 2 == 0 && 8 * 4096 <= C::LDS_B + C::LDS_A),
+                "the K-split form: one tile of 32 x 64 blocks on the pre-split path, 4 loaders");
   static_assert(NWP >= 1 && NBI % NWP == 0, "a wave's weight pieces lie in one K-step");
   static_assert(U % 2 == 0 && (T == 1 || T >= U), "fragment parity; at most one chunk start per load set");
   constexpr int NORM_BYTES = halo_norm_bytes<KH, KW, BNT, PREC, ENC>(C::LDS_B, C::LDS_A, D);
@@ -231,9 +259,11 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
 #endif
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool loader = w >= 4;  // the last NL waves move the operands, the first 4 compute
-  const int lw = loader ? w - 4 : w;  // loader index (compute waves: their block index)
+  constexpr int NCW = 4 * KS;  // compute waves
+  const bool loader = w >= NCW;  // the last NL waves move the operands, the first NCW compute
+  const int lw = loader ? w - NCW : w;  // loader index (compute waves: their block index)
   const int wc = w & 3;  // compute waves: block index
+  const int kp = KS > 1 ? (w >> 2) & (KS - 1) : 0;  // compute waves: K-step parity (KS = 2)
 
   const HaloArgs& a = args[prob];
   const raft_conv2d_params& p = a.p;
@@ -588,6 +618,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
       }
 #endif
       wait_vm<0>();
+      if constexpr (KS > 1) __builtin_amdgcn_s_barrier();  // (the compute waves' epilogue exchange)
       return;
     }
     // Super-step s: issue load set s+D, wait until load set s+2 has landed
@@ -649,7 +680,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
   // so neither the LDS latency nor the split stalls the MFMA stream.
   // B cursor: the weight ring slot of the next K-step to read; A cursor:
   // (tap, ky, kx) and the patch ring slot of the next K-step to read.
-  int b_bs = 0;
+  int b_bs = kp;  // (KS = 2: the odd waves start at K-step 1)
   int a_t = 0, a_ky = 0, a_kx = 0, a_ps = 0;
   struct Frag {
     h8 ah[MF][2], al[MF][2];
@@ -667,7 +698,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
           F.bl[sb][qq] = *reinterpret_cast<const h8*>(Bb + (cb + sb * 32 + m) * WROW + (((4 + 2 * h + qq) ^ bsw) << 4));
       }
     }
-    b_bs = b_bs + 1 == SB ? 0 : b_bs + 1;
+    b_bs = b_bs + KS >= SB ? b_bs + KS - SB : b_bs + KS;  // (KS = 2: this wave's next K-step)
   };
   auto advance_a = [&]() {
     ++a_kx;
@@ -705,7 +736,8 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
         if constexpr (X3) F.al[f][qq] = *reinterpret_cast<const h8*>(row + (((4 + 2 * h + qq) ^ sw) << 4));
       }
     }
-    advance_a();
+#pragma unroll
+    for (int k = 0; k < KS; ++k) advance_a();
   };
   auto split_a = [&](Frag& F) {
 #pragma unroll
@@ -826,13 +858,67 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
     }
   };
 
+  // KS = 2: the even and odd waves of a block hold partial sums of all 64 columns.  Each keeps one 32-column
+  // half (even: columns 0-31, odd: 32-63), hands the other half to its partner through LDS (the operand rings
+  // are free by now: 4 KiB per wave) and stores its half: the block's epilogue runs on both waves of the SIMD.
+  // The sum even + odd is one fp32 addition per element (commutative: the same bits on either wave).
+  auto epilogue_ks2 = [&](const Tile& t) {
+    if constexpr (KS > 1) {
+      if constexpr (X3 && !SC) {
+#pragma unroll
+        for (int sb = 0; sb < NSUB; ++sb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[0][sb][r] += accx[0][sb][r] * (1.0f / SPLIT_SCALE);
+      }
+      f32x16 keep, send;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        keep[r] = kp ? acc[0][1][r] : acc[0][0][r];
+        send[r] = kp ? acc[0][0][r] : acc[0][1][r];
+      }
+      // LDS slot of wave (wc, kp): 64 lanes x 64 B, the lane's four 16-B quads rotated by lane & 3
+      f32x4* mine = reinterpret_cast<f32x4*>(smem + (wc * 2 + kp) * 4096) + lane * 4;
+      const f32x4* theirs = reinterpret_cast<const f32x4*>(smem + (wc * 2 + (kp ^ 1)) * 4096) + lane * 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        mine[q ^ (lane & 3)] = f32x4{send[4 * q], send[4 * q + 1], send[4 * q + 2], send[4 * q + 3]};
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_s_barrier();  // (the loaders join it on their way out)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 o = theirs[q ^ (lane & 3)];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) keep[4 * q + i] += o[i];
+      }
+      const int oh = __builtin_amdgcn_readfirstlane(p.out_h), ow = __builtin_amdgcn_readfirstlane(p.out_w);
+      const int rowb = t.b * oh;
+      int rows[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mm = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int y = t.y0 + 2 * wm + (mm >> 4), x = t.x0 + (mm & 15);
+        rows[r] = ((y < oh) & (x < ow)) ? (rowb + y) * ow + x : -1;
+      }
+      tile_epilogue<false>(p, rows, t.n0 + cb + kp * 32 + m, keep);
+    }
+  };
+
   // ---- compute waves: pipeline ---------------------------------------------
   // Super-step s runs K-steps Us .. Us+U-1 (its reads reach K-step U(s+1)+1,
   // all in load sets s and s+1), then one barrier.  K-steps past nk (up to
   // nkp) run on zero weights and zero patches: they add exact zeros, and the
   // loop body has no branches.  A tile's last super-step reads nothing ahead
   // (the next tile's first fragments are read after its epilogue).
-  if constexpr (NL == 8) {  // (each compute wave also issues the prologue pieces of loader lw + 4)
+  if constexpr (KS > 1) {
+    if (kp) advance_a();  // the odd waves' first K-step is K-step 1
+  }
+  if constexpr (KS > 1) {  // the even waves issue the prologue pieces of loader lw (the odd ones none)
+    if (kp == 0) {
+#pragma unroll
+      for (int u = 0; u < DW; ++u) issue_weights(u);
+      wait_vm<NWP * (DW - 2)>();
+    }
+  } else if constexpr (NL == 8) {  // (each compute wave also issues the prologue pieces of loader lw + 4)
     const WPieces wp1 = wpieces(lw + 4);
 #pragma unroll
     for (int u = 0; u < DW; ++u) {
@@ -854,6 +940,37 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
   unsigned long long t_cmp = 0, t_wait = 0, t_bar = 0, t_epi = 0, t0 = hstamp_now();
   const unsigned long long c_loop = t0;
 #endif
+  // one K-step on the pre-split path: the fragments of this wave's next K-step into nxt while the
+  // MFMAs run on cur (SGB: the reads pinned one per MFMA gap, one scheduling region per K-step)
+  auto kstep_split = [&](Frag& nxt, const Frag& cur) {
+    if constexpr (SGB > 0) __builtin_amdgcn_sched_barrier(0);
+    read_b(nxt);
+    read_a_split(nxt);
+    mfma_step(cur);
+    if constexpr (SGB > 0) {
+      constexpr int NRD = NRD1;
+      constexpr int NMF = 2 * MF * NSUB * (X3 ? 3 : 1);
+      constexpr int RPG = SGB;
+      constexpr int NG = NRD / RPG < NMF ? NRD / RPG : NMF;  // full read groups
+      constexpr int REM = NRD - NG * RPG;                     // the rest, in slot NG (or NMF - 1)
+#pragma unroll
+      for (int i = 0; i < NMF; ++i) {
+        if (i < NG) __builtin_amdgcn_sched_group_barrier(0x100, RPG, 0);
+        if constexpr (REM > 0) {
+          if (i == (NG < NMF ? NG : NMF - 1)) __builtin_amdgcn_sched_group_barrier(0x100, REM, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // KS = 2: this wave's U / 2 K-steps of a super-step; PAR: the fragment buffer of its first (the
+  // buffers alternate per own K-step, so with one own K-step per super-step the loop runs in pairs)
+  auto superstep_ks = [&](auto par_tag) {
+    constexpr int PAR = decltype(par_tag)::value;
+#pragma unroll
+    for (int e = 0; e < U / KS; ++e) kstep_split(F[(PAR + e + 1) & 1], F[(PAR + e) & 1]);
+  };
   // one super-step's K-steps; LAST: the tile's last super-step, which reads nothing ahead
   auto superstep = [&](auto last_tag) {
     constexpr bool LAST = decltype(last_tag)::value;
@@ -866,9 +983,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
       if (LAST && e == U - 1) {
         mfma_step(F[e & 1]);
       } else if constexpr (LSPLIT) {
-        read_b(F[(e + 1) & 1]);
-        read_a_split(F[(e + 1) & 1]);
-        mfma_step(F[e & 1]);
+        kstep_split(F[(e + 1) & 1], F[e & 1]);
       } else {
         read_b(F[(e + 1) & 1]);
         mfma_step(F[e & 1]);
@@ -884,7 +999,10 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
     unsigned long long t2 = hstamp_now();
     t_cmp += t2 - t0;
 #endif
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the next fragments are in registers
+    if constexpr (RELAX)
+      __builtin_amdgcn_s_waitcnt(0xC07F | (NRD1 << 8));  // lgkmcnt(NRD1): all but the look-ahead reads
+    else
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the next fragments are in registers
     if (first) wait_vm<0>();              // the prologue's weight sets 2 .. D-1 (this wave's only DMAs)
     first = false;
 #ifdef STAMPS
@@ -897,12 +1015,36 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
     t_bar += t0 - t3;
 #endif
   };
-  if constexpr (!MT) {
+  if constexpr (KS > 1) {
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    int s = 0;
+    if constexpr ((U / KS) % 2 == 1) {
+      for (; s + 1 < NS; s += 2) {
+        superstep_ks(P0{});
+        step_end();
+        superstep_ks(P1{});
+        step_end();
+      }
+    }
+    for (; s < NS; ++s) {
+      superstep_ks(P0{});
+      step_end();
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // (the last look-ahead reads, before the ring is reused)
+    __builtin_amdgcn_sched_barrier(0);
+    epilogue_ks2(tile0);
+#ifdef STAMPS
+    const unsigned long long t4 = hstamp_now();
+    t_epi += t4 - t0;
+#endif
+  } else if constexpr (!MT) {
     // one tile: the last super-step's look-ahead reads land in ring slots nobody writes any more
     for (int s = 0; s < NS; ++s) {
       superstep(std::false_type{});
       step_end();
     }
+    if constexpr (RELAX) __builtin_amdgcn_s_waitcnt(0xC07F);  // (the last look-ahead reads, before exit)
     __builtin_amdgcn_sched_barrier(0);
     epilogue(tile0);
 #ifdef STAMPS
@@ -942,7 +1084,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
 #ifdef STAMPS
   {
     const unsigned long long c_exit = hstamp_now(), r_exit = hstamp_real();
-    const unsigned wid = blockIdx.x * 4 + w;
+    const unsigned wid = blockIdx.x * NCW + w;
     if (lane == 0 && wid < 16384) {
       unsigned long long* g = g_hstamp + wid * 8;
       g[0] = r_entry;
@@ -960,8 +1102,8 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
 // One conv (or an independent pair, raft_conv2d_pair) per launch: work-group g runs tiles
 // N-tile g % gn of spatial tiles (g / gn) * m .. + m-1 of its conv (the pair's first grid0
 // work-groups take a[0]'s tiles).
-template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH, bool MT = false, int NL = 4>
-__global__ __launch_bounds__(64 * (4 + NL)) void conv_halo_kernel(HaloLaunch hl) {
+template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH, bool MT = false, int NL = 4, int KS = 1>
+__global__ __launch_bounds__(64 * (4 * KS + NL)) void conv_halo_kernel(HaloLaunch hl) {
   using C = HaloCfg<KH, KW, BNT, PREC == RAFT_PREC_F16X3 ? 128 : 64, TH>;
   constexpr int NORM_BYTES = halo_norm_bytes<KH, KW, BNT, PREC, ENC>(C::LDS_B, C::LDS_A, C::D);
   __shared__ __attribute__((aligned(1024))) char smem[C::LDS_B + C::LDS_A + NORM_BYTES];
@@ -974,7 +1116,7 @@ __global__ __launch_bounds__(64 * (4 + NL)) void conv_halo_kernel(HaloLaunch hl)
     const int ntl = min(hl.m, (prob ? hl.sp1 : hl.sp0) - st0);
     halo_body<KH, KW, BNT, PREC, ENC, TH, true, NL>(hl.a, prob, g % gn, st0, ntl, smem);
   } else {  // (hl.m == 1)
-    halo_body<KH, KW, BNT, PREC, ENC, TH, false, NL>(hl.a, prob, g % gn, g / gn, 1, smem);
+    halo_body<KH, KW, BNT, PREC, ENC, TH, false, NL, KS>(hl.a, prob, g % gn, g / gn, 1, smem);
   }
 }
 
@@ -993,6 +1135,18 @@ bool halo_nl8() {
   }
   return v == 8;
 }
+// the K-split form (two compute waves per SIMD, halo_body KS = 2) for the one-tile f16x3 update convs with
+// 64-column tiles: RAFT_HALO_KS2=1 (or raft_conv2d_set_halo_ks)
+std::atomic<int> g_halo_ks{0};  // 0: from the environment
+bool halo_ks2() {
+  int v = g_halo_ks.load(std::memory_order_relaxed);
+  if (v == 0) {
+    const char* e = getenv("RAFT_HALO_KS2");
+    v = e && e[0] == '1' ? 2 : 1;
+    g_halo_ks.store(v, std::memory_order_relaxed);
+  }
+  return v == 2;
+}
 bool halo_nl8_enc() {
   static const bool v = [] {
     // (default on: config 2 +0.1 / +0.3 % in two interleaved pairs on one box, profiles/r05f_experiments.txt)
@@ -1001,9 +1155,17 @@ bool halo_nl8_enc() {
   }();
   return v;
 }
+// the shapes compiled without the multi-tile body (launch_halo_mt): halo_mt_ok never plans m > 1 for
+// them, and the launch refuses m > 1 (the one-tile kernel would run only 1/m of the spatial tiles)
+constexpr bool halo_no_mt(int prec, int taps, int bn) { return prec != RAFT_PREC_F16X3 && taps == 9 && bn == 128; }
+
 template <int KH, int KW, int BNT, int PREC, bool ENC = false, int TH = HTH>
 void launch_halo_mt(const HaloLaunch& l, dim3 grid, hipStream_t s) {
-  constexpr bool NO_MT = PREC != RAFT_PREC_F16X3 && KH * KW == 9 && BNT == 128;
+  constexpr bool NO_MT = halo_no_mt(PREC, KH * KW, BNT);
+  if (NO_MT && l.m > 1) {
+    fprintf(stderr, "raft_hip: internal error: a one-tile-only halo conv was planned with %d tiles per work-group\n", l.m);
+    abort();
+  }
   // the 8-loader form: one-tile f16x3 update-block convs (default; RAFT_HALO_NL8=0: 4 loaders)
   constexpr bool CAN_NL8 = PREC == RAFT_PREC_F16X3 && !ENC && TH == HTH && BNT <= 64 && KH * KW > 1;
   // and for the encoders' f16x3 3x3 convs on 128-pixel tiles (default; RAFT_HALO_NL8_ENC=0: 4): their loaders also
@@ -1018,9 +1180,17 @@ void launch_halo_mt(const HaloLaunch& l, dim3 grid, hipStream_t s) {
       return;
     }
   }
+  // the K-split form: the one-tile f16x3 update convs with 64-column tiles on the pre-split path
+  constexpr bool CAN_KS2 = CAN_NL8 && BNT == 64 && HaloCfg<KH, KW, BNT, 128, TH>::D == 3;
   if (!NO_MT && l.m > 1) {
     hipLaunchKernelGGL((conv_halo_kernel<KH, KW, BNT, PREC, ENC, TH, !NO_MT>), grid, dim3(512), 0, s, l);
   } else {
+    if constexpr (CAN_KS2) {
+      if (halo_ks2()) {
+        hipLaunchKernelGGL((conv_halo_kernel<KH, KW, BNT, PREC, ENC, TH, false, 4, 2>), grid, dim3(768), 0, s, l);
+        return;
+      }
+    }
     if constexpr (CAN_NL8) {
       if (halo_nl8()) {
         hipLaunchKernelGGL((conv_halo_kernel<KH, KW, BNT, PREC, ENC, TH, false, 8>), grid, dim3(768), 0, s, l);
@@ -1245,7 +1415,8 @@ bool halo_mt_ok(const HaloArgs& a, int bn, int th, long m) {
   // modes' 3x3 convs with several N-tiles ran 18-30 % slower on multi-tile work-groups (their short
   // K loops do not cover the next tile's loads beside the last one's stores); their 1x1 / 1x5 convs
   // and every f16x3 conv gained
-  if (a.p.precision != RAFT_PREC_F16X3 && T == 9 && (a.gn > 1 || bn == 128)) return false;  // (wide: unmeasured)
+  if (halo_no_mt(a.p.precision, T, bn)) return false;  // (not compiled: wide tiles unmeasured)
+  if (a.p.precision != RAFT_PREC_F16X3 && T == 9 && a.gn > 1) return false;
   const int n1 = halo_nkp(a.nk, U, T, false), nm = halo_nkp(a.nk, U, T, true);
   if ((long)(nm - n1) * 8 > n1) return false;
   if (a.p.in_norm) {

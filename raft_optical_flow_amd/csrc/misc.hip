@@ -517,7 +517,13 @@ __global__ __launch_bounds__(64 * MERGE2_WAVES) void instnorm_merge_fused_kernel
                            __double_as_longlong(((red[0][q][lane] + red[1][q][lane]) + red[2][q][lane]) + red[3][q][lane]),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sums have left for memory (sc1)
+    // the sums have left for memory (sc1).  The hand-off is the measured valid form of
+    // MI355X_MICROARCH.md (inter-workgroup visibility, first row of the sc1 table): every byte stored
+    // sc1 and drained before ONE lane's agent-scope add; the block whose add returns G - 1 reads them
+    // with sc1 loads only, behind a workgroup barrier, so no L1-resident copy can be read stale.  An
+    // acq_rel add would order the same bytes through a whole-L2 write-back and an L1 invalidate
+    // (~1.7 us each on this chip) per merge.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) is_last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
   }
   __syncthreads();
@@ -551,7 +557,9 @@ __global__ __launch_bounds__(64 * MERGE2_WAVES) void instnorm_merge_fused_kernel
   }
   __syncthreads();
   if (w != 0) return;
-  if (lane == 0) *cnt = 0;  // (the next launch starts from zero; kernel boundary orders it)
+  // the next launch starts from zero (an agent-scope store, like every other access to the counter; the
+  // kernel boundary orders it before the next launch's adds)
+  if (lane == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (!cok) return;
   double n = 0.0, s1 = 0.0, s2 = 0.0;
 #pragma unroll

@@ -192,18 +192,35 @@ class RAFT(nn.Module):
             packs[prec] = got
         return got[1]
 
-    def plan(self, batch, height, width, iters, test_mode=True, flow_init=False, device=None, prec=None):
-        device = device or next(self.parameters()).device
-        prec = prec or self.resolved_precision()
-        pk = self.packed(device, prec)
+    def _plan_key(self, batch, height, width, iters, test_mode, flow_init, prec):
         # the stream layout knobs are read when a plan is built, so they are part of its key
         knobs = (os.environ.get("RAFT_CTX_SIDE", "1"), os.environ.get("RAFT_FLOW_SIDE", "1"),
                  os.environ.get("RAFT_CONV_PAIR", "1"), os.environ.get("RAFT_FUSE_CONVF1", "1"),
                  os.environ.get("RAFT_FUSE_CONVC1", "1"), os.environ.get("RAFT_EPI_STATS", "1"),
                  os.environ.get("RAFT_IN_NORM", "1"))
         guard = self.range_guard != "off"  # "off": no device-side checks either
-        key = (batch, height, width, iters, bool(test_mode), bool(self.args.alternate_corr), bool(flow_init), prec,
-               knobs, guard)
+        return (batch, height, width, iters, bool(test_mode), bool(self.args.alternate_corr), bool(flow_init), prec,
+                knobs, guard)
+
+    def _cached_plan(self, batch, height, width, iters, test_mode, flow_init, device):
+        """The cached plan of this call and the weights key its packed weights were made from, WITHOUT
+        checking that key against the parameters (forward() checks it while the plan runs); None when
+        the call has no plan yet."""
+        prec = self.resolved_precision()
+        cache = self._dev_cache(device)
+        got = cache["packed"].get(prec)
+        if got is None:
+            return None
+        pl = cache["plans"].get(self._plan_key(batch, height, width, iters, test_mode, flow_init, prec))
+        if pl is None or pl.pk is not got[1]:
+            return None
+        return pl, got[0]
+
+    def plan(self, batch, height, width, iters, test_mode=True, flow_init=False, device=None, prec=None):
+        device = device or next(self.parameters()).device
+        prec = prec or self.resolved_precision()
+        pk = self.packed(device, prec)
+        key = self._plan_key(batch, height, width, iters, test_mode, flow_init, prec)
         plans = self._dev_cache(device)["plans"]
         pl = plans.get(key)
         if pl is None:
@@ -211,7 +228,7 @@ class RAFT(nn.Module):
                 plans.popitem(last=False)[1].release()
             pl = RaftPlan(pk, batch, height, width, iters, test_mode=test_mode,
                           alternate=bool(self.args.alternate_corr), flow_init=flow_init, device=device,
-                          range_guard=guard)
+                          range_guard=key[-1])
             plans[key] = pl
         else:
             plans.move_to_end(key)
@@ -279,18 +296,36 @@ class RAFT(nn.Module):
         if self._pending and _prec is None:
             self.check_range_guard(block=False)  # earlier forwards whose flags have landed
         b, _, H, W = image1.shape
-        pl = self.plan(b, H, W, iters, test_mode, flow_init is not None, image1.device, prec=_prec)
-        pl.set_inputs(image1, image2, flow_init)
         mode = self.range_guard
         if mode == "deferred" and self.__dict__.get("_is_replica", False):
             mode = "fallback"  # a DataParallel replica lives for one forward: nothing can be deferred
-        guard = pl.guarded and mode != "off"
-        if guard:
-            pl.range_flag.zero_()
-        if self.hip_graph and (pl.graph is not None or pl.runs > 0):
-            pl.replay()
-        else:
-            pl.run()
+        # Steady state (same weights, shape and settings as a cached plan): the plan is enqueued first and
+        # the weights key -- a walk over every parameter, ~0.2-0.7 ms of host time -- is checked while it
+        # runs, instead of leaving the GPU idle between back-to-back forwards.  Changed weights (in-place
+        # edits, load_state_dict, .to()) are caught by that check: the stale run is discarded and the
+        # forward re-run on freshly packed weights, so the result is the one the reference would return.
+        cached = None
+        if _prec is None and self.hip_graph and not self.__dict__.get("_is_replica", False):
+            cached = self._cached_plan(b, H, W, iters, test_mode, flow_init is not None, image1.device)
+        while True:
+            if cached is not None:
+                pl, wkey = cached
+            else:
+                pl = self.plan(b, H, W, iters, test_mode, flow_init is not None, image1.device, prec=_prec)
+            pl.set_inputs(image1, image2, flow_init)
+            guard = pl.guarded and mode != "off"
+            if guard:
+                pl.range_flag.zero_()
+            if self.hip_graph and (pl.graph is not None or pl.runs > 0):
+                pl.replay()
+            else:
+                pl.run()
+            if cached is None or (self._source()._weights_key(), str(image1.device)) == wkey:
+                break
+            # the weights changed since the plan was packed: let the stale run finish before its plan
+            # can be released, then take the checked path
+            torch.cuda.current_stream().synchronize()
+            cached = None
         outs = pl.outputs(clone=True)
         if not guard:
             return outs

@@ -1120,6 +1120,30 @@ def test_f16x3_range_guard_falls_back_to_fp32():
     assert not bool(torch.isfinite(up_off).all()) or maxabs(up_off, rup) > 1e-3
 
 
+def test_forward_repacks_weights_changed_between_calls():
+    """The steady-state forward() enqueues its cached plan before it checks the weights key (raft.py):
+    weights edited in place or reloaded by load_state_dict after earlier forwards must still give the
+    result of a model built from the new weights, bit for bit, and the original weights the original
+    result."""
+    from raft_optical_flow_amd.init import seeded_state_dict
+    g = load_golden("raft_full_rand_b1_128x192_i32.npz")
+    m, _ = make_model(False, 0)
+    i1, i2 = t(g["image1"]), t(g["image2"])
+    with torch.no_grad():
+        for _ in range(3):  # eager run, graph capture, replay: the plan is cached
+            a_low, a_up = m(i1, i2, iters=4, test_mode=True)
+        m.update_block.flow_head.conv2.weight.mul_(1.5)  # in place, after the plan was packed
+        b_low, b_up = m(i1, i2, iters=4, test_mode=True)
+        ref, _ = make_model(False, 0)
+        ref.load_state_dict(m.state_dict())
+        r_low, r_up = ref(i1, i2, iters=4, test_mode=True)
+        assert maxabs(b_up, r_up) == 0.0 and maxabs(b_low, r_low) == 0.0
+        assert maxabs(a_up, b_up) > 1e-3
+        m.load_state_dict(seeded_state_dict(m, 0))  # back to the first weights (an in-place copy_)
+        c_low, c_up = m(i1, i2, iters=4, test_mode=True)
+        assert maxabs(c_up, a_up) == 0.0 and maxabs(c_low, a_low) == 0.0
+
+
 def test_range_guard_deferred_forwards_queue_without_host_sync():
     """"deferred" mode: back-to-back forwards enqueue without waiting for the GPU (the flag is read
     once its copy has landed): behind a ~50 ms spin kernel, two forward() calls return while the
