@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define RAFT_HIP_ABI_VERSION 17
+#define RAFT_HIP_ABI_VERSION 18
 
 /* Negative return codes (argument errors, raised before any launch). */
 #define RAFT_E_INVALID (-1)   /* bad size / null pointer / unsupported shape */
@@ -401,6 +401,13 @@ int raft_conv2d_pair(const raft_conv2d_params* p0, const raft_conv2d_params* p1,
  * Returns the previous count; other values only query.  Process-wide; plans capture launches, so
  * set it before building / capturing a plan. */
 int raft_conv2d_set_halo_loaders(int nl);
+/* The compute waves per SIMD of the same convs when their N tile is 64 columns: 2 (default; the K-split form:
+ * waves w and w + 4 take the even / odd K-steps of one 32 x 64 block, their partial sums meet in LDS and each
+ * stores half the columns; 4 loader waves, 768 threads) or 1.  The two forms sum the K-steps in different orders
+ * (results within fp32 rounding of each other; each deterministic).  Returns the previous count; other values
+ * only query.  Process-wide; set it before building / capturing a plan.  (Engine-level knob; no reference
+ * counterpart.) */
+int raft_conv2d_set_halo_ks(int ks);
 /* fp32 packed weight [n_pad][k_pad] -> split form for RAFT_PREC_F16X3 / F16:
  * per row and 32-wide K-step, 32 f16 hi then 32 f16 lo (lo scaled by 2048);
  * out holds n_pad*k_pad*4 bytes, like the input. */

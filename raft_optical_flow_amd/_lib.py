@@ -29,7 +29,7 @@ PREC_F16 = 2     # single f16 product (mixed precision)
 PREC_BF16 = 3    # single bf16 product on v_mfma_f32_32x32x16_bf16 (bf16 mixed precision)
 PRECISIONS = {"fp32": PREC_FP32, "f16x3": PREC_F16X3, "f16": PREC_F16, "bf16": PREC_BF16}
 
-ABI_VERSION = 17
+ABI_VERSION = 18
 RANGE_LIMIT = 32768.0  # RAFT_RANGE_LIMIT: |x| above it raises the f16x3 range guard
 
 EPI_LINEAR = 0
@@ -118,6 +118,7 @@ _PROTOS = {
     "raft_instnorm_merge_ws": (c_int, [P, c_int, c_int, c_int, c_int, c_float, P, P, P]),
     "raft_instnorm_merge_counters": (c_size_t, [c_int, c_int]),
     "raft_conv2d_set_halo_loaders": (c_int, [c_int]),
+    "raft_conv2d_set_halo_ks": (c_int, [c_int]),
     "raft_instnorm_merge_fused": (c_int, [P, c_int, c_int, c_int, c_int, c_float, P, P, P, P]),
     "raft_conv2d_split_weight": (c_int, [P, P, c_int, c_int, P]),
     "raft_conv2d_split_weight_prec": (c_int, [P, P, c_int, c_int, c_int, P]),

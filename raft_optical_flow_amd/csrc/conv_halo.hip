@@ -207,6 +207,15 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
   constexpr int RPP = 1024 / WROW;             // rows per 1-KiB DMA piece
   constexpr int NBI = BNT / RPP;    // 1-KiB DMA pieces per weight block (one K-step)
   constexpr int NWP = U * NBI / NL;  // weight pieces per loader wave per load set
+  // KSW (KS = 2, dev builds -DHALO_KSW=1): the compute waves issue the weight DMAs (NWPC pieces each per load
+  // set) and the loaders stage only the patches.  Measured slower than the loaders issuing both (the DMA issue
+  // sits in the compute waves' MFMA stream: profiles/r06b_experiments.txt), so off by default.
+#ifndef HALO_KSW
+#define HALO_KSW 0
+#endif
+  constexpr bool KSW = KS > 1 && HALO_KSW;
+  constexpr int NWPC = KSW ? U * NBI / (4 * KS) : 1;
+  constexpr int LNWP = KSW ? 0 : NWP;  // weight pieces a loader issues per load set
   // Compute waves (32-pixel MFMA row blocks = two tile rows): TH = 8, BNT <= 64: 4 waves along M,
   // each one block (tile rows 2w, 2w+1) x all BNT columns; TH = 8, BNT = 128 (the one-product
   // modes' wide tiles): 2 x 2 waves, each 2 blocks (64 pixels) x 64 columns; TH = 16, BNT = 64:
@@ -225,7 +234,10 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
   // pre-split (f16 hi | lo, the weight-row format), so the MFMA waves read
   // ready fragments; 1x1 convs (a patch per K-step, D = 2) keep fp32 patches
   // moved by LDS-DMA and split in the MFMA waves.
-  constexpr bool LSPLIT = T > 1 && D == 3;
+#ifndef HALO_NOLSPLIT  // dev builds: the update convs' patches as fp32 by LDS-DMA, split by the compute waves
+#define HALO_NOLSPLIT 0
+#endif
+  constexpr bool LSPLIT = T > 1 && D == 3 && !(HALO_NOLSPLIT && !ENC);
   // SGB: the pre-split path's fragment reads of K-step j+1 pinned into K-step j's MFMA stream, SGB reads
   // per MFMA gap, one K-step per scheduling region.  Left to itself the compiler sinks each read to just
   // before its MFMA and waits lgkmcnt(1) there (the LDS round trip exposed several times per K-step).
@@ -234,7 +246,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
 #ifndef HALO_SGB
 #define HALO_SGB 1
 #endif
-  constexpr int SGB = ENC ? 0 : HALO_SGB;
+  constexpr int SGB = (ENC && NL == 8) ? 0 : HALO_SGB;
   // RELAX (with SGB's pinned regions): the barrier at the end of a super-step waits only for the reads of
   // its own load sets, not for the look-ahead reads of the next super-step's first K-step issued in its last
   // K-step (lgkmcnt(NRD) instead of lgkmcnt(0): LDS reads complete in order), so the last read's LDS round
@@ -247,7 +259,8 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
   constexpr bool RELAX = HALO_RELAX && SGB > 0 && LSPLIT && !MT && patch_slots(T, U, D, 1) == PA && NRD1 <= 15;
   static_assert(D >= 2 && C::LDS_B + C::LDS_A <= C::LB, "LDS budget");
   static_assert(KS == 1 || (KS == 2 && !MT && !ENC && LSPLIT && SGB > 0 && MF == 1 && NSUB == 2 && NL == 4 &&
-                            SB % 2 == 0 && 8 * 4096 <= C::LDS_B + C::LDS_A),
+                            SB % 2 == 0 && 8 * 4096 <= C::LDS_B + C::LDS_A && DW == D && NBI % NWPC == 0 &&
+                            NWPC >= 1),
                 "the K-split form: one tile of 32 x 64 blocks on the pre-split path, 4 loaders");
   static_assert(NWP >= 1 && NBI % NWP == 0, "a wave's weight pieces lie in one K-step");
   static_assert(U % 2 == 0 && (T == 1 || T >= U), "fragment parity; at most one chunk start per load set");
@@ -326,6 +339,32 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
     return q;
   };
   const WPieces wp0 = wpieces(lw);
+  // the compute waves' pieces (KSW): NWPC consecutive pieces of one K-step's block per compute wave
+  struct WPiecesC {
+    int ew, wpc0;
+    unsigned off[NWPC];
+  };
+  auto wpieces_c = [&](int ci) {
+    WPiecesC q;
+    q.ew = (ci * NWPC) / NBI;
+    q.wpc0 = (ci * NWPC) % NBI;
+#pragma unroll
+    for (int k = 0; k < NWPC; ++k) {
+      const int r = RPP * (q.wpc0 + k) + lane / QPR;
+      const int qd = X3 ? (lane & 7) ^ ((r >> 1) & 7) : (lane & 3) ^ ((r >> 2) & 3);
+      q.off[k] = (unsigned)(r + nt * BNT) * ((unsigned)a.K * 4u) + (unsigned)qd * 16u;
+    }
+    return q;
+  };
+  auto issue_weights_c = [&](int u, const WPiecesC& q) {  // (!MT: load set u of the one tile)
+    const int j = U * u + q.ew;
+    const bool in = j < nk;
+    const int c = j / T, t = j - c * T;
+    const unsigned soff = in ? (unsigned)(t * nch + c) * 128u : 0u;
+    char* dst = smem + (U * (u % (DW + 1)) + q.ew) * (BNT * WROW) + q.wpc0 * 1024;
+#pragma unroll
+    for (int k = 0; k < NWPC; ++k) dma16(rs_w, dst + k * 1024, in ? q.off[k] : OFF_INVALID, soff);
+  };
   auto issue_weights_q = [&](int u, const WPieces& q) {
     int kt, ul;
     set_tile(u, kt, ul);
@@ -565,7 +604,7 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
 #endif
       for (int s = 0; s < NS; ++s) {
         if (pend_k >= 0) {
-          wait_vm<NWP>();  // that patch's loads (the weights issued after them may fly on)
+          wait_vm<LNWP>();  // that patch's loads (the weights issued after them may fly on)
           store_patch(pend_k, pend_c, pv[0]);
           pend_k = -1;
         }
@@ -582,12 +621,12 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
           LSTAMP(l_ld);
           // (in the same branch as the patch loads: on every path the compiler sees NWP DMAs behind
           // them, so its own waits for the staged registers stay at vmcnt(NWP), not vmcnt(0))
-          if constexpr (DW == D) {
+          if constexpr (DW == D && !KSW) {
             issue_weights(s + D);
             nnew += NWP;
           }
         }
-        if constexpr (DW > D) {
+        if constexpr (DW > D && !KSW) {
           if (s + DW < NS) {
             issue_weights(s + DW);
             nnew += NWP;
@@ -912,7 +951,12 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
   if constexpr (KS > 1) {
     if (kp) advance_a();  // the odd waves' first K-step is K-step 1
   }
-  if constexpr (KS > 1) {  // the even waves issue the prologue pieces of loader lw (the odd ones none)
+  const WPiecesC wpc = wpieces_c(KSW ? w : 0);
+  if constexpr (KSW) {  // every compute wave issues its pieces of sets 0 .. D-1 (and later of every set)
+#pragma unroll
+    for (int u = 0; u < DW; ++u) issue_weights_c(u, wpc);
+    wait_vm<NWPC * (DW - 2)>();
+  } else if constexpr (KS > 1) {  // the even compute waves issue the prologue pieces of loader wc
     if (kp == 0) {
 #pragma unroll
       for (int u = 0; u < DW; ++u) issue_weights(u);
@@ -966,8 +1010,16 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
   };
   // KS = 2: this wave's U / 2 K-steps of a super-step; PAR: the fragment buffer of its first (the
   // buffers alternate per own K-step, so with one own K-step per super-step the loop runs in pairs)
-  auto superstep_ks = [&](auto par_tag) {
+  int nnew_c = 0;  // KSW: weight pieces this wave issued in the current super-step
+  auto superstep_ks = [&](auto par_tag, int s) {
     constexpr int PAR = decltype(par_tag)::value;
+    nnew_c = 0;
+    if constexpr (KSW) {
+      if (s + D < NS) {
+        issue_weights_c(s + D, wpc);
+        nnew_c = NWPC;
+      }
+    }
 #pragma unroll
     for (int e = 0; e < U / KS; ++e) kstep_split(F[(PAR + e + 1) & 1], F[(PAR + e) & 1]);
   };
@@ -1003,7 +1055,11 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
       __builtin_amdgcn_s_waitcnt(0xC07F | (NRD1 << 8));  // lgkmcnt(NRD1): all but the look-ahead reads
     else
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the next fragments are in registers
-    if (first) wait_vm<0>();              // the prologue's weight sets 2 .. D-1 (this wave's only DMAs)
+    if constexpr (KSW) {
+      wait_vm_n(nnew_c);  // this wave's pieces of every set but the one issued in this super-step have landed
+    } else {
+      if (first) wait_vm<0>();  // the prologue's weight sets 2 .. D-1 (this wave's only DMAs)
+    }
     first = false;
 #ifdef STAMPS
     unsigned long long t3 = hstamp_now();
@@ -1021,14 +1077,14 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
     int s = 0;
     if constexpr ((U / KS) % 2 == 1) {
       for (; s + 1 < NS; s += 2) {
-        superstep_ks(P0{});
+        superstep_ks(P0{}, s);
         step_end();
-        superstep_ks(P1{});
+        superstep_ks(P1{}, s + 1);
         step_end();
       }
     }
     for (; s < NS; ++s) {
-      superstep_ks(P0{});
+      superstep_ks(P0{}, s);
       step_end();
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // (the last look-ahead reads, before the ring is reused)
@@ -1136,13 +1192,15 @@ bool halo_nl8() {
   return v == 8;
 }
 // the K-split form (two compute waves per SIMD, halo_body KS = 2) for the one-tile f16x3 update convs with
-// 64-column tiles: RAFT_HALO_KS2=1 (or raft_conv2d_set_halo_ks)
+// 64-column tiles (default; RAFT_HALO_KS2=0 or raft_conv2d_set_halo_ks(1): one compute wave per SIMD).
+// Config 2, bench.py interleaved on one box: 144.7 / 143.9 / 144.2 -> 146.9 / 147.0 / 147.0 pairs/s, the
+// iteration's update convs 151-153 -> 146-148 us (profiles/r06b_experiments.txt)
 std::atomic<int> g_halo_ks{0};  // 0: from the environment
 bool halo_ks2() {
   int v = g_halo_ks.load(std::memory_order_relaxed);
   if (v == 0) {
     const char* e = getenv("RAFT_HALO_KS2");
-    v = e && e[0] == '1' ? 2 : 1;
+    v = e && e[0] == '0' ? 1 : 2;
     g_halo_ks.store(v, std::memory_order_relaxed);
   }
   return v == 2;
@@ -1181,7 +1239,7 @@ void launch_halo_mt(const HaloLaunch& l, dim3 grid, hipStream_t s) {
     }
   }
   // the K-split form: the one-tile f16x3 update convs with 64-column tiles on the pre-split path
-  constexpr bool CAN_KS2 = CAN_NL8 && BNT == 64 && HaloCfg<KH, KW, BNT, 128, TH>::D == 3;
+  constexpr bool CAN_KS2 = CAN_NL8 && BNT == 64 && HaloCfg<KH, KW, BNT, 128, TH>::D == 3 && !HALO_NOLSPLIT;
   if (!NO_MT && l.m > 1) {
     hipLaunchKernelGGL((conv_halo_kernel<KH, KW, BNT, PREC, ENC, TH, !NO_MT>), grid, dim3(512), 0, s, l);
   } else {
@@ -1500,6 +1558,14 @@ extern "C" int raft_debug_lstamps(unsigned long long* host, int n, int clear) {
 extern "C" int raft_conv2d_set_halo_loaders(int nl) {
   const int prev = halo_nl8() ? 8 : 4;
   if (nl == 4 || nl == 8) g_halo_nl.store(nl, std::memory_order_relaxed);
+  return prev;
+}
+
+// the compute waves per SIMD of the one-tile f16x3 update convs with 64-column tiles (1 or 2); returns the
+// previous
+extern "C" int raft_conv2d_set_halo_ks(int ks) {
+  const int prev = halo_ks2() ? 2 : 1;
+  if (ks == 1 || ks == 2) g_halo_ks.store(ks, std::memory_order_relaxed);
   return prev;
 }
 

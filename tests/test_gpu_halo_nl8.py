@@ -22,8 +22,10 @@ def loaders():
     from raft_optical_flow_amd import _lib
     lib = _lib.load()
     prev = lib.raft_conv2d_set_halo_loaders(0)
+    prev_ks = lib.raft_conv2d_set_halo_ks(1)  # (the one-compute-wave form, whose loader count this varies)
     yield lib
     lib.raft_conv2d_set_halo_loaders(prev)
+    lib.raft_conv2d_set_halo_ks(prev_ks)
 
 
 def _run(lib, nl, pc, x, B, H, W, cout):

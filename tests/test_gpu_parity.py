@@ -876,29 +876,42 @@ def test_conv2d_two_segments_and_gru_epilogues(prec):
     (1, 5, 96, 128, 64, 64, 1, 9, 19),       # another shape class
     (3, 3, 64, 64, 64, 64, 1, 8, 16),        # 3x3 beside 1x1 below: shapes differ -> two launches
 ])
-def test_conv2d_pair_equals_two_convs(kh, kw, c0, n0, c1, n1, B, H, W, prec):
-    """raft_conv2d_pair == raft_conv2d twice (bit for bit: each tile runs the same K-walk)."""
+@pytest.mark.parametrize("ks", [1, 2])
+def test_conv2d_pair_equals_two_convs(kh, kw, c0, n0, c1, n1, B, H, W, prec, ks):
+    """raft_conv2d_pair == raft_conv2d twice, bit for bit (each tile runs the same K-walk), with one compute
+    wave per SIMD (raft_conv2d_set_halo_ks(1)).  With two (the K-split form, the default) a conv that runs
+    64-column tiles in the pair but 32-column ones alone sums its K-steps in another order: there the two
+    agree within 1e-5 of the output's magnitude, and bit for bit wherever both take the same form."""
     from raft_optical_flow_amd import kernels as K
     from raft_optical_flow_amd import _lib
-    g = torch.Generator().manual_seed(c0 + n1)
-    shapes = [(c0, n0, kh, kw), (c1, n1, kh, kw) if (c1, n1) != (64, 64) or kh == 1 else (c1, n1, 1, 1)]
-    xs, pcs, outs_pair, outs_seq = [], [], [], []
-    for cin, cout, a, b in shapes:
-        x = torch.randn(B, cin, H, W, generator=g)
-        w = torch.randn(cout, cin, a, b, generator=g) / np.sqrt(cin * a * b)
-        pc = K.pack_conv(w, torch.randn(cout, generator=g), 1, ((a - 1) // 2, (b - 1) // 2), device=DEV)
-        pc.precision = _lib.PRECISIONS[prec]
-        xs.append(K.Rows(K.nchw_to_rows(x.to(DEV))))
-        pcs.append(pc)
-        outs_pair.append(K.Rows(torch.full((B * H * W, cout), 7.0, device=DEV)))
-        outs_seq.append(K.Rows(torch.full((B * H * W, cout), 7.0, device=DEV)))
-    prm = [K.conv_params(pcs[i], xs[i], B, H, W, outs_pair[i], epilogue=_lib.EPI_RELU) for i in range(2)]
-    K.conv_pair_launch(prm[0], prm[1])(K.stream_handle())
-    for i in range(2):
-        K.conv2d_rows(pcs[i], xs[i], B, H, W, outs_seq[i], epilogue=_lib.EPI_RELU)
-    torch.cuda.synchronize()
-    for i in range(2):
-        assert torch.equal(outs_pair[i].t, outs_seq[i].t), (i, maxabs(outs_pair[i].t, outs_seq[i].t))
+    lib = _lib.load()
+    prev_ks = lib.raft_conv2d_set_halo_ks(ks)
+    try:
+        g = torch.Generator().manual_seed(c0 + n1)
+        shapes = [(c0, n0, kh, kw), (c1, n1, kh, kw) if (c1, n1) != (64, 64) or kh == 1 else (c1, n1, 1, 1)]
+        xs, pcs, outs_pair, outs_seq = [], [], [], []
+        for cin, cout, a, b in shapes:
+            x = torch.randn(B, cin, H, W, generator=g)
+            w = torch.randn(cout, cin, a, b, generator=g) / np.sqrt(cin * a * b)
+            pc = K.pack_conv(w, torch.randn(cout, generator=g), 1, ((a - 1) // 2, (b - 1) // 2), device=DEV)
+            pc.precision = _lib.PRECISIONS[prec]
+            xs.append(K.Rows(K.nchw_to_rows(x.to(DEV))))
+            pcs.append(pc)
+            outs_pair.append(K.Rows(torch.full((B * H * W, cout), 7.0, device=DEV)))
+            outs_seq.append(K.Rows(torch.full((B * H * W, cout), 7.0, device=DEV)))
+        prm = [K.conv_params(pcs[i], xs[i], B, H, W, outs_pair[i], epilogue=_lib.EPI_RELU) for i in range(2)]
+        K.conv_pair_launch(prm[0], prm[1])(K.stream_handle())
+        for i in range(2):
+            K.conv2d_rows(pcs[i], xs[i], B, H, W, outs_seq[i], epilogue=_lib.EPI_RELU)
+        torch.cuda.synchronize()
+        for i in range(2):
+            err = maxabs(outs_pair[i].t, outs_seq[i].t)
+            if ks == 1:
+                assert torch.equal(outs_pair[i].t, outs_seq[i].t), (i, err)
+            else:
+                assert err <= 1e-5 * float(outs_seq[i].t.abs().max()), (i, err)
+    finally:
+        lib.raft_conv2d_set_halo_ks(prev_ks)
 
 
 def test_conv2d_pair_with_a_dependence_runs_in_order():
