@@ -133,10 +133,10 @@ __device__ __forceinline__ unsigned eidx(int row, int ld, int col) {
   return (unsigned)(row < 0 ? 0 : row) * (unsigned)ld + (unsigned)col;
 }
 // WT: sc1 loads (served past the CU's L1: data another work-group of the launch wrote through)
-template <bool WT = false>
+template <bool WT = false, int R0 = 0, int RN = 16>
 __device__ __forceinline__ void load_rows(const float* base, int ld, const int (&rows)[16], int col, float (&t)[16]) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
+  for (int r = R0; r < R0 + RN; ++r) {
     if constexpr (WT)
       t[r] = __hip_atomic_load(base + eidx(rows[r], ld, col), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else
@@ -203,20 +203,22 @@ __device__ __forceinline__ void store_tile16(float* dst, int ld, long nrows, con
 }
 
 // WT: write-through stores (sc1: the bytes leave the XCD's L2 at once)
-template <bool WT = false>
+// R0, RN: only accumulator rows R0 .. R0 + RN - 1 (the K-split form's halves, halo_body KS = 2)
+template <bool WT = false, int R0 = 0, int RN = 16>
 __device__ __forceinline__ void tile_epilogue(const raft_conv2d_params& p, const int (&rows)[16], int n,
                                               const f32x16& acc) {
+  static_assert(!WT || (R0 == 0 && RN == 16), "write-through epilogues store whole 16-row tiles");
   const bool ncol = n < p.n;
   const int nc = ncol ? n : p.n - 1;  // clamped column for loads
   float v[16];
   const float bias = p.bias ? p.bias[nc] : 0.f;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = acc[r] + bias;
+  for (int r = R0; r < R0 + RN; ++r) v[r] = acc[r] + bias;
   if (p.add0) {
     float t[16];
-    load_rows<WT>(p.add0, p.add0_ld, rows, nc, t);
+    load_rows<WT, R0, RN>(p.add0, p.add0_ld, rows, nc, t);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] += t[r];
+    for (int r = R0; r < R0 + RN; ++r) v[r] += t[r];
   }
   // 1) operand loads, 2) values, 3) stores: destination dst[row * ld + col]
   float* dst = p.out;
@@ -224,55 +226,55 @@ __device__ __forceinline__ void tile_epilogue(const raft_conv2d_params& p, const
   const int epi = p.epilogue;
   if (epi == RAFT_EPI_LINEAR) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] *= p.alpha;
+    for (int r = R0; r < R0 + RN; ++r) v[r] *= p.alpha;
   } else if (epi == RAFT_EPI_RELU) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = fmaxf(v[r], 0.f);
+    for (int r = R0; r < R0 + RN; ++r) v[r] = fmaxf(v[r], 0.f);
   } else if (epi == RAFT_EPI_RESID_RELU) {
     float t[16];
-    load_rows<WT>(p.aux0, p.aux0_ld, rows, nc, t);
+    load_rows<WT, R0, RN>(p.aux0, p.aux0_ld, rows, nc, t);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = fmaxf(t[r] + fmaxf(v[r], 0.f), 0.f);
+    for (int r = R0; r < R0 + RN; ++r) v[r] = fmaxf(t[r] + fmaxf(v[r], 0.f), 0.f);
   } else if (epi == RAFT_EPI_GRU_ZR) {
     if (nc < p.split) {  // a wave's 32 columns lie on one side of split (split % 32 == 0, host-checked)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = sigmoid_bf(v[r]);
+      for (int r = R0; r < R0 + RN; ++r) v[r] = sigmoid_bf(v[r]);
     } else {
       col = nc - p.split;
       float t[16];
-      load_rows<WT>(p.aux0, p.aux0_ld, rows, col, t);
+      load_rows<WT, R0, RN>(p.aux0, p.aux0_ld, rows, col, t);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = sigmoid_bf(v[r]) * t[r];
+      for (int r = R0; r < R0 + RN; ++r) v[r] = sigmoid_bf(v[r]) * t[r];
       dst = p.out1;
       ld = p.out1_ld;
     }
   } else if (epi == RAFT_EPI_GRU_Q) {
     float h[16], z[16];
-    load_rows<WT>(p.aux0, p.aux0_ld, rows, nc, h);
-    load_rows<WT>(p.aux1, p.aux1_ld, rows, nc, z);
+    load_rows<WT, R0, RN>(p.aux0, p.aux0_ld, rows, nc, h);
+    load_rows<WT, R0, RN>(p.aux1, p.aux1_ld, rows, nc, z);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = (1.0f - z[r]) * h[r] + z[r] * tanh_bf(v[r]);
+    for (int r = R0; r < R0 + RN; ++r) v[r] = (1.0f - z[r]) * h[r] + z[r] * tanh_bf(v[r]);
   } else if (epi == RAFT_EPI_TANH_RELU) {
     if (nc < p.split) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = tanh_bf(v[r]);
+      for (int r = R0; r < R0 + RN; ++r) v[r] = tanh_bf(v[r]);
     } else {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = fmaxf(v[r], 0.f);
+      for (int r = R0; r < R0 + RN; ++r) v[r] = fmaxf(v[r], 0.f);
       dst = p.out1;
       ld = p.out1_ld;
       col = n - p.split;
     }
   } else if (epi == RAFT_EPI_ADD_TO_OUT) {
     float t[16];
-    load_rows<WT>(p.out, p.out_ld, rows, nc, t);
+    load_rows<WT, R0, RN>(p.out, p.out_ld, rows, nc, t);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] += t[r];
+    for (int r = R0; r < R0 + RN; ++r) v[r] += t[r];
   }
   if (p.range_flag) {  // f16x3 range guard (raft_hip.h): out-of-range outputs raise the flag
     bool big = false;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) big |= ncol && rows[r] >= 0 && fabsf(v[r]) > RAFT_RANGE_LIMIT;
+    for (int r = R0; r < R0 + RN; ++r) big |= ncol && rows[r] >= 0 && fabsf(v[r]) > RAFT_RANGE_LIMIT;
     if (big) *p.range_flag = 1;
   }
   // write-through outputs: 16-B stores (a 4-B sc1 store is a fabric write of its own); plain
@@ -282,7 +284,7 @@ __device__ __forceinline__ void tile_epilogue(const raft_conv2d_params& p, const
     return;
   }
 #pragma unroll
-  for (int r = 0; r < 16; ++r)
+  for (int r = R0; r < R0 + RN; ++r)
     if (ncol && rows[r] >= 0) {
       if constexpr (WT)
         __hip_atomic_store(dst + eidx(rows[r], ld, col), v[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -258,8 +258,8 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
   constexpr int NRD1 = NSUB * 2 * (X3 ? 2 : 1) + MF * 2 * (X3 ? 2 : 1);  // LDS reads per K-step
   constexpr bool RELAX = HALO_RELAX && SGB > 0 && LSPLIT && !MT && patch_slots(T, U, D, 1) == PA && NRD1 <= 15;
   static_assert(D >= 2 && C::LDS_B + C::LDS_A <= C::LB, "LDS budget");
-  static_assert(KS == 1 || (KS == 2 && !MT && !ENC && LSPLIT && SGB > 0 && MF == 1 && NSUB == 2 && NL == 4 &&
-                            SB % 2 == 0 && 8 * 4096 <= C::LDS_B + C::LDS_A && DW == D && NBI % NWPC == 0 &&
+  static_assert(KS == 1 || (KS == 2 && !MT && !ENC && LSPLIT && SGB > 0 && MF == 1 && NSUB <= 2 && (NL == 4 || NL == 8) &&
+                            SB % 2 == 0 && 8 * 4096 <= C::LDS_B + C::LDS_A && (DW == D || !KSW) && NBI % NWPC == 0 &&
                             NWPC >= 1),
                 "the K-split form: one tile of 32 x 64 blocks on the pre-split path, 4 loaders");
   static_assert(NWP >= 1 && NBI % NWP == 0, "a wave's weight pieces lie in one K-step");
@@ -397,6 +397,9 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
   }
 
   if (loader) {
+#ifdef HALO_LPRIO  // dev builds: the loader waves' issue priority
+    __builtin_amdgcn_s_setprio(HALO_LPRIO);
+#endif
     // ---- loader waves ------------------------------------------------------
     // (the weights of the prologue's load sets 0 .. D-1 are issued by the MFMA
     // waves, which have nothing else to do then: an LDS-DMA costs its issuing
@@ -897,12 +900,55 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
     }
   };
 
-  // KS = 2: the even and odd waves of a block hold partial sums of all 64 columns.  Each keeps one 32-column
-  // half (even: columns 0-31, odd: 32-63), hands the other half to its partner through LDS (the operand rings
-  // are free by now: 4 KiB per wave) and stores its half: the block's epilogue runs on both waves of the SIMD.
-  // The sum even + odd is one fp32 addition per element (commutative: the same bits on either wave).
+  // KS = 2: the even and odd waves of a block hold partial sums of all its outputs.  Each keeps one half (64
+  // columns: even waves columns 0-31, odd 32-63; 32 columns: even waves the block's first tile row, odd the
+  // second), hands the other half to its partner through LDS (the operand rings are free by now: <= 4 KiB per
+  // wave) and stores its half: the block's epilogue runs on both waves of the SIMD.  The sum even + odd is one
+  // fp32 addition per element (commutative: the same bits on either wave).
   auto epilogue_ks2 = [&](const Tile& t) {
-    if constexpr (KS > 1) {
+    if constexpr (KS > 1 && NSUB == 1) {
+      if constexpr (X3 && !SC) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[0][0][r] += accx[0][0][r] * (1.0f / SPLIT_SCALE);
+      }
+      // rows r < 8: the first tile row of the block (m < 16); r >= 8 the second
+      f32x4* mine = reinterpret_cast<f32x4*>(smem + (wc * 2 + kp) * 4096) + lane * 2;
+      const f32x4* theirs = reinterpret_cast<const f32x4*>(smem + (wc * 2 + (kp ^ 1)) * 4096) + lane * 2;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        f32x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = kp ? acc[0][0][4 * q + i] : acc[0][0][8 + 4 * q + i];
+        mine[q ^ (lane & 1)] = v;
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_s_barrier();  // (the loaders join it on their way out)
+      f32x16 keep = acc[0][0];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const f32x4 o = theirs[q ^ (lane & 1)];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (kp)
+            keep[8 + 4 * q + i] += o[i];
+          else
+            keep[4 * q + i] += o[i];
+        }
+      }
+      const int oh = __builtin_amdgcn_readfirstlane(p.out_h), ow = __builtin_amdgcn_readfirstlane(p.out_w);
+      const int rowb = t.b * oh;
+      int rows[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mm = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int y = t.y0 + 2 * wm + (mm >> 4), x = t.x0 + (mm & 15);
+        rows[r] = ((y < oh) & (x < ow)) ? (rowb + y) * ow + x : -1;
+      }
+      if (kp)
+        tile_epilogue<false, 8, 8>(p, rows, t.n0 + cb + m, keep);
+      else
+        tile_epilogue<false, 0, 8>(p, rows, t.n0 + cb + m, keep);
+    } else if constexpr (KS > 1) {
       if constexpr (X3 && !SC) {
 #pragma unroll
         for (int sb = 0; sb < NSUB; ++sb)
@@ -956,8 +1002,8 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
 #pragma unroll
     for (int u = 0; u < DW; ++u) issue_weights_c(u, wpc);
     wait_vm<NWPC * (DW - 2)>();
-  } else if constexpr (KS > 1) {  // the even compute waves issue the prologue pieces of loader wc
-    if (kp == 0) {
+  } else if constexpr (KS > 1) {  // compute wave w issues the prologue pieces of loader w (4 loaders: the even waves)
+    if (NL == 8 || kp == 0) {
 #pragma unroll
       for (int u = 0; u < DW; ++u) issue_weights(u);
       wait_vm<NWP * (DW - 2)>();
@@ -979,7 +1025,14 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
 #ifdef HALO_PRIO
   __builtin_amdgcn_s_setprio(HALO_PRIO);
 #endif
-  first_frags();
+  // SB1 (KS = 2, dev builds -DHALO_KS2_SB1=1): one fragment buffer per compute wave (each K-step's fragments
+  // read at its start; the partner wave's MFMAs cover the LDS round trip), for the 128 VGPRs of 1024-thread
+  // work-groups
+#ifndef HALO_KS2_SB1
+#define HALO_KS2_SB1 0
+#endif
+  constexpr bool SB1 = KS > 1 && HALO_KS2_SB1;
+  if constexpr (!SB1) first_frags();
 #ifdef STAMPS
   unsigned long long t_cmp = 0, t_wait = 0, t_bar = 0, t_epi = 0, t0 = hstamp_now();
   const unsigned long long c_loop = t0;
@@ -1021,7 +1074,17 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
       }
     }
 #pragma unroll
-    for (int e = 0; e < U / KS; ++e) kstep_split(F[(PAR + e + 1) & 1], F[(PAR + e) & 1]);
+    for (int e = 0; e < U / KS; ++e) {
+      if constexpr (SB1) {
+        __builtin_amdgcn_sched_barrier(0);
+        read_b(F[0]);
+        read_a_split(F[0]);
+        mfma_step(F[0]);
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        kstep_split(F[(PAR + e + 1) & 1], F[(PAR + e) & 1]);
+      }
+    }
   };
   // one super-step's K-steps; LAST: the tile's last super-step, which reads nothing ahead
   auto superstep = [&](auto last_tag) {
@@ -1191,6 +1254,12 @@ bool halo_nl8() {
   }
   return v == 8;
 }
+#ifndef HALO_KS2_NL8
+#define HALO_KS2_NL8 0
+#endif
+#ifndef HALO_KS2_BN32  // dev builds: the K-split form for the 32-column update convs too (measured slower: their
+#define HALO_KS2_BN32 0  // 4 K-steps per super-step leave the 4 loaders further behind, profiles/r06b_experiments.txt)
+#endif
 // the K-split form (two compute waves per SIMD, halo_body KS = 2) for the one-tile f16x3 update convs with
 // 64-column tiles (default; RAFT_HALO_KS2=0 or raft_conv2d_set_halo_ks(1): one compute wave per SIMD).
 // Config 2, bench.py interleaved on one box: 144.7 / 143.9 / 144.2 -> 146.9 / 147.0 / 147.0 pairs/s, the
@@ -1239,13 +1308,18 @@ void launch_halo_mt(const HaloLaunch& l, dim3 grid, hipStream_t s) {
     }
   }
   // the K-split form: the one-tile f16x3 update convs with 64-column tiles on the pre-split path
-  constexpr bool CAN_KS2 = CAN_NL8 && BNT == 64 && HaloCfg<KH, KW, BNT, 128, TH>::D == 3 && !HALO_NOLSPLIT;
+  constexpr bool CAN_KS2 = CAN_NL8 && (BNT == 64 || (BNT == 32 && HALO_KS2_BN32)) &&
+                           HaloCfg<KH, KW, BNT, 128, TH>::D == 3 && !HALO_NOLSPLIT;
   if (!NO_MT && l.m > 1) {
     hipLaunchKernelGGL((conv_halo_kernel<KH, KW, BNT, PREC, ENC, TH, !NO_MT>), grid, dim3(512), 0, s, l);
   } else {
     if constexpr (CAN_KS2) {
       if (halo_ks2()) {
+#if HALO_KS2_NL8  // dev builds: 8 loaders beside the 8 compute waves (1024 threads, 128 VGPRs per wave)
+        hipLaunchKernelGGL((conv_halo_kernel<KH, KW, BNT, PREC, ENC, TH, false, 8, 2>), grid, dim3(1024), 0, s, l);
+#else
         hipLaunchKernelGGL((conv_halo_kernel<KH, KW, BNT, PREC, ENC, TH, false, 4, 2>), grid, dim3(768), 0, s, l);
+#endif
         return;
       }
     }
