@@ -570,6 +570,39 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
           }
         }
       };
+#ifdef HALO_ABL_PDMA
+      // TIMING ABLATION (dev builds only, WRONG results): the patches moved by LDS-DMA as they are in
+      // memory (fp32) into the pre-split slots, no register staging and no split -- the bound on what
+      // pre-split activation rows in memory would give the loaders (the update convs only)
+      if constexpr (!ENC) {
+#pragma unroll
+        for (int u = 0; u < D; ++u) {
+          int kt, c;
+          if (set_chunk(u, kt, c)) issue_patch(kt, c);
+        }
+        wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        for (int s = 0; s < NS; ++s) {
+          int nnew = 0;
+          if (s + D < NS) {
+            int kt, c;
+            if (set_chunk(s + D, kt, c)) {
+              issue_patch(kt, c);
+              nnew += pcw;
+            }
+            if constexpr (DW == D) {
+              issue_weights(s + D);
+              nnew += NWP;
+            }
+          }
+          wait_vm_n(s + 1 < NS ? nnew : 0);
+          __builtin_amdgcn_s_barrier();
+        }
+        wait_vm<0>();
+        if constexpr (KS > 1) __builtin_amdgcn_s_barrier();
+        return;
+      }
+#endif
       constexpr int PMAX = (U * D + T - 1) / T + 1;  // chunk starts in the prologue's sets
       Staged pv[PMAX];
       int pks[PMAX], pcs[PMAX];

@@ -693,6 +693,79 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
   };
   f32x16 acc = {}, accx = {}, facc = {}, faccx = {};
   const bool f1w = wv < LC_F1N / 32;  // (wave-uniform)
+#ifndef LC_SGB
+#define LC_SGB 1
+#endif
+  if constexpr (LC_SGB) {
+    // The K stream with its schedule pinned (one scheduling region per K-step): the weight loads of step
+    // j + PF first, then the A fragments of step j + 1 from LDS one per MFMA gap beside step j's MFMAs.  Left
+    // to itself the compiler sank both to just before their use (a vmcnt / lgkmcnt wait per MFMA pair: the L2
+    // round trip of every weight K-step exposed).  Every statement is unconditional so a step is one basic
+    // block: waves 4-7 load convf1's weight addresses of wave 3 and read its A operand without using them.
+    struct AF {
+      h8 ah[2], al[2];
+    };
+    auto read_af = [&](const char* A, AF& f) {
+      const char* row = A + m * 128;
+#pragma unroll
+      for (int qq = 0; qq < 2; ++qq) {
+        f.ah[qq] = *reinterpret_cast<const h8*>(row + (((2 * h + qq) ^ sw) << 4));
+        if constexpr (X3) f.al[qq] = *reinterpret_cast<const h8*>(row + (((4 + 2 * h + qq) ^ sw) << 4));
+      }
+    };
+    auto mfma_af = [&](const AF& f, const h8 (&B)[NT], f32x16& c, f32x16& cx) {
+#pragma unroll
+      for (int qq = 0; qq < 2; ++qq) {
+        if constexpr (BF) {
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8, f.ah[qq]), __builtin_bit_cast(bf8, B[qq]),
+                                                      c, 0, 0, 0);
+        } else {
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah[qq], B[qq], c, 0, 0, 0);
+        }
+        if constexpr (X3) {
+          cx = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah[qq], B[2 + qq], cx, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.al[qq], B[qq], c, 0, 0, 0);
+        }
+      }
+    };
+    auto load_w_any = [&](int j, h8 (&dst)[NT]) {  // (waves 4-7: convf1's steps of wave 3, unused)
+      const int wq = j < LC_KS ? wv : (wv < LC_F1N / 32 ? wv : LC_F1N / 32 - 1);
+      const h8* wf = j < LC_KS ? g.wfrag + ((j * (LC_N / 32) + wq) * 4) * 64
+                               : g.f1frag + (((j - LC_KS) * (LC_F1N / 32) + wq) * 4) * 64;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) dst[t] = wf[t * 64 + lane];
+    };
+    constexpr int NRA = X3 ? 4 : 2, NMA = X3 ? 6 : 2;
+    auto groups = [&](bool loads) {
+      if (loads) __builtin_amdgcn_sched_group_barrier(0x020, NT, 0);  // the weight loads first
+#pragma unroll
+      for (int i = 0; i < NMA; ++i) {
+        if (i < NRA) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+    };
+    AF af[2];
+    read_af(Abase, af[0]);
+#pragma unroll
+    for (int j = 0; j < LC_KS; ++j) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (j + PF < LC_KS + LC_F1KS) load_w_any(j + PF, wb[(j + PF) % (PF + 1)]);
+      read_af(j + 1 < LC_KS ? Abase + (j + 1) * (LC_M * 128) : smem + LC_OFF_A1, af[(j + 1) & 1]);
+      mfma_af(af[j & 1], wb[j % (PF + 1)], acc, accx);
+      groups(j + PF < LC_KS + LC_F1KS);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (f1w) {
+#pragma unroll
+      for (int j = LC_KS; j < LC_KS + LC_F1KS; ++j) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (j + PF < LC_KS + LC_F1KS) load_w_any(j + PF, wb[(j + PF) % (PF + 1)]);
+        if (j + 1 < LC_KS + LC_F1KS) read_af(smem + LC_OFF_A1 + (j + 1 - LC_KS) * (LC_M * 128), af[(j + 1) & 1]);
+        mfma_af(af[j & 1], wb[j % (PF + 1)], facc, faccx);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  } else {
 #pragma unroll
   for (int j = 0; j < LC_KS; ++j) {
     // (the K stream continues into convf1's steps on waves 0-3)
@@ -705,6 +778,7 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
       if (j + PF < LC_KS + LC_F1KS) load_w(j + PF, wb[(j + PF) % (PF + 1)]);
       kstep(smem + LC_OFF_A1 + (j - LC_KS) * (LC_M * 128), wb[j % (PF + 1)], facc, faccx);
     }
+  }
   }
   if constexpr (X3) {
 #pragma unroll
