@@ -658,8 +658,10 @@ __device__ __forceinline__ void halo_body(const HaloArgs* args, int prob, int nt
           // (in the same branch as the patch loads: on every path the compiler sees NWP DMAs behind
           // them, so its own waits for the staged registers stay at vmcnt(NWP), not vmcnt(0))
           if constexpr (DW == D && !KSW) {
+#ifndef HALO_ABL_NOW  // TIMING ABLATION (dev builds only, WRONG results): no weight DMAs after the prologue
             issue_weights(s + D);
             nnew += NWP;
+#endif
           }
         }
         if constexpr (DW > D && !KSW) {
