@@ -518,6 +518,16 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
           const f32x2 hh = __builtin_elementwise_fma(c0, (f32x2){ex, ex}, c1 * (f32x2){xt[k], xt[k]});
           val[iy] = fmaf(sS, hh.x, ty * hh.y);
         }
+#ifndef LC_TAPSGB
+#define LC_TAPSGB 1
+#endif
+#if LC_TAPSGB && LC_TAPS2
+        // the nine y-entries read first, then every tap's corner pairs, then the arithmetic: one LDS round
+        // trip per phase instead of one per tap (the compiler had waited after each tap's reads)
+        __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * RD, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 4 * RD, 0);
+#endif
       }
     } else if (col) {
       unsigned deferred = 0;
