@@ -105,6 +105,10 @@ int raft_corr_build_prec(const float* fmap1, const float* fmap2, int ld, int B, 
  * raft_corr_build_prec (ws_bytes may then be 0).  RAFT_CORR_BUILD4=0: always raft_corr_build_prec.
  * (Argument order since ABI 15: ..., pyramid, ws, ws_bytes, stream.) */
 size_t raft_corr_build_ws_bytes(int B, int H, int W, int C);
+/* The workspace raft_corr_build_ws needs for its 256 x 256 kernel at this shape and precision, or 0 when that
+ * call would take raft_corr_build_prec's kernel (not f16x3, C not a multiple of 16 in [64, 1024], maps past
+ * 2^31 bytes, or RAFT_CORR_BUILD4=0): callers size the workspace from it instead of restating the rule. */
+size_t raft_corr_build_ws_bytes_prec(int B, int H, int W, int C, int precision);
 int raft_corr_build_ws(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C,
                        int num_levels, float sqrt_c, int precision, float* pyramid, void* ws, size_t ws_bytes,
                        raft_stream_t stream);

@@ -78,6 +78,7 @@ _PROTOS = {
     "raft_corr_build": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, P, P]),
     "raft_corr_build_prec": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, P, P]),
     "raft_corr_build_ws_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "raft_corr_build_ws_bytes_prec": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "raft_corr_build_ws": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, P, P, c_size_t, P]),
     "raft_corr_pyramid_level": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "raft_corr_lookup": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, c_int, c_int, P, c_int, P, P]),

@@ -1310,12 +1310,10 @@ bool halo_ks2() {
   return v == 2;
 }
 bool halo_nl8_enc() {
-  static const bool v = [] {
-    // (default on: config 2 +0.1 / +0.3 % in two interleaved pairs on one box, profiles/r05f_experiments.txt)
-    const char* e = getenv("RAFT_HALO_NL8_ENC");
-    return !(e && e[0] == '0');
-  }();
-  return v;
+  // (default on: config 2 +0.1 / +0.3 % in two interleaved pairs on one box, profiles/r05f_experiments.txt;
+  // read per launch so that a test can switch it -- a plan captures the launches it made)
+  const char* e = getenv("RAFT_HALO_NL8_ENC");
+  return !(e && e[0] == '0');
 }
 // the shapes compiled without the multi-tile body (launch_halo_mt): halo_mt_ok never plans m > 1 for
 // them, and the launch refuses m > 1 (the one-tile kernel would run only 1/m of the spatial tiles)

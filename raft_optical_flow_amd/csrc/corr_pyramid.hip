@@ -1377,21 +1377,32 @@ extern "C" size_t raft_corr_build_ws_bytes(int B, int H, int W, int C) {
   return 2 * (size_t)B * H * W * C * 4 + 4096;  // the two split maps + the epilogue sink
 }
 
+namespace raft {
+// whether raft_corr_build_ws takes the 256 x 256 kernel (corr_build4) for this shape: f16x3, C a multiple of
+// 16 with >= 4 half-steps, 32-bit map offsets, RAFT_CORR_BUILD4 not 0 (the operand checks -- ld, alignment,
+// a workspace -- come on top, per call)
+static bool corr_build4_shape(int B, int H, int W, int C, int precision) {
+  const char* e = getenv("RAFT_CORR_BUILD4");
+  if (e && e[0] == '0') return false;
+  return precision == RAFT_PREC_F16X3 && C % 16 == 0 && C >= 64 && C <= 1024 && B > 0 && H > 0 && W > 0 &&
+         (double)B * H * W * C * 4 < 2147483648.0;
+}
+}  // namespace raft
+
+extern "C" size_t raft_corr_build_ws_bytes_prec(int B, int H, int W, int C, int precision) {
+  return raft::corr_build4_shape(B, H, W, C, precision) ? raft_corr_build_ws_bytes(B, H, W, C) : 0;
+}
+
 extern "C" int raft_corr_build_ws(const float* fmap1, const float* fmap2, int ld, int B, int H, int W, int C, int L,
                                   float sqrt_c, int precision, float* pyramid, void* ws, size_t ws_bytes,
                                   raft_stream_t stream) {
   using namespace raft;
-  static const bool on = [] {
-    const char* e = getenv("RAFT_CORR_BUILD4");
-    return !(e && e[0] == '0');
-  }();
   const long P = (long)H * W;
-  // the 256 x 256 kernel: f16x3, C a multiple of 16 with >= 4 half-steps, 32-bit map offsets
-  // (no workspace, or an operand off 16-B alignment: the shape does not fit either, as in ABI 14)
-  const bool fits = precision == RAFT_PREC_F16X3 && C % 16 == 0 && C >= 64 && C <= 1024 && ld % 4 == 0 &&
-                    ld >= C && (double)B * P * C * 4 < 2147483648.0 && ws != nullptr &&
+  // the 256 x 256 kernel where corr_build4_shape says so (raft_corr_build_ws_bytes_prec: its workspace) and
+  // the operands fit it (no workspace, or an operand off 16-B alignment: the other kernel, as in ABI 14)
+  const bool fits = corr_build4_shape(B, H, W, C, precision) && ld % 4 == 0 && ld >= C && ws != nullptr &&
                     (((uintptr_t)fmap1 | (uintptr_t)fmap2 | (uintptr_t)pyramid | (uintptr_t)ws) & 15) == 0;
-  if (!on || !fits) return raft_corr_build_prec(fmap1, fmap2, ld, B, H, W, C, L, sqrt_c, precision, pyramid, stream);
+  if (!fits) return raft_corr_build_prec(fmap1, fmap2, ld, B, H, W, C, L, sqrt_c, precision, pyramid, stream);
   RAFT_REQUIRE(fmap1 && fmap2 && pyramid, "raft_corr_build_ws: null pointer");
   RAFT_REQUIRE(B > 0 && H > 0 && W > 0 && L >= 1 && L <= LK_MAXL, "raft_corr_build_ws: bad sizes");
   RAFT_REQUIRE(ws_bytes >= raft_corr_build_ws_bytes(B, H, W, C), "raft_corr_build_ws: workspace too small "
@@ -1437,7 +1448,8 @@ extern "C" int raft_corr_build_ws(const float* fmap1, const float* fmap2, int ld
   // RAFT_CB4_W4=1: 4-wave work-groups, two per CU (r05p: config 2's map 156 -> 142 us alone, config 4's
   // 1.50 -> 1.54 ms, config 5's 2.47 -> 2.80 ms: the half-size units move 1.5x the operand bytes per
   // flop; the forward unchanged at config 2, 1.5 % slower at config 5), default: 8 waves, one per CU
-  static const bool w4 = [] {
+  // (read per call, like RAFT_CB_ORDER: a test can switch it; a plan captures the launch it made)
+  const bool w4 = [] {
     const char* e = getenv("RAFT_CB4_W4");
     return e && e[0] == '1';
   }();

@@ -598,6 +598,32 @@ def plan_update(L, pu: PackedUpdate, ub: UpdateBuffers, B, h, w, with_mask: bool
                   range_flag=None)
 
 
+def _order_context_branch(L, f0, c0):
+    """Enqueue order of the two encoder branches: L[f0:c0] is the feature network + correlation build
+    (main stream), L[c0:] the context network (side stream).  The streams fix the dependencies; the order
+    only decides which launches the hipGraph executor dispatches first.  RAFT_CTX_ORDER: `late` (the
+    context network enqueued after the whole feature branch), `early` (before it), `mix` (interleaved in
+    proportion, so the context network's small 1/4- and 1/8-res layers run beside the feature network
+    instead of after the correlation build)."""
+    order = os.environ.get("RAFT_CTX_ORDER", "late")
+    if order == "late":
+        return
+    feat, ctx = L[f0:c0], L[c0:]
+    if order == "early":
+        merged = ctx + feat
+    elif order == "mix":
+        merged, j = [], 0
+        for i, l in enumerate(feat):
+            merged.append(l)
+            want = (i + 1) * len(ctx) // len(feat)
+            merged.extend(ctx[j:want])
+            j = max(j, want)
+        merged.extend(ctx[j:])
+    else:
+        raise ValueError(f"RAFT_CTX_ORDER={order!r}: expected late, early or mix")
+    L[f0:] = merged
+
+
 # ----------------------------------------------------------------------------
 # The whole forward
 # ----------------------------------------------------------------------------
@@ -664,9 +690,9 @@ class RaftPlan:
             cprec = _lib.PREC_FP32 if pk.precision == _lib.PREC_FP32 else _lib.PREC_F16X3
             # (f16x3: fmaps split once into the workspace, the volume on 256 x 256 tiles: raft_hip.h)
             # (the workspace only where the library takes that path: raft_corr_build_ws)
-            fits4 = (cprec == _lib.PREC_F16X3 and C % 16 == 0 and 64 <= C <= 1024 and B * h * w * C * 4 < 2 ** 31
-                     and os.environ.get("RAFT_CORR_BUILD4", "1") != "0")
-            wsb = int(_lib.load().raft_corr_build_ws_bytes(B, h, w, C)) if fits4 else 0
+            # (the library's own rule: raft_corr_build_ws_bytes_prec is 0 where that kernel does not apply)
+            wsb = int(_lib.load().raft_corr_build_ws_bytes_prec(B, h, w, C, cprec))
+            fits4 = wsb > 0
             self.corr_ws = A.flat((wsb + 3) // 4) if fits4 else None
             L.append(Launch("raft_corr_build_ws", fmap1.data_ptr(), fmap2.data_ptr(), C, B, h, w, C, lv, div,
                             cprec, self.pyramid.data_ptr(), self.corr_ws.data_ptr() if fits4 else None, wsb))
@@ -695,6 +721,7 @@ class RaftPlan:
             for l in L[n_ctx:]:
                 if isinstance(l, Launch):  # FORK / JOIN markers are plain strings
                     l.side = True
+            _order_context_branch(L, L.index(K.FORK) + 1, n_ctx)
             L.append(K.JOIN)
         L.append(Launch("raft_init_coords", ub.coords.data_ptr(),
                         self.flow_init.data_ptr() if self.flow_init is not None else None, B, h, w))

@@ -170,3 +170,17 @@ def test_stats_slots_host_side():
     s, hw = slots(96, 128, 3, 2, 3, 9, 11)             # 30 output rows per image: one tile each
     assert s == 2
     assert slots(64, 96, 3, 2, 2, 220, 512, epilogue=_lib.EPI_RELU)[0] == 0
+
+
+def test_corr_build_ws_bytes_prec_host_side():
+    """raft_corr_build_ws_bytes_prec (host logic only): the 256 x 256 correlation build's workspace where
+    raft_corr_build_ws takes that kernel (f16x3, C % 16 == 0, 64 <= C <= 1024), 0 where it falls back."""
+    from raft_optical_flow_amd import _lib
+    lib = _lib.load()
+    full = lib.raft_corr_build_ws_bytes(1, 55, 128, 256)
+    assert full > 0
+    assert lib.raft_corr_build_ws_bytes_prec(1, 55, 128, 256, _lib.PREC_F16X3) == full
+    for prec in (_lib.PREC_FP32, _lib.PREC_F16, _lib.PREC_BF16):
+        assert lib.raft_corr_build_ws_bytes_prec(1, 55, 128, 256, prec) == 0
+    assert lib.raft_corr_build_ws_bytes_prec(1, 55, 128, 72, _lib.PREC_F16X3) == 0
+    assert lib.raft_corr_build_ws_bytes_prec(1, 55, 128, 48, _lib.PREC_F16X3) == 0

@@ -143,3 +143,31 @@ def test_corr_build_ws_without_workspace_falls_back():
               out2.data_ptr(), ws.data_ptr() + 4, wsb, K.stream_handle())
     torch.cuda.synchronize()
     assert torch.equal(out2, ref)
+
+
+@pytest.mark.parametrize("B,H,W,C,L", [(1, 55, 128, 256, 4), (2, 37, 53, 256, 2), (3, 9, 70, 64, 1)])
+def test_corr_build_w4_equals_default(monkeypatch, B, H, W, C, L):
+    """The opt-in 4-wave correlation build (RAFT_CB4_W4=1: two work-groups per CU, 256 targets x 128 queries
+    per unit, level 2 pooled in registers where L > 2) writes the same pyramid as the default 8-wave build
+    bit for bit (each query's sums run the same K walk), for L = 1, 2 and 4."""
+    g = torch.Generator(device=DEV).manual_seed(B * 100 + L)
+    f = torch.randn(2 * B * H * W, C, device=DEV, generator=g)
+    f1, f2 = f[: B * H * W], f[B * H * W:]
+    monkeypatch.delenv("RAFT_CB4_W4", raising=False)
+    ref = _build_ws(f1, f2, C, B, H, W, C, L, pad=0.0)
+    monkeypatch.setenv("RAFT_CB4_W4", "1")
+    got = _build_ws(f1, f2, C, B, H, W, C, L, pad=0.0)
+    assert torch.equal(got, ref)
+
+
+def test_corr_build_ws_bytes_prec_is_the_librarys_rule(monkeypatch):
+    """raft_corr_build_ws_bytes_prec: the workspace where raft_corr_build_ws takes the 256 x 256 kernel, 0 where
+    it falls back (so callers do not restate the rule)."""
+    from raft_optical_flow_amd import _lib
+    lib = _lib.load()
+    assert lib.raft_corr_build_ws_bytes_prec(1, 55, 128, 256, _lib.PREC_F16X3) == lib.raft_corr_build_ws_bytes(1, 55, 128, 256)
+    assert lib.raft_corr_build_ws_bytes_prec(1, 55, 128, 256, _lib.PREC_FP32) == 0
+    assert lib.raft_corr_build_ws_bytes_prec(1, 55, 128, 72, _lib.PREC_F16X3) == 0     # C % 16
+    assert lib.raft_corr_build_ws_bytes_prec(1, 55, 128, 48, _lib.PREC_F16X3) == 0     # C < 64
+    monkeypatch.setenv("RAFT_CORR_BUILD4", "0")
+    assert lib.raft_corr_build_ws_bytes_prec(1, 55, 128, 256, _lib.PREC_F16X3) == 0

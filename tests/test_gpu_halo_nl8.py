@@ -69,3 +69,46 @@ def test_eight_loaders_forward(loaders):
             outs.append(m(i1, i2, iters=12, test_mode=True)[1])
         torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("cin,cout,B,H,W,in_norm", [(64, 64, 2, 61, 131, True), (64, 64, 2, 61, 131, False),
+                                                    (96, 96, 2, 30, 70, True), (64, 64, 1, 9, 20, True)])
+def test_encoder_eight_loaders_equal_four(monkeypatch, cin, cout, B, H, W, in_norm):
+    """The encoders' 3x3 convs with 8 loader waves (default) and 4 (RAFT_HALO_NL8_ENC=0) -- with the loaders'
+    input InstanceNorm and the epilogue's statistics partials, on multi-tile (several rounds) and one-tile grids
+    -- give the same outputs and the same statistics bit for bit."""
+    import ctypes
+    from raft_optical_flow_amd import _lib
+    from raft_optical_flow_amd import kernels as K
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(cin + H + W)
+    x = torch.randn(B, cin, H, W, generator=g) * 2.0 + 0.5
+    w = torch.randn(cout, cin, 3, 3, generator=g) / np.sqrt(cin * 9)
+    b = torch.randn(cout, generator=g) * 0.1
+    pc = K.pack_conv(w, b, 1, 1, device=DEV)
+    pc.precision = _lib.PREC_F16X3
+    src = K.Rows(K.nchw_to_rows(x.to(DEV)))
+    mean = x.double().mean((2, 3))
+    rstd = 1.0 / torch.sqrt(x.double().var((2, 3), unbiased=False) + 1e-5)
+    st = torch.stack([mean, rstd], -1).float().contiguous().to(DEV)
+
+    def run():
+        out = K.Rows(torch.full((B * H * W, cout), 7.0, device=DEV))
+        p = K.conv_params(pc, src, B, H, W, out)
+        if in_norm:
+            p.in_norm, p.in_norm_relu = st.data_ptr(), 1
+            assert lib.raft_conv2d_in_norm_ok(ctypes.byref(p)) == 1
+        slots = int(lib.raft_conv2d_stats_slots(ctypes.byref(p)))
+        assert slots > 0
+        part = torch.full((B * slots * cout * 4,), float("nan"), device=DEV)
+        p.stats_part, p.stats_ld = part.data_ptr(), cout
+        K.conv_launch(p)(K.stream_handle())
+        torch.cuda.synchronize()
+        return out.t.clone(), part.clone()
+
+    monkeypatch.delenv("RAFT_HALO_NL8_ENC", raising=False)
+    a_out, a_st = run()
+    monkeypatch.setenv("RAFT_HALO_NL8_ENC", "0")
+    b_out, b_st = run()
+    assert torch.equal(a_out, b_out)
+    assert torch.equal(a_st, b_st)
