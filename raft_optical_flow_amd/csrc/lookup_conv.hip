@@ -501,6 +501,51 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
         const char* p0 = reinterpret_cast<const char*>(&patch[pidx<4>(0, xwk, l)]);
         const char* p1 = reinterpret_cast<const char*>(&patch[pidx<4>(0, xwk + 1, l)]);
         auto at = [](const char* bp, int byte) { return *reinterpret_cast<const float*>(bp + byte); };
+#ifndef LC_TAPS3
+#define LC_TAPS3 1
+#endif
+#if LC_TAPS3 && LC_TAPS2
+        // The nine y-entries first.  Where every lane's nine rows are consecutive (the common case: the float
+        // round trip moved no floor), tap iy's lower row is tap iy + 1's upper row: the lane reads its two
+        // columns once, RD + 1 rows each (10 LDS reads of two rows, 4 * RS bytes apart, instead of 18), and
+        // each tap takes its four corners from registers -- the same values, the same arithmetic.
+        int ro[RD];
+        float tyv[RD];
+        bool cons = true;
+#pragma unroll
+        for (int iy = 0; iy < RD; ++iy) {
+          const int2 ye = *reinterpret_cast<const int2*>(&yt[l * RD + iy]);
+          ro[iy] = ye.x;
+          tyv[iy] = __int_as_float(ye.y);
+        }
+#pragma unroll
+        for (int iy = 1; iy < RD; ++iy) cons &= ro[iy] == ro[0] + iy * (4 * RS);  // (one row: 4 * RS bytes)
+        if (__all(cons)) {
+          const char* q0 = p0 + ro[0];
+          const char* q1 = p1 + ro[0];
+          float a0[RD + 1], a1[RD + 1];
+#pragma unroll
+          for (int r = 0; r <= RD; ++r) {
+            a0[r] = at(q0, r * (4 * RS));
+            a1[r] = at(q1, r * (4 * RS));
+          }
+#pragma unroll
+          for (int iy = 0; iy < RD; ++iy) {
+            const float ty = tyv[iy], sS = 1.0f - ty;
+            const f32x2 c0 = {a0[iy], a0[iy + 1]}, c1 = {a1[iy], a1[iy + 1]};
+            const f32x2 hh = __builtin_elementwise_fma(c0, (f32x2){ex, ex}, c1 * (f32x2){xt[k], xt[k]});
+            val[iy] = fmaf(sS, hh.x, ty * hh.y);
+          }
+        } else {
+#pragma unroll
+          for (int iy = 0; iy < RD; ++iy) {
+            const float ty = tyv[iy], sS = 1.0f - ty;
+            const f32x2 c0 = {at(p0, ro[iy]), at(p0, ro[iy] + 4 * RS)}, c1 = {at(p1, ro[iy]), at(p1, ro[iy] + 4 * RS)};
+            const f32x2 hh = __builtin_elementwise_fma(c0, (f32x2){ex, ex}, c1 * (f32x2){xt[k], xt[k]});
+            val[iy] = fmaf(sS, hh.x, ty * hh.y);
+          }
+        }
+#else
 #pragma unroll
         for (int iy = 0; iy < RD; ++iy) {
 #if LC_TAPS2
@@ -528,6 +573,7 @@ __global__ __launch_bounds__(512) void lookup_conv_kernel(LookupConvArgs g) {
         __builtin_amdgcn_sched_group_barrier(0x100, 2 * RD, 0);
         __builtin_amdgcn_sched_group_barrier(0x002, 4 * RD, 0);
 #endif
+#endif  // LC_TAPS3
       }
     } else if (col) {
       unsigned deferred = 0;
